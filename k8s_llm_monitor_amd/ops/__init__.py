@@ -1,0 +1,271 @@
+"""Fused operators.  GPU tensors run the gfx950 HIP kernels of ``_k8sllm_ops`` (built in-tree by
+``python -m k8s_llm_monitor_amd.ops.build``); CPU tensors run the fp32 references of
+:mod:`.reference`.  A GPU tensor never silently falls back: if the extension is missing on a
+GPU box the call raises, so tests and benchmarks always exercise the native kernels.
+"""
+from __future__ import annotations
+
+import importlib
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_EXT = None
+_EXT_ERR: Optional[BaseException] = None
+
+
+def native():
+    """The compiled extension module (raises with the build hint if unavailable)."""
+    global _EXT, _EXT_ERR
+    if _EXT is None and _EXT_ERR is None:
+        try:
+            _EXT = importlib.import_module("k8s_llm_monitor_amd.ops._k8sllm_ops")
+        except BaseException as e:  # noqa: BLE001 - remember why, re-raise on GPU use
+            _EXT_ERR = e
+    if _EXT is None:
+        raise RuntimeError(
+            "gfx950 kernels (_k8sllm_ops) are not built/loadable; run "
+            "`python -m k8s_llm_monitor_amd.ops.build` (cause: %r)" % (_EXT_ERR,))
+    return _EXT
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ---------------------------------------------------------------- norms / activations
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        r = ref.rms_norm(x, w, eps)
+        return out.copy_(r) if out is not None else r
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    native().rms_norm(out, x, w, eps)
+    return out
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """residual <- x + residual (bf16); returns rms_norm(residual) * w."""
+    if not _gpu(x):
+        y, s = ref.fused_add_rms_norm(x, residual, w, eps)
+        residual.copy_(s)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    native().fused_add_rms_norm(out, x, residual, w, eps)
+    return out
+
+
+def layer_norm(x, w, b, eps):
+    if not _gpu(x):
+        return ref.layer_norm(x, w, b, eps)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    native().layer_norm(out, x, w, b, eps)
+    return out
+
+
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.silu_mul(x)
+    if out is None:
+        out = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
+    native().silu_mul(out, x)
+    return out
+
+
+def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.gelu_tanh(x)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    native().gelu_tanh(out, x)
+    return out
+
+
+def embedding(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int = 0,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(weight):
+        return ref.embedding(ids, weight, vocab_start)
+    if out is None:
+        out = torch.empty(ids.numel(), weight.shape[1], dtype=weight.dtype, device=weight.device)
+    native().embedding(out, ids, weight, vocab_start)
+    return out
+
+
+# ---------------------------------------------------------------- attention
+
+def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                   k_cache: Optional[torch.Tensor], v_cache: Optional[torch.Tensor],
+                   slot_mapping: Optional[torch.Tensor], Hq: int, Hkv: int, D: int,
+                   apply_rope: bool = True) -> None:
+    """In place: rotate q and k inside the fused QKV rows; write k, v into the paged cache."""
+    if not _gpu(qkv):
+        ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, Hq, Hkv, D, apply_rope)
+        return
+    empty = _empty_i32(qkv.device)
+    native().rope_and_cache(qkv, positions, cos_sin,
+                            k_cache if k_cache is not None else empty,
+                            v_cache if v_cache is not None else empty,
+                            slot_mapping if slot_mapping is not None else empty,
+                            Hq, Hkv, D, apply_rope)
+
+
+_EMPTY = {}
+
+
+def _empty_i32(device) -> torch.Tensor:
+    t = _EMPTY.get(device)
+    if t is None:
+        t = _EMPTY[device] = torch.empty(0, dtype=torch.int32, device=device)
+    return t
+
+
+PARTITION = 256  # tokens per decode partition (must match paged_decode.hip kPT)
+
+
+def decode_workspace(max_batch: int, Hq: int, D: int, max_model_len: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    np_ = max(1, (max_model_len + PARTITION - 1) // PARTITION)
+    part_out = torch.empty(max_batch, Hq, np_, D, dtype=torch.float32, device=device)
+    part_ml = torch.empty(max_batch, Hq, np_, 2, dtype=torch.float32, device=device)
+    return part_out, part_ml
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                 seq_lens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
+                 workspace: Optional[tuple] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(q):
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale)
+        return out.copy_(r) if out is not None else r
+    B = seq_lens.shape[0]
+    if workspace is None:
+        workspace = decode_workspace(B, Hq, D, block_tables.shape[1] * k_cache.shape[3], q.device)
+    if out is None:
+        out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
+    native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, workspace[0], workspace[1],
+                          Hq, Hkv, D, scale)
+    return out
+
+
+def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128) -> tuple[list[int], list[int]]:
+    """Q-block schedule for flash_prefill: (seq index, first q row) per 128-row block, heaviest
+    (largest first row, i.e. longest causal span) first so the tail of the grid is short."""
+    items = []
+    for i in range(len(cu_seqlens_cpu) - 1):
+        n = cu_seqlens_cpu[i + 1] - cu_seqlens_cpu[i]
+        for s in range(0, n, block):
+            items.append((s, i))
+    items.sort(key=lambda t: -t[0])
+    return [i for _, i in items], [s for s, _ in items]
+
+
+def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
+                  qblocks: Optional[tuple[torch.Tensor, torch.Tensor]] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(qkv):
+        return ref.flash_prefill(qkv, cu_seqlens, Hq, Hkv, D, scale)
+    if qblocks is None:
+        qs, st = prefill_qblocks(cu_seqlens.tolist())
+        qblocks = (torch.tensor(qs, dtype=torch.int32, device=qkv.device),
+                   torch.tensor(st, dtype=torch.int32, device=qkv.device))
+    if out is None:
+        out = torch.empty(qkv.shape[0], Hq * D, dtype=qkv.dtype, device=qkv.device)
+    native().flash_prefill(out, qkv, cu_seqlens, qblocks[0], qblocks[1], Hq, Hkv, D, scale)
+    return out
+
+
+# ---------------------------------------------------------------- sampling
+
+def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None, top_k: Optional[torch.Tensor] = None,
+           top_p: Optional[torch.Tensor] = None, rng: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Next tokens [B] int32.  temperature <= 0 (or None) is greedy."""
+    if not _gpu(logits):
+        return _sample_cpu(logits, temperature, top_k, top_p, rng)
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+    native().sample(out, logits, temperature, top_k, top_p, rng)
+    return out
+
+
+def _sample_cpu(logits, temperature, top_k, top_p, rng):
+    B = logits.shape[0]
+    res = torch.empty(B, dtype=torch.int32)
+    gen = torch.Generator().manual_seed(int(rng[0]) * 1000003 + int(rng[1])) if rng is not None else None
+    for b in range(B):
+        t = float(temperature[b]) if temperature is not None else 0.0
+        x = logits[b].float()
+        if t <= 0:
+            res[b] = int(x.argmax())
+            continue
+        x = x / t
+        if top_k is not None and 0 < int(top_k[b]) < x.numel():
+            kth = torch.topk(x, int(top_k[b])).values[-1]
+            x = x.masked_fill(x < kth, float("-inf"))
+        if top_p is not None and float(top_p[b]) < 1.0:
+            p = torch.softmax(x, -1)
+            sp, si = torch.sort(p, descending=True)
+            keep = torch.cumsum(sp, 0) - sp < float(top_p[b])
+            mask = torch.zeros_like(p, dtype=torch.bool)
+            mask[si[keep]] = True
+            x = x.masked_fill(~mask, float("-inf"))
+        res[b] = int(torch.multinomial(torch.softmax(x, -1), 1, generator=gen))
+    return res
+
+
+# ---------------------------------------------------------------- mixture of experts
+
+def moe_route(router_logits: torch.Tensor, k: int, renorm: bool = True):
+    if not _gpu(router_logits):
+        return ref.moe_route(router_logits, k, renorm)
+    T = router_logits.shape[0]
+    lf = router_logits.float().contiguous()
+    ids = torch.empty(T, k, dtype=torch.int32, device=lf.device)
+    w = torch.empty(T, k, dtype=torch.float32, device=lf.device)
+    native().moe_route(lf, ids, w, renorm)
+    return ids, w
+
+
+def moe_align(ids: torch.Tensor, E: int):
+    if not _gpu(ids) or E > 16:
+        return ref.moe_align(ids, E)
+    n = ids.numel()
+    offsets = torch.empty(E + 1, dtype=torch.int32, device=ids.device)
+    sorted_idx = torch.empty(n, dtype=torch.int32, device=ids.device)
+    inv_idx = torch.empty(n, dtype=torch.int32, device=ids.device)
+    native().moe_align(ids.contiguous(), E, offsets, sorted_idx, inv_idx)
+    return offsets, sorted_idx, inv_idx
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor, div: int = 1) -> torch.Tensor:
+    if not _gpu(x):
+        return x[(idx.long() // div)]
+    out = torch.empty(idx.numel(), x.shape[1], dtype=x.dtype, device=x.device)
+    native().gather_rows(out, x.contiguous(), idx, div)
+    return out
+
+
+def moe_combine(y: torch.Tensor, inv_idx: torch.Tensor, w: torch.Tensor, T: int) -> torch.Tensor:
+    if not _gpu(y):
+        return ref.moe_combine(y, inv_idx, w, T)
+    out = torch.empty(T, y.shape[1], dtype=y.dtype, device=y.device)
+    native().moe_combine(out, y.contiguous(), inv_idx, w.contiguous())
+    return out
+
+
+def softmax_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)

@@ -1,0 +1,235 @@
+// PyTorch bindings for the gfx950 kernels.  The kernels themselves are plain HIP compiled by
+// hipcc (no torch headers); this translation unit validates tensors, picks the current HIP
+// stream (so every op is hipGraph-capturable) and calls the C launchers.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int k8sllm_rmsnorm(void* out, const void* x, void* residual, const void* w, long rows, int d, float eps,
+                   long x_stride, long out_stride, hipStream_t s);
+int k8sllm_layernorm(void* out, const void* x, const void* w, const void* b, long rows, int d, float eps,
+                     hipStream_t s);
+int k8sllm_silu_mul(void* out, const void* x, long rows, int F, hipStream_t s);
+int k8sllm_gelu_tanh(void* out, const void* x, long n, hipStream_t s);
+int k8sllm_embedding(void* out, const int* ids, const void* weight, long T, int d, int vocab_start, int rows,
+                     hipStream_t s);
+int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, void* k_cache,
+                      void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D, int block_size,
+                      int apply_rope, hipStream_t s);
+int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q, long q_stride,
+                        const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
+                        const int* seq_lens, int B, int Hq, int Hkv, int D, int NP, float scale, hipStream_t s);
+int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride, const int* cu_seqlens,
+                         const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
+                         hipStream_t s);
+int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V, const float* temps,
+                  const int* top_k, const float* top_p, const int64_t* rng, hipStream_t s);
+int k8sllm_moe_route(const void* logits, long T, int E, int K, int renorm, int* topk_ids, float* topk_w,
+                     hipStream_t s);
+int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, int* sorted_idx, int* inv_idx,
+                     hipStream_t s);
+int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
+                       int d, hipStream_t s);
+int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "k8sllm kernel launch failed: ", what, " rc=", rc); }
+
+void dev_bf16(const torch::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, n, " must be bfloat16");
+}
+
+void dev_i32(const torch::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kInt32, n, " must be int32");
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+}
+
+void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
+  dev_bf16(out, "out"); dev_bf16(x, "x"); dev_bf16(w, "w");
+  const int d = (int)x.size(-1);
+  TORCH_CHECK(x.stride(-1) == 1 && out.stride(-1) == 1 && w.is_contiguous(), "rms_norm: inner dim must be contiguous");
+  const long rows = x.numel() / d;
+  const long xs = x.dim() > 1 ? x.stride(-2) : d, os = out.dim() > 1 ? out.stride(-2) : d;
+  check(k8sllm_rmsnorm(out.data_ptr(), x.data_ptr(), nullptr, w.data_ptr(), rows, d, (float)eps, xs, os, cur()),
+        "rms_norm");
+}
+
+void fused_add_rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor residual, torch::Tensor w, double eps) {
+  dev_bf16(out, "out"); dev_bf16(x, "x"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
+  TORCH_CHECK(residual.is_contiguous() && w.is_contiguous() && x.stride(-1) == 1, "fused_add_rms_norm layout");
+  const int d = (int)x.size(-1);
+  const long rows = x.numel() / d;
+  TORCH_CHECK(residual.numel() == rows * d, "residual shape");
+  const long xs = x.dim() > 1 ? x.stride(-2) : d, os = out.dim() > 1 ? out.stride(-2) : d;
+  check(k8sllm_rmsnorm(out.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(), rows, d, (float)eps, xs, os,
+                       cur()),
+        "fused_add_rms_norm");
+}
+
+void layer_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps) {
+  dev_bf16(out, "out"); dev_bf16(x, "x"); dev_bf16(w, "w"); dev_bf16(b, "b");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "layer_norm: contiguous");
+  const int d = (int)x.size(-1);
+  check(k8sllm_layernorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(), x.numel() / d, d, (float)eps, cur()),
+        "layer_norm");
+}
+
+void silu_mul(torch::Tensor out, torch::Tensor x) {
+  dev_bf16(out, "out"); dev_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "silu_mul: contiguous");
+  const int F = (int)out.size(-1);
+  TORCH_CHECK(x.size(-1) == 2 * F, "silu_mul: x last dim must be 2*F");
+  check(k8sllm_silu_mul(out.data_ptr(), x.data_ptr(), out.numel() / F, F, cur()), "silu_mul");
+}
+
+void gelu_tanh(torch::Tensor out, torch::Tensor x) {
+  dev_bf16(out, "out"); dev_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel(), "gelu: shape");
+  check(k8sllm_gelu_tanh(out.data_ptr(), x.data_ptr(), x.numel(), cur()), "gelu_tanh");
+}
+
+void embedding(torch::Tensor out, torch::Tensor ids, torch::Tensor weight, int64_t vocab_start) {
+  dev_bf16(out, "out"); dev_bf16(weight, "weight"); dev_i32(ids, "ids");
+  TORCH_CHECK(weight.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
+  const int d = (int)weight.size(1);
+  check(k8sllm_embedding(out.data_ptr(), ids.data_ptr<int>(), weight.data_ptr(), ids.numel(), d, (int)vocab_start,
+                         (int)weight.size(0), cur()),
+        "embedding");
+}
+
+void rope_and_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, torch::Tensor k_cache,
+                    torch::Tensor v_cache, torch::Tensor slot_mapping, int64_t Hq, int64_t Hkv, int64_t D,
+                    bool apply_rope) {
+  dev_bf16(qkv, "qkv"); dev_i32(positions, "positions");
+  TORCH_CHECK(qkv.stride(-1) == 1 && qkv.dim() == 2, "qkv must be [T, (Hq+2Hkv)*D] with unit inner stride");
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv width");
+  TORCH_CHECK(cos_sin.scalar_type() == torch::kFloat32 && cos_sin.is_contiguous() && cos_sin.size(1) == D, "cos_sin");
+  const bool has_cache = slot_mapping.numel() > 0;
+  int block_size = 16;
+  if (has_cache) {
+    dev_i32(slot_mapping, "slot_mapping");
+    dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
+    // k_cache [NB, Hkv, D/8, BS, 8], v_cache [NB, Hkv, D, BS]
+    TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == Hkv && k_cache.size(4) == 8, "k_cache layout");
+    TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == Hkv && v_cache.size(2) == D, "v_cache layout");
+    block_size = (int)k_cache.size(3);
+  }
+  check(k8sllm_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                          has_cache ? k_cache.data_ptr() : nullptr, has_cache ? v_cache.data_ptr() : nullptr,
+                          has_cache ? slot_mapping.data_ptr<int>() : nullptr, qkv.size(0), (int)Hq, (int)Hkv, (int)D,
+                          block_size, apply_rope ? 1 : 0, cur()),
+        "rope_and_cache");
+}
+
+void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                  torch::Tensor block_tables, torch::Tensor seq_lens, torch::Tensor part_out, torch::Tensor part_ml,
+                  int64_t Hq, int64_t Hkv, int64_t D, double scale) {
+  dev_bf16(out, "out"); dev_bf16(q, "q"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
+  dev_i32(block_tables, "block_tables"); dev_i32(seq_lens, "seq_lens");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "q must be [B, >=Hq*D] rows");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [B, Hq*D]");
+  TORCH_CHECK(k_cache.size(3) == 16 && v_cache.size(3) == 16, "paged_decode expects block_size 16");
+  TORCH_CHECK(part_out.scalar_type() == torch::kFloat32 && part_ml.scalar_type() == torch::kFloat32, "partials fp32");
+  const int B = (int)seq_lens.size(0);
+  const int NP = (int)part_out.size(2);
+  TORCH_CHECK(part_out.size(0) >= B && part_out.size(1) == Hq && part_out.size(3) == D, "part_out shape");
+  TORCH_CHECK(NP * 256 >= block_tables.size(1) * 16, "too few partitions for the block table width");
+  check(k8sllm_paged_decode(out.data_ptr(), out.stride(0), part_out.data_ptr<float>(), part_ml.data_ptr<float>(),
+                            q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                            block_tables.data_ptr<int>(), (int)block_tables.stride(0), seq_lens.data_ptr<int>(), B,
+                            (int)Hq, (int)Hkv, (int)D, NP, (float)scale, cur()),
+        "paged_decode");
+}
+
+void flash_prefill(torch::Tensor out, torch::Tensor qkv, torch::Tensor cu_seqlens, torch::Tensor qb_seq,
+                   torch::Tensor qb_start, int64_t Hq, int64_t Hkv, int64_t D, double scale) {
+  dev_bf16(out, "out"); dev_bf16(qkv, "qkv");
+  dev_i32(cu_seqlens, "cu_seqlens"); dev_i32(qb_seq, "qb_seq"); dev_i32(qb_start, "qb_start");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv rows");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [T, Hq*D]");
+  check(k8sllm_flash_prefill(out.data_ptr(), out.stride(0), qkv.data_ptr(), qkv.stride(0), cu_seqlens.data_ptr<int>(),
+                             qb_seq.data_ptr<int>(), qb_start.data_ptr<int>(), (int)qb_seq.numel(), (int)Hq, (int)Hkv,
+                             (int)D, (float)scale, cur()),
+        "flash_prefill");
+}
+
+void sample(torch::Tensor out, torch::Tensor logits, c10::optional<torch::Tensor> temps,
+            c10::optional<torch::Tensor> top_k, c10::optional<torch::Tensor> top_p, c10::optional<torch::Tensor> rng) {
+  dev_i32(out, "out");
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
+  const bool f32 = logits.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(f32 || logits.scalar_type() == torch::kBFloat16, "logits must be fp32 or bf16");
+  const float* t = temps && temps->numel() ? temps->data_ptr<float>() : nullptr;
+  const int* k = top_k && top_k->numel() ? top_k->data_ptr<int>() : nullptr;
+  const float* p = top_p && top_p->numel() ? top_p->data_ptr<float>() : nullptr;
+  const int64_t* r = rng && rng->numel() ? rng->data_ptr<int64_t>() : nullptr;
+  check(k8sllm_sample(out.data_ptr<int>(), logits.data_ptr(), f32 ? 1 : 0, logits.size(0), logits.stride(0),
+                      (int)logits.size(1), t, k, p, r, cur()),
+        "sample");
+}
+
+void moe_route(torch::Tensor logits, torch::Tensor topk_ids, torch::Tensor topk_w, bool renorm) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous(), "router logits");
+  TORCH_CHECK(logits.scalar_type() == torch::kFloat32, "router logits must be fp32");
+  dev_i32(topk_ids, "topk_ids");
+  const int E = (int)logits.size(1);
+  const int K = (int)topk_ids.size(1);
+  TORCH_CHECK(E <= 64 && K <= E, "moe_route supports up to 64 experts");
+  check(k8sllm_moe_route(logits.data_ptr(), logits.size(0), E, K, renorm ? 1 : 0, topk_ids.data_ptr<int>(),
+                         topk_w.data_ptr<float>(), cur()),
+        "moe_route");
+}
+
+void moe_align(torch::Tensor topk_ids, int64_t E, torch::Tensor expert_offsets, torch::Tensor sorted_idx,
+               torch::Tensor inv_idx) {
+  dev_i32(topk_ids, "topk_ids"); dev_i32(expert_offsets, "expert_offsets");
+  dev_i32(sorted_idx, "sorted_idx"); dev_i32(inv_idx, "inv_idx");
+  TORCH_CHECK(expert_offsets.numel() == E + 1, "expert_offsets size");
+  check(k8sllm_moe_align(topk_ids.data_ptr<int>(), topk_ids.numel(), (int)E, expert_offsets.data_ptr<int>(),
+                         sorted_idx.data_ptr<int>(), inv_idx.data_ptr<int>(), cur()),
+        "moe_align");
+}
+
+void moe_combine(torch::Tensor out, torch::Tensor expert_out, torch::Tensor inv_idx, torch::Tensor topk_w) {
+  dev_bf16(out, "out"); dev_bf16(expert_out, "expert_out"); dev_i32(inv_idx, "inv_idx");
+  TORCH_CHECK(out.is_contiguous() && expert_out.is_contiguous(), "moe_combine contiguous");
+  const int d = (int)out.size(1);
+  check(k8sllm_moe_combine(out.data_ptr(), expert_out.data_ptr(), inv_idx.data_ptr<int>(), topk_w.data_ptr<float>(),
+                           out.size(0), (int)topk_w.size(1), d, cur()),
+        "moe_combine");
+}
+
+void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t div) {
+  dev_bf16(out, "out"); dev_bf16(x, "x"); dev_i32(idx, "idx");
+  TORCH_CHECK(out.is_contiguous() && x.is_contiguous(), "gather_rows contiguous");
+  check(k8sllm_gather_rows(out.data_ptr(), x.data_ptr(), idx.data_ptr<int>(), idx.numel(), (int)x.size(1), (int)div,
+                           cur()),
+        "gather_rows");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_k8sllm_ops, m) {
+  m.doc() = "gfx950 HIP kernels for k8s-llm-monitor-amd";
+  m.def("rms_norm", &rms_norm);
+  m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("layer_norm", &layer_norm);
+  m.def("silu_mul", &silu_mul);
+  m.def("gelu_tanh", &gelu_tanh);
+  m.def("embedding", &embedding);
+  m.def("rope_and_cache", &rope_and_cache);
+  m.def("paged_decode", &paged_decode);
+  m.def("flash_prefill", &flash_prefill);
+  m.def("sample", &sample);
+  m.def("moe_route", &moe_route);
+  m.def("moe_align", &moe_align);
+  m.def("moe_combine", &moe_combine);
+  m.def("gather_rows", &gather_rows);
+}

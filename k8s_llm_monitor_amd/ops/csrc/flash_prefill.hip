@@ -1,0 +1,190 @@
+// Causal varlen flash-attention forward (prefill) with GQA on gfx950.
+//
+// Workgroup = 4 waves = 128 query rows of one query head; each wave owns 32 rows.
+// K/V tiles of 64 keys are staged through LDS (XOR-swizzled so that both the row reads of K
+// and the transposed reads of V are bank-conflict free).  All products use
+// v_mfma_f32_32x32x16_bf16 in the "swapped" orientation (cdna_hip_programming.md §3):
+//   S^T[kv][q] = K[kv][:] . Q[q][:]        A = K (ds_read_b128),   B = Q^T (registers)
+//   O^T[d][q] += V^T[d][kv] . P^T[kv][q]    A = V^T (ds_read_b64_tr_b16), B = S^T accumulator
+// With the query on the MFMA column (= lane), the online-softmax statistics (m, l) and the
+// rescale of O are lane-local: no cross-lane traffic except one xor-32 per reduction.
+// The score accumulator is converted to bf16 and consumed as the PV B operand in place.
+#include "common.h"
+
+namespace k8sllm {
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restrict__ out, long out_stride,
+                                                               const bf16_t* __restrict__ qkv, long qkv_stride,
+                                                               const int* __restrict__ cu_seqlens,
+                                                               const int* __restrict__ qb_seq,
+                                                               const int* __restrict__ qb_start, int Hq, int Hkv,
+                                                               float scale_log2) {
+  static_assert(D == 128, "prefill kernel is specialised for head_dim 128");
+  constexpr int KS = D / 16;  // 8 k-steps over the head dim
+  constexpr int DT = D / 32;  // 4 output tiles of 32 dims
+  constexpr int CH = D / 8;   // 16-byte chunks per row (16)
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[64 * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[64 * D];
+
+  const int qb = blockIdx.x;
+  const int hq = blockIdx.y;
+  const int G = Hq / Hkv;
+  const int kvh = hq / G;
+  const int seq = qb_seq[qb];
+  const int qs = qb_start[qb];
+  const int s0 = cu_seqlens[seq];
+  const int L = cu_seqlens[seq + 1] - s0;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int myq = qs + wave * 32 + r32;
+  const bf16_t* base = qkv + (long)s0 * qkv_stride;
+  const int koff = (Hq + kvh) * D, voff = (Hq + Hkv + kvh) * D;
+
+  bf16x8 qf[KS];
+  if (myq < L) {
+    const bf16_t* qp = base + (long)myq * qkv_stride + hq * D + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+  }
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  const int wave_q0 = qs + wave * 32;
+  const int kv_end = min(L, qs + 128);
+  // per-lane constants of the transposed V read (see header): group g = lane>>4
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int vcol_base = 16 * ((lane >> 4) & 1) + 4 * p4;
+
+  for (int k0 = 0; k0 < kv_end; k0 += 64) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CH, ch = c % CH;
+      const int kr = k0 + r;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (kr < L) {
+        kv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + koff + ch * 8);
+        vv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + voff + ch * 8);
+      }
+      *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
+      *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
+    }
+    __syncthreads();
+    if (k0 > wave_q0 + 31) continue;  // every key of this tile is in the future of every row of this wave
+
+    f32x16 sacc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[i][r] = 0.f;
+      const int kr = 32 * i + r32;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = 2 * ks + hh;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (kr * CH + (ch ^ (kr & 15))) * 8);
+        sacc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[i], 0, 0, 0);
+      }
+    }
+
+    const bool need_mask = (k0 + 63 > wave_q0) || (k0 + 64 > L);
+    float mx = -1e30f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = sacc[i][r] * scale_log2;
+        if (need_mask) {
+          const int kv = k0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (kv > myq || kv >= L) v = -1e30f;
+        }
+        sacc[i][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = exp2f(m - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(sacc[i][r] - mnew);
+        sacc[i][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sacc[i][8 * s + j];
+        const int row0 = 32 * i + 16 * s + 4 * hh + q4;  // + 8*jj
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int colv = 32 * dt + vcol_base;
+          const int ch = colv >> 3, half = (colv >> 2) & 1;
+          s16x4 t[2];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int row = row0 + 8 * jj;
+            const bf16_t* addr = Vs + (row * CH + (ch ^ ((row & 3) << 2))) * 8 + half * 4;
+            t[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(addr));
+          }
+          const bf16x8 a = __builtin_bit_cast(
+              bf16x8, make_uint4(__builtin_bit_cast(uint2, t[0]).x, __builtin_bit_cast(uint2, t[0]).y,
+                                 __builtin_bit_cast(uint2, t[1]).x, __builtin_bit_cast(uint2, t[1]).y));
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[dt], 0, 0, 0);
+        }
+      }
+  }
+
+  if (myq < L) {
+    const float inv = 1.f / l;
+    bf16_t* op = out + (long)(s0 + myq) * out_stride + (long)hq * D + 4 * hh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 v;
+        v.x = pack2(o[dt][4 * k] * inv, o[dt][4 * k + 1] * inv);
+        v.y = pack2(o[dt][4 * k + 2] * inv, o[dt][4 * k + 3] * inv);
+        *reinterpret_cast<uint2*>(op + 32 * dt + 8 * k) = v;
+      }
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride,
+                                    const int* cu_seqlens, const int* qb_seq, const int* qb_start, int n_qblocks,
+                                    int Hq, int Hkv, int D, float scale, hipStream_t s) {
+  if (n_qblocks <= 0) return 0;
+  if (D != 128 || Hq % Hkv != 0) return -1;
+  hipLaunchKernelGGL((flash_prefill_kernel<128>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out, out_stride,
+                     (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv,
+                     scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,104 @@
+// Rotary embedding (neox half-split pairs i, i+D/2) applied in place to the q and k
+// sections of the fused QKV GEMM output, fused with the paged KV-cache write.
+// SURVEY.md §2.12 K-2.
+//
+// KV-cache layouts (chosen for the decode kernel's MFMA operand loads, see paged_decode.hip):
+//   key_cache   [num_blocks][Hkv][D/8][BS][8]   -> one 16-dim "piece" of all BS tokens is
+//                                                   contiguous: a wave loads 1 KiB per instr.
+//   value_cache [num_blocks][Hkv][D][BS]        -> V^T per block: 8 tokens of one dim are
+//                                                   contiguous (MFMA A-operand of O^T = V^T P^T).
+#include "common.h"
+
+namespace k8sllm {
+
+// One workgroup per token.  Work items: (Hq + Hkv) heads x D/8 "quads" of rotary pairs
+// (each item rotates 4 pairs = 8 B of the lower half and 8 B of the upper half), then
+// Hkv heads x D/8 value chunks of 8 dims (16 B) that are only copied into the cache.
+template <int D>
+__global__ __launch_bounds__(256) void rope_cache_kernel(bf16_t* __restrict__ qkv, long qkv_stride,
+                                                         const int* __restrict__ positions,
+                                                         const float* __restrict__ cos_sin,  // [max_pos][D]: cos | sin
+                                                         bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+                                                         const int* __restrict__ slot_mapping, int Hq, int Hkv,
+                                                         int block_size, int apply_rope) {
+  constexpr int HALF = D / 2;
+  constexpr int QPH = D / 8;  // items per head
+  const int t = blockIdx.x;
+  const int pos = positions[t];
+  const int slot = slot_mapping ? slot_mapping[t] : -1;
+  const int blk = slot >= 0 ? slot / block_size : 0;
+  const int off = slot >= 0 ? slot - blk * block_size : 0;
+  bf16_t* row = qkv + (long)t * qkv_stride;
+  const float* cs = cos_sin + (long)pos * D;
+  const int n_rope = (Hq + Hkv) * QPH;
+  const int n_total = n_rope + Hkv * QPH;
+  for (int w = threadIdx.x; w < n_total; w += 256) {
+    if (w < n_rope) {
+      const int head = w / QPH;
+      const int p = (w - head * QPH) * 4;  // first of 4 pairs, p in [0, HALF)
+      bf16_t* hp = row + head * D;
+      uint2 a = *reinterpret_cast<const uint2*>(hp + p);
+      uint2 b = *reinterpret_cast<const uint2*>(hp + HALF + p);
+      float x1[4] = {lo_bf(a.x), hi_bf(a.x), lo_bf(a.y), hi_bf(a.y)};
+      float x2[4] = {lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+      if (apply_rope) {
+        const float4 c = *reinterpret_cast<const float4*>(cs + p);
+        const float4 s = *reinterpret_cast<const float4*>(cs + HALF + p);
+        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float o1 = x1[j] * cc[j] - x2[j] * ss[j];
+          const float o2 = x2[j] * cc[j] + x1[j] * ss[j];
+          x1[j] = o1;
+          x2[j] = o2;
+        }
+      }
+      a.x = pack2(x1[0], x1[1]);
+      a.y = pack2(x1[2], x1[3]);
+      b.x = pack2(x2[0], x2[1]);
+      b.y = pack2(x2[2], x2[3]);
+      *reinterpret_cast<uint2*>(hp + p) = a;
+      *reinterpret_cast<uint2*>(hp + HALF + p) = b;
+      if (head >= Hq && slot >= 0) {
+        const int kh = head - Hq;
+        bf16_t* kb = k_cache + ((long)blk * Hkv + kh) * (D * block_size);
+        // dims p..p+3 live in piece p/8 at inner offset p%8 (4-aligned)
+        *reinterpret_cast<uint2*>(kb + ((p >> 3) * block_size + off) * 8 + (p & 7)) = a;
+        const int p2 = HALF + p;
+        *reinterpret_cast<uint2*>(kb + ((p2 >> 3) * block_size + off) * 8 + (p2 & 7)) = b;
+      }
+    } else if (slot >= 0) {
+      const int i = w - n_rope;
+      const int vh = i / QPH;
+      const int c = (i - vh * QPH) * 8;
+      const bf16_t* vp = row + (Hq + Hkv + vh) * D + c;
+      const uint4 v = *reinterpret_cast<const uint4*>(vp);
+      bf16_t* vb = v_cache + ((long)blk * Hkv + vh) * (D * block_size) + off;
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vb[(long)(c + 2 * j) * block_size] = (bf16_t)(wv[j] & 0xffff);
+        vb[(long)(c + 2 * j + 1) * block_size] = (bf16_t)(wv[j] >> 16);
+      }
+    }
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+extern "C" int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, void* k_cache,
+                                 void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D,
+                                 int block_size, int apply_rope, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (D == 128)
+    hipLaunchKernelGGL((rope_cache_kernel<128>), dim3(T), dim3(256), 0, s, (bf16_t*)qkv, qkv_stride, positions,
+                       cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
+  else if (D == 64)
+    hipLaunchKernelGGL((rope_cache_kernel<64>), dim3(T), dim3(256), 0, s, (bf16_t*)qkv, qkv_stride, positions,
+                       cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,206 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from k8s_llm_monitor_amd import ops
+from k8s_llm_monitor_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    ops.native()  # fail loudly when the extension is missing on a GPU box
+    torch.manual_seed(0)
+
+
+def _close(a, b, atol, rtol=0.0, what=""):
+    err = (a.float() - b.float()).abs()
+    tol = atol + rtol * b.float().abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("rows,d", [(1, 4096), (64, 4096), (333, 8192), (7, 768), (5, 1024)])
+def test_rms_norm(rows, d):
+    x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(d, device=DEV, dtype=torch.bfloat16)
+    y = ops.rms_norm(x, w, 1e-5)
+    _close(y, ref.rms_norm(x.cpu(), w.cpu(), 1e-5).to(DEV), atol=2e-2, rtol=1e-2, what="rms_norm")
+
+
+@pytest.mark.parametrize("rows,d", [(64, 4096), (129, 8192)])
+def test_fused_add_rms_norm(rows, d):
+    x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(d, device=DEV, dtype=torch.bfloat16)
+    y_ref, s_ref = ref.fused_add_rms_norm(x.cpu(), r.cpu(), w.cpu(), 1e-5)
+    y = ops.fused_add_rms_norm(x, r, w, 1e-5)
+    _close(r, s_ref.to(DEV), atol=1e-2, rtol=1e-2, what="residual")
+    _close(y, y_ref.to(DEV), atol=3e-2, rtol=1e-2, what="norm")
+
+
+def test_layer_norm():
+    x = torch.randn(37, 768, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(768, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(768, device=DEV, dtype=torch.bfloat16)
+    _close(ops.layer_norm(x, w, b, 1e-5), ref.layer_norm(x.cpu(), w.cpu(), b.cpu(), 1e-5).to(DEV),
+           atol=3e-2, rtol=1e-2, what="layer_norm")
+
+
+@pytest.mark.parametrize("rows,F", [(1, 14336), (64, 14336), (300, 3584)])
+def test_silu_mul(rows, F):
+    x = torch.randn(rows, 2 * F, device=DEV, dtype=torch.bfloat16)
+    _close(ops.silu_mul(x), ref.silu_mul(x.cpu()).to(DEV), atol=2e-2, rtol=1e-2, what="silu_mul")
+
+
+def test_gelu():
+    x = torch.randn(100, 3072, device=DEV, dtype=torch.bfloat16)
+    _close(ops.gelu_tanh(x), ref.gelu_tanh(x.cpu()).to(DEV), atol=2e-2, rtol=1e-2, what="gelu")
+
+
+def test_embedding_vocab_parallel():
+    w = torch.randn(1000, 512, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, 2000, (77,), device=DEV, dtype=torch.int32)
+    y = ops.embedding(ids, w, vocab_start=500)
+    assert torch.equal(y.cpu(), ref.embedding(ids.cpu(), w.cpu(), 500))
+
+
+def _make_cache(nb, hkv, d, bs=16):
+    k = torch.randn(nb, hkv, d // 8, bs, 8, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(nb, hkv, d, bs, device=DEV, dtype=torch.bfloat16)
+    return k, v
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (8, 8, 128), (64, 8, 128), (16, 4, 64)])
+def test_rope_and_cache(hq, hkv, d):
+    T, nb = 50, 16
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(8192, d, 500000.0, device=DEV)
+    slots = torch.randperm(nb * 16, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1  # padding token: no cache write
+    kc, vc = _make_cache(nb, hkv, d)
+    kc0, vc0 = kc.clone().cpu(), vc.clone().cpu()
+    q2 = qkv.clone().cpu()
+    ops.rope_and_cache(qkv, pos, cs, kc, vc, slots, hq, hkv, d)
+    ref.rope_and_cache(q2, pos.cpu(), cs.cpu(), kc0, vc0, slots.cpu(), hq, hkv, d)
+    _close(qkv, q2.to(DEV), atol=2e-2, rtol=1e-2, what="rope qkv")
+    _close(kc, kc0.to(DEV), atol=2e-2, rtol=1e-2, what="k_cache")
+    assert torch.equal(vc.cpu(), vc0), "v_cache"
+
+
+@pytest.mark.parametrize("B,hq,hkv,d,maxlen", [(1, 32, 8, 128, 33), (8, 32, 8, 128, 1100), (64, 32, 8, 128, 700),
+                                                (3, 64, 8, 128, 2000), (5, 8, 8, 128, 300), (4, 16, 4, 64, 513)])
+def test_paged_decode(B, hq, hkv, d, maxlen):
+    bs = 16
+    max_blocks = (maxlen + bs - 1) // bs + 1
+    nb = B * max_blocks + 4
+    kc, vc = _make_cache(nb, hkv, d, bs)
+    lens = torch.randint(1, maxlen + 1, (B,), dtype=torch.int32)
+    lens[0] = maxlen
+    perm = torch.randperm(nb)[: B * max_blocks].view(B, max_blocks).to(torch.int32)
+    bt = perm.to(DEV)
+    q = torch.randn(B, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)  # q inside fused rows
+    scale = 1.0 / math.sqrt(d)
+    y = ops.paged_decode(q, kc, vc, bt, lens.to(DEV), hq, hkv, d, scale)
+    r = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), perm, lens, hq, hkv, d, scale)
+    _close(y, r.to(DEV), atol=2e-2, rtol=2e-2, what="paged_decode")
+
+
+def test_paged_decode_zero_len_rows():
+    hq, hkv, d = 32, 8, 128
+    kc, vc = _make_cache(64, hkv, d)
+    bt = torch.arange(64, device=DEV, dtype=torch.int32).view(4, 16)
+    lens = torch.tensor([0, 17, 0, 256], device=DEV, dtype=torch.int32)
+    q = torch.randn(4, hq * d, device=DEV, dtype=torch.bfloat16)
+    y = ops.paged_decode(q, kc, vc, bt, lens, hq, hkv, d, 0.088)
+    assert torch.all(y[0] == 0) and torch.all(y[2] == 0)
+    r = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens.cpu(), hq, hkv, d, 0.088)
+    _close(y, r.to(DEV), atol=2e-2, rtol=2e-2, what="paged_decode pad rows")
+
+
+@pytest.mark.parametrize("lens,hq,hkv", [([1], 32, 8), ([128], 32, 8), ([300, 77, 1024], 32, 8),
+                                         ([513, 200], 64, 8), ([129, 64], 8, 8)])
+def test_flash_prefill(lens, hq, hkv):
+    d = 128
+    T = sum(lens)
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0).tolist()), dtype=torch.int32, device=DEV)
+    scale = 1.0 / math.sqrt(d)
+    y = ops.flash_prefill(qkv, cu, hq, hkv, d, scale)
+    r = ref.flash_prefill(qkv.cpu(), cu.cpu(), hq, hkv, d, scale)
+    _close(y, r.to(DEV), atol=2e-2, rtol=2e-2, what="flash_prefill")
+
+
+def test_flash_prefill_softmax_spike():
+    """Force a large running-max jump mid-sequence (rescale branch) - rule 26."""
+    hq, hkv, d, L = 8, 8, 128, 300
+    qkv = torch.randn(L, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16) * 0.1
+    qkv[200, hq * d:(hq + hkv) * d] *= 400.0  # one key much larger than the rest
+    cu = torch.tensor([0, L], dtype=torch.int32, device=DEV)
+    y = ops.flash_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d))
+    r = ref.flash_prefill(qkv.cpu(), cu.cpu(), hq, hkv, d, 1 / math.sqrt(d))
+    _close(y, r.to(DEV), atol=3e-2, rtol=2e-2, what="flash_prefill spike")
+
+
+@pytest.mark.parametrize("V", [128256, 32000, 50304])
+def test_sample_greedy(V):
+    logits = torch.randn(64, V, device=DEV, dtype=torch.bfloat16)
+    logits[5, 1234] = 100.0
+    tok = ops.sample(logits)
+    assert torch.equal(tok.cpu(), ref.greedy(logits.cpu()))
+    tok32 = ops.sample(logits.float())
+    assert torch.equal(tok32.cpu(), ref.greedy(logits.cpu()))
+
+
+def test_sample_topk_topp_temperature():
+    B, V = 16, 32000
+    logits = torch.randn(B, V, device=DEV, dtype=torch.float32) * 3
+    temps = torch.full((B,), 0.7, device=DEV)
+    topk = torch.full((B,), 5, device=DEV, dtype=torch.int32)
+    topp = torch.ones(B, device=DEV)
+    rng = torch.tensor([1234, 0], device=DEV, dtype=torch.int64)
+    allowed = torch.topk(logits, 5, dim=-1).indices
+    for i in range(20):
+        rng[1] = i
+        tok = ops.sample(logits, temps, topk, topp, rng).long()
+        assert (allowed == tok[:, None]).any(-1).all(), "top-k violated"
+    # top-p: with p small only the argmax survives
+    topk.zero_()
+    topp.fill_(1e-6)
+    tok = ops.sample(logits, temps, topk, topp, rng)
+    assert torch.equal(tok.cpu(), ref.greedy(logits.cpu()))
+
+
+def test_sample_distribution():
+    """Gumbel-max must sample softmax(logits/T): empirical frequencies over 4 tokens."""
+    V = 4
+    base = torch.tensor([0.0, 1.0, 2.0, 0.5])
+    B = 4096
+    logits = base.repeat(B, 1).to(DEV)
+    temps = torch.full((B,), 1.0, device=DEV)
+    rng = torch.tensor([7, 3], device=DEV, dtype=torch.int64)
+    tok = ops.sample(logits, temps, None, None, rng).cpu()
+    freq = torch.bincount(tok.long(), minlength=V).float() / B
+    assert torch.allclose(freq, torch.softmax(base, 0), atol=0.03)
+
+
+def test_moe_route_align_combine():
+    T, E, K, d = 300, 8, 2, 256
+    logits = torch.randn(T, E, device=DEV)
+    ids, w = ops.moe_route(logits, K, True)
+    rids, rw = ref.moe_route(logits.cpu(), K, True)
+    assert torch.equal(ids.cpu(), rids)
+    assert torch.allclose(w.cpu(), rw, atol=1e-5)
+    off, srt, inv = ops.moe_align(ids, E)
+    roff, rsrt, rinv = ref.moe_align(ids.cpu(), E)
+    assert torch.equal(off.cpu(), roff) and torch.equal(srt.cpu(), rsrt) and torch.equal(inv.cpu(), rinv)
+    x = torch.randn(T, d, device=DEV, dtype=torch.bfloat16)
+    xs = ops.gather_rows(x, srt, K)
+    assert torch.equal(xs.cpu(), x.cpu()[srt.cpu().long() // K])
+    y = ops.moe_combine(xs, inv, w, T)
+    _close(y, ref.moe_combine(xs.cpu(), inv.cpu(), w.cpu(), T).to(DEV), atol=2e-2, rtol=1e-2, what="combine")
