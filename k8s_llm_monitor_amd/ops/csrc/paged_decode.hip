@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(float* __restrict__ p
     const long ph = ((long)b * Hq + kvh * G + h) * NP + part;
     part_out[ph * D + d] = o;
     if (d == 0) {
-      part_ml[ph * 2] = M;
+      part_ml[ph * 2] = fmaxf(fmaxf(s_max[0][h], s_max[1][h]), fmaxf(s_max[2][h], s_max[3][h]));
       part_ml[ph * 2 + 1] = s_sum[0][h] + s_sum[1][h] + s_sum[2][h] + s_sum[3][h];
     }
   }
