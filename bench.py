@@ -1,0 +1,151 @@
+#!/usr/bin/env python
+"""Headline benchmark: diagnostic queries/sec + p50 answer latency, Llama-3-8B TP=1, on the
+``/api/v1/query`` path (BASELINE.json "metric").
+
+One process per GPU (torchrun launches N ranks); each rank is an independent TP=1 engine replica
+(data-parallel serving, weak scaling: per-GPU work is fixed).  One *step* = one wave of
+``--batch`` concurrent diagnostic queries per GPU, each a synthetic cluster-state prompt in the
+reference's prompt format answered with up to ``--max-new-tokens`` tokens through the
+continuous-batching engine (prefill + hipGraph decode + sampling).  With ``--path http`` (default)
+every query is a real ``POST /api/v1/query`` to the in-process REST server; ``--path engine``
+submits to the engine queue directly (same engine, no HTTP).
+
+Timing: W untimed warmup waves, then a barrier + device sync, K timed waves, a device sync + barrier;
+the elapsed time is the MAX over ranks.  ``value`` = total queries answered by all ranks / that
+time.  Weights are random-init (no checkpoints offline), prompts are synthetic (``data``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
+    ap.add_argument("--max-new-tokens", type=int, default=256)
+    ap.add_argument("--kv-cache-gb", type=float, default=48.0)
+    ap.add_argument("--path", choices=["http", "engine"], default="engine")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    a = ap.parse_args()
+
+    import torch
+
+    from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
+    from k8s_llm_monitor_amd.llm.synthetic import synthetic_cluster_prompt
+    from k8s_llm_monitor_amd.parallel import comm
+    from k8s_llm_monitor_amd.parallel.state import barrier_all, init_parallel
+
+    ps = init_parallel(tp_size=1)
+    rank, world = ps.rank, ps.world_size
+    if a.gpus != world and world > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    on_gpu = ps.device.type == "cuda"
+    if on_gpu:
+        from k8s_llm_monitor_amd import ops
+        ops.native()  # fail loudly if the HIP kernels are missing
+
+    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, max_model_len=8192,
+                                 kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
+                                 seed=a.seed + rank), pstate=ps)
+    eng.warmup()
+    svc = EngineService(eng)
+    server = None
+    if a.path == "http":
+        from k8s_llm_monitor_amd.monitor.app import build_app_for_bench
+
+        server, port = build_app_for_bench(svc)
+    params = SamplingParams(max_tokens=a.max_new_tokens, temperature=0.1, ignore_eos=True)
+
+    def wave(w: int) -> tuple[list[float], int, int]:
+        prompts = [synthetic_cluster_prompt(seed=(rank * 1_000_003 + w * a.batch + i)) for i in range(a.batch)]
+        t0 = time.perf_counter()
+        if a.path == "http":
+            from k8s_llm_monitor_amd.monitor.app import post_queries
+
+            res = post_queries(port, [p for p in prompts], a.max_new_tokens)
+            lat = [r["latency_ms"] for r in res]
+            ptok = sum(r["prompt_tokens"] for r in res)
+            gtok = sum(r["completion_tokens"] for r in res)
+        else:
+            futs = [svc.submit(p, params) for p in prompts]
+            outs = [f.result() for f in futs]
+            lat = [s.timings()["latency_ms"] for _, s in outs]
+            ptok = sum(len(s.prompt_ids) for _, s in outs)
+            gtok = sum(len(s.output_ids) for _, s in outs)
+        del t0
+        return lat, ptok, gtok
+
+    for w in range(a.warmup):
+        wave(w)
+    barrier_all()
+    if on_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lats, ptoks, gtoks = [], 0, 0
+    for k in range(a.steps):
+        lat, p, g = wave(a.warmup + k)
+        lats += lat
+        ptoks += p
+        gtoks += g
+    if on_gpu:
+        torch.cuda.synchronize()
+    barrier_all()
+    elapsed = time.perf_counter() - t0
+    t_max = comm.all_reduce_max_scalar(elapsed)
+    total_q = comm.all_reduce_sum_scalar(float(a.batch * a.steps))
+    total_gen = comm.all_reduce_sum_scalar(float(gtoks))
+    p50_local = statistics.median(lats)
+    p50 = comm.all_reduce_max_scalar(p50_local)
+    stats = svc.stats()
+    svc.close()
+    if server is not None:
+        server.shutdown()
+    if rank == 0:
+        qps = total_q / t_max
+        res = {
+            "metric": "diagnostic queries/sec (Llama-3-8B TP=1, /api/v1/query)",
+            "value": round(qps, 4),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(t_max / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
+            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": 8192,
+                       "parallelism": f"dp{world}" if world > 1 else "tp1",
+                       "prompt_tokens_mean": round(ptoks / max(1, a.batch * a.steps), 1),
+                       "max_new_tokens": a.max_new_tokens, "path": a.path},
+            "p50_latency_ms": round(p50, 2),
+            "p99_latency_ms": round(sorted(lats)[min(len(lats) - 1, int(len(lats) * 0.99))], 2),
+            "generated_tokens_per_s": round(total_gen / t_max, 1),
+            "decode_steps": stats.get("decode_steps"),
+            "prefill_steps": stats.get("prefill_steps"),
+        }
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,223 @@
+"""Model runner: owns the paged KV cache, turns a StepPlan into device tensors, runs the model
+and samples.
+
+Decode steps are replayed from hipGraphs (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) captured
+once per batch-size bucket.  A bucket's graph reads static device buffers (token ids, positions,
+slot mapping, block tables, sequence lengths, sampling parameters, RNG state) that the host
+refreshes with a handful of async copies before each replay; the only host<->device sync per
+step is reading back the sampled token ids.  Prefill runs eagerly (variable shapes).
+
+KV-cache layouts are the ones the HIP kernels are written for (``ops/csrc/rope_cache.hip``):
+K ``[NB, Hkv, D/8, 16, 8]`` and V ``[NB, Hkv, D, 16]`` per layer, one allocation for all layers
+sized from ``kv_cache_gb`` (MI355X: 288 GB HBM per GPU - an 8B model leaves >250 GB for KV).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.llama import AttnMeta, CausalLM
+from .sequence import Sequence
+
+BLOCK_SIZE = 16
+DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256)
+
+
+@dataclass
+class RunnerConfig:
+    max_num_seqs: int = 64
+    max_model_len: int = 8192
+    kv_cache_gb: float = 16.0
+    num_blocks: Optional[int] = None  # overrides kv_cache_gb
+    use_graphs: bool = True
+    seed: int = 0
+
+
+class ModelRunner:
+    def __init__(self, model: CausalLM, cfg: RunnerConfig):
+        self.model = model
+        self.cfg = cfg
+        self.device = model.device
+        c = model.cfg
+        self.max_len = min(cfg.max_model_len, c.max_position)
+        self.max_blocks_per_seq = (self.max_len + BLOCK_SIZE - 1) // BLOCK_SIZE
+        L, hkv, D = c.n_layers, model.hkv, model.D
+        per_block = 2 * L * hkv * D * BLOCK_SIZE * 2  # bytes (K + V, bf16)
+        nb = cfg.num_blocks or max(self.max_blocks_per_seq + 1, int(cfg.kv_cache_gb * (1 << 30) // per_block))
+        self.num_blocks = nb
+        self.k_cache = torch.zeros(L, nb, hkv, D // 8, BLOCK_SIZE, 8, dtype=model.dtype, device=self.device)
+        self.v_cache = torch.zeros(L, nb, hkv, D, BLOCK_SIZE, dtype=model.dtype, device=self.device)
+        self.kv = [(self.k_cache[i], self.v_cache[i]) for i in range(L)]
+        self.is_gpu = self.device.type == "cuda"
+        B = cfg.max_num_seqs
+        self.B = B
+        dev = self.device
+        # static decode inputs (graph inputs)
+        self.d_ids = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_pos = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_slots = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        self.d_bt = torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, device=dev)
+        self.d_lens = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_temp = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.d_topk = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_topp = torch.ones(B, dtype=torch.float32, device=dev)
+        self.rng = torch.tensor([cfg.seed, 0], dtype=torch.int64, device=dev)
+        self.d_out = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev) \
+            if self.is_gpu else None
+        # pinned host staging
+        pin = self.is_gpu
+        self.h_ids = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_pos = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_slots = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_lens = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_bt = torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
+        self.h_temp = torch.zeros(B, dtype=torch.float32, pin_memory=pin)
+        self.h_topk = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_topp = torch.ones(B, dtype=torch.float32, pin_memory=pin)
+        self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        # numpy views of the pinned buffers: cheap per-element host writes
+        self.n_ids, self.n_pos, self.n_slots = self.h_ids.numpy(), self.h_pos.numpy(), self.h_slots.numpy()
+        self.n_lens, self.n_bt = self.h_lens.numpy(), self.h_bt.numpy()
+        self.n_temp, self.n_topk, self.n_topp = self.h_temp.numpy(), self.h_topk.numpy(), self.h_topp.numpy()
+        self.buckets = [b for b in DEFAULT_BUCKETS if b < B] + [B]
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self.n_steps = {"prefill": 0, "decode": 0}
+
+    # --------------------------------------------------------------------- helpers
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"batch {n} exceeds max_num_seqs {self.B}")
+
+    def _sample(self, logits: torch.Tensor, temp, topk, topp, out=None) -> torch.Tensor:
+        tok = ops.sample(logits, temp, topk, topp, self.rng, out=out)
+        self.rng[1:] += 1  # fresh numbers next step (also inside a captured graph)
+        return tok
+
+    # --------------------------------------------------------------------- prefill
+    def prefill(self, seqs: list[Sequence]) -> list[int]:
+        """Run whole prompts (prompt + any tokens generated before a preemption); returns the first
+        sampled token of each sequence."""
+        dev = self.device
+        lens = [s.num_tokens for s in seqs]
+        ids = np.concatenate([np.asarray(s.all_ids, dtype=np.int32) for s in seqs])
+        pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        slots = np.empty(ids.shape[0], dtype=np.int32)
+        o = 0
+        for s, n in zip(seqs, lens):
+            bt = np.asarray(s.block_table, dtype=np.int64)
+            p = np.arange(n)
+            slots[o:o + n] = bt[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
+            o += n
+        cu = np.zeros(len(seqs) + 1, dtype=np.int32)
+        cu[1:] = np.cumsum(lens)
+        qs, st = ops.prefill_qblocks(cu.tolist())
+        t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dt, non_blocking=True)
+        meta = AttnMeta(is_prefill=True, positions=t(pos), slot_mapping=t(slots), cu_seqlens=t(cu),
+                        qb_seq=t(np.asarray(qs, dtype=np.int32)), qb_start=t(np.asarray(st, dtype=np.int32)),
+                        logits_idx=t(cu[1:] - 1, torch.int64))
+        logits = self.model.forward(t(ids), meta, self.kv)
+        S = len(seqs)
+        temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32).to(dev)
+        topk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int32).to(dev)
+        topp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32).to(dev)
+        tok = self._sample(logits, temp, topk, topp)
+        self.n_steps["prefill"] += 1
+        return tok[:S].cpu().tolist()
+
+    # --------------------------------------------------------------------- decode
+    def _decode_body(self, b: int) -> None:
+        meta = AttnMeta(is_prefill=False, positions=self.d_pos[:b], slot_mapping=self.d_slots[:b],
+                        block_tables=self.d_bt[:b], seq_lens=self.d_lens[:b], decode_ws=self.decode_ws)
+        logits = self.model.forward(self.d_ids[:b], meta, self.kv)
+        self._sample(logits, self.d_temp[:b], self.d_topk[:b], self.d_topp[:b], out=self.d_out[:b])
+
+    def capture_graphs(self, buckets: Optional[list[int]] = None) -> None:
+        if not (self.is_gpu and self.cfg.use_graphs):
+            return
+        torch.cuda.synchronize()
+        # replays must not disturb real sequences: capture with empty rows (len 0, no cache write)
+        self.d_lens.zero_()
+        self.d_slots.fill_(-1)
+        rng_state = self.rng.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._decode_body(self.B)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        for b in sorted(buckets or self.buckets, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._decode_body(b)
+            self.graphs[b] = g
+        torch.cuda.synchronize()
+        self.rng.copy_(rng_state)
+
+    def decode(self, seqs: list[Sequence]) -> list[int]:
+        n = len(seqs)
+        b = self.bucket_for(n) if self.graphs else n
+        ids, pos_a, slots, lens = self.n_ids, self.n_pos, self.n_slots, self.n_lens
+        temp, topk, topp, bt_a = self.n_temp, self.n_topk, self.n_topp, self.n_bt
+        bt_a[:b] = 0
+        for i, s in enumerate(seqs):
+            pos = s.num_tokens - 1  # position of the token being fed (the last generated one)
+            bt = s.block_table
+            ids[i] = s.last_token
+            pos_a[i] = pos
+            slots[i] = bt[pos // BLOCK_SIZE] * BLOCK_SIZE + pos % BLOCK_SIZE
+            lens[i] = pos + 1
+            bt_a[i, : len(bt)] = bt
+            p = s.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k
+            topp[i] = p.top_p
+        if b > n:
+            ids[n:b] = 0
+            pos_a[n:b] = 0
+            slots[n:b] = -1
+            lens[n:b] = 0
+            temp[n:b] = 0
+            topk[n:b] = 0
+            topp[n:b] = 1
+        hb = self.h_bt[:b]
+        nb = True
+        self.d_ids[:b].copy_(self.h_ids[:b], non_blocking=nb)
+        self.d_pos[:b].copy_(self.h_pos[:b], non_blocking=nb)
+        self.d_slots[:b].copy_(self.h_slots[:b], non_blocking=nb)
+        self.d_lens[:b].copy_(self.h_lens[:b], non_blocking=nb)
+        self.d_bt[:b].copy_(hb, non_blocking=nb)
+        self.d_temp[:b].copy_(self.h_temp[:b], non_blocking=nb)
+        self.d_topk[:b].copy_(self.h_topk[:b], non_blocking=nb)
+        self.d_topp[:b].copy_(self.h_topp[:b], non_blocking=nb)
+        g = self.graphs.get(b)
+        if g is not None:
+            g.replay()
+        else:
+            self._decode_body(b)
+        self.n_steps["decode"] += 1
+        if self.is_gpu:
+            self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return self.h_out[:n].tolist()
+        return self.d_out[:n].tolist()
+
+    def memory_report(self) -> dict:
+        kv = (self.k_cache.numel() + self.v_cache.numel()) * self.k_cache.element_size()
+        return {"kv_cache_bytes": kv, "kv_blocks": self.num_blocks, "block_size": BLOCK_SIZE,
+                "max_model_len": self.max_len, "graph_buckets": sorted(self.graphs)}
+
+
+def kv_blocks_for(cfg_layers: int, hkv: int, D: int, gb: float) -> int:
+    per_block = 2 * cfg_layers * hkv * D * BLOCK_SIZE * 2
+    return int(math.floor(gb * (1 << 30) / per_block))

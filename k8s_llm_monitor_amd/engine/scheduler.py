@@ -1,0 +1,134 @@
+"""Continuous-batching scheduler.
+
+Each engine step is either a *prefill* step (admit waiting requests whose whole prompts fit the
+token budget and the free KV blocks) or a *decode* step (one token for every running sequence).
+Prefill has priority so newly arrived diagnostic queries join the running batch at the next
+step; decode steps are captured hipGraphs, so keeping them homogeneous keeps them replayable.
+When the cache runs out during decode the most recently admitted sequence is preempted
+(blocks freed, re-queued at the front, recomputed later) - a full cache degrades throughput, it
+never fails requests ("OOM on KV-cache allocation leads to request rejection with
+503, not a crash"; here it does not even reject).
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .block_manager import BlockManager
+from .sequence import Sequence, SeqStatus
+
+
+@dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 64
+    max_prefill_tokens: int = 16384
+    max_model_len: int = 8192
+
+
+@dataclass
+class StepPlan:
+    is_prefill: bool
+    seqs: list[Sequence] = field(default_factory=list)
+    preempted: list[Sequence] = field(default_factory=list)
+
+    @property
+    def empty(self) -> bool:
+        return not self.seqs
+
+
+class Scheduler:
+    def __init__(self, cfg: SchedulerConfig, blocks: BlockManager):
+        self.cfg = cfg
+        self.blocks = blocks
+        self.waiting: deque[Sequence] = deque()
+        self.running: list[Sequence] = []
+
+    def add(self, seq: Sequence) -> None:
+        if len(seq.prompt_ids) == 0:
+            raise ValueError("empty prompt")
+        if len(seq.prompt_ids) >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {len(seq.prompt_ids)} tokens exceeds max_model_len {self.cfg.max_model_len}")
+        if self.blocks.blocks_needed(len(seq.prompt_ids) + 1) > self.blocks.num_blocks:
+            raise ValueError("prompt larger than the whole KV cache")
+        seq.status = SeqStatus.WAITING
+        self.waiting.append(seq)
+
+    def abort(self, seq: Sequence) -> None:
+        if seq in self.running:
+            self.running.remove(seq)
+        try:
+            self.waiting.remove(seq)
+        except ValueError:
+            pass
+        self.blocks.free(seq)
+        seq.status = SeqStatus.ABORTED
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def schedule(self) -> StepPlan:
+        # 1. prefill newly arrived (or preempted) requests
+        if self.waiting and len(self.running) < self.cfg.max_num_seqs:
+            plan = StepPlan(is_prefill=True)
+            budget = self.cfg.max_prefill_tokens
+            while self.waiting and len(self.running) + len(plan.seqs) < self.cfg.max_num_seqs:
+                seq = self.waiting[0]
+                n = seq.num_tokens
+                if plan.seqs and n > budget:
+                    break
+                if not self.blocks.can_allocate(seq):
+                    break
+                self.waiting.popleft()
+                self.blocks.allocate(seq)
+                seq.status = SeqStatus.RUNNING
+                plan.seqs.append(seq)
+                budget -= n
+                if budget <= 0:
+                    break
+            if plan.seqs:
+                self.running.extend(plan.seqs)
+                return plan
+        # 2. decode every running sequence
+        plan = StepPlan(is_prefill=False)
+        i = 0
+        while i < len(self.running):
+            seq = self.running[i]
+            if self.blocks.ensure_slot(seq):
+                i += 1
+                continue
+            victim = self.running.pop()  # youngest
+            self._preempt(victim)
+            plan.preempted.append(victim)
+            # retry the same index (the victim may have been this very sequence)
+        plan.seqs = list(self.running)
+        return plan
+
+    def _preempt(self, seq: Sequence) -> None:
+        self.blocks.free(seq)
+        seq.status = SeqStatus.WAITING
+        seq.n_preemptions += 1
+        self.waiting.appendleft(seq)
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        if seq in self.running:
+            self.running.remove(seq)
+        self.blocks.free(seq)
+
+    def stats(self) -> dict:
+        return {
+            "waiting": len(self.waiting),
+            "running": len(self.running),
+            "kv_blocks_total": self.blocks.num_blocks,
+            "kv_blocks_free": self.blocks.num_free,
+            "kv_usage": round(self.blocks.usage(), 4),
+        }
+
+
+def next_plan_or_none(s: Scheduler) -> Optional[StepPlan]:
+    if not s.has_work():
+        return None
+    p = s.schedule()
+    return None if p.empty else p

@@ -1,0 +1,308 @@
+"""Decoder-only causal LMs served by the diagnostic engine: Llama-3 (dense), Mixtral (MoE) and
+GPT-2 (the CPU plumbing config), with Megatron tensor parallelism.
+
+Nothing here exists in the reference ("no LLM, no GPU code"); the model replaces
+the remote ``callLLMAPI`` step of the doc sketch ``docs/metrics-usage-example.md:244-306``.
+
+Hot path per layer (GPU), all on the current HIP stream so a decode step captures into one
+hipGraph:
+
+  fused_add_rms_norm (HIP) -> QKV GEMM (hipBLASLt) -> rope_and_cache (HIP: RoPE + paged KV write)
+  -> flash_prefill | paged_decode (HIP MFMA) -> o_proj GEMM (+ RCCL all-reduce at TP>1)
+  -> fused_add_rms_norm (HIP) -> gate_up GEMM -> silu_mul (HIP) -> down GEMM (+ all-reduce)
+
+Weights are stored fused and pre-sharded: ``wqkv`` [(Hq+2Hkv)/tp * D, d] (column-parallel),
+``wo`` [d, Hq/tp * D] (row-parallel), ``w13`` [2F/tp, d] (gate rows then up rows of this rank's
+shard), ``w2`` [d, F/tp].  Random init is seeded per tensor name, and every rank generates the
+full tensor then keeps its shard, so any TP degree reproduces the TP=1 model exactly.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel.comm import shard_range, tp_all_gather_last, tp_all_reduce
+from ..parallel.state import ParallelState, get_state
+from .config import ModelConfig
+
+
+@dataclass
+class AttnMeta:
+    """Per-step batch metadata (built by the engine's model runner)."""
+
+    is_prefill: bool
+    positions: torch.Tensor  # [T] int32
+    slot_mapping: torch.Tensor  # [T] int32, -1 = do not write the cache
+    # prefill (whole prompts in this step)
+    cu_seqlens: Optional[torch.Tensor] = None  # [S+1] int32
+    qb_seq: Optional[torch.Tensor] = None  # flash_prefill q-block schedule
+    qb_start: Optional[torch.Tensor] = None
+    logits_idx: Optional[torch.Tensor] = None  # [S] int64 rows that produce logits
+    # decode (one token per sequence)
+    block_tables: Optional[torch.Tensor] = None  # [B, W] int32
+    seq_lens: Optional[torch.Tensor] = None  # [B] int32 (including the token being decoded)
+    decode_ws: Optional[tuple] = None  # paged_decode partial buffers
+
+
+def _seed_for(name: str, seed: int) -> int:
+    h = hashlib.blake2b(f"{seed}:{name}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & 0x7FFF_FFFF_FFFF_FFFF
+
+
+class CausalLM:
+    def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16, seed: int = 0,
+                 pstate: Optional[ParallelState] = None, init_std: float = 0.02):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.seed = seed
+        self.ps = pstate or get_state()
+        tp, r = self.ps.tp_size, self.ps.tp_rank
+        if cfg.n_heads % tp or cfg.n_kv_heads % tp or cfg.ffn_dim % tp or cfg.vocab_size_padded(tp) % tp:
+            raise ValueError(f"{cfg.name}: heads/ffn/vocab not divisible by tp={tp}")
+        self.tp, self.rank = tp, r
+        self.hq = cfg.n_heads // tp
+        self.hkv = cfg.n_kv_heads // tp
+        self.D = cfg.head_dim
+        self.f_local = cfg.ffn_dim // tp
+        self.vocab_padded = cfg.vocab_size_padded(tp)
+        self.v_lo, self.v_hi = shard_range(self.vocab_padded, tp, r)
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.std = init_std
+        if cfg.is_moe:
+            if cfg.n_experts % tp:
+                raise ValueError("n_experts must be divisible by tp for expert parallelism")
+            self.e_lo, self.e_hi = shard_range(cfg.n_experts, tp, r)
+        self.layers: list[dict] = []
+        self._build()
+        self.cos_sin = None
+        if cfg.arch == "llama":
+            self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, cfg.rope_scaling,
+                                            device=self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _rand(self, name: str, shape, std: Optional[float] = None) -> torch.Tensor:
+        g = torch.Generator(device=self.device)
+        g.manual_seed(_seed_for(name, self.seed))
+        t = torch.empty(shape, dtype=torch.float32 if self.device.type == "cpu" else self.dtype, device=self.device)
+        t.normal_(0.0, self.std if std is None else std, generator=g)
+        return t.to(self.dtype)
+
+    def _ones(self, n) -> torch.Tensor:
+        return torch.ones(n, dtype=self.dtype, device=self.device)
+
+    def _zeros(self, n) -> torch.Tensor:
+        return torch.zeros(n, dtype=self.dtype, device=self.device)
+
+    def _build(self) -> None:
+        c = self.cfg
+        d, D, tp, r = c.d_model, self.D, self.tp, self.rank
+        out_std = self.std / math.sqrt(2 * c.n_layers)
+        emb = self._rand("embed", (self.vocab_padded, d))
+        self.embed = emb[self.v_lo:self.v_hi].contiguous()
+        del emb
+        if c.tie_embeddings:
+            self.lm_head = self.embed
+        else:
+            lm = self._rand("lm_head", (self.vocab_padded, d))
+            self.lm_head = lm[self.v_lo:self.v_hi].contiguous()
+            del lm
+        if c.arch == "gpt2":
+            self.pos_embed = self._rand("pos_embed", (c.max_position, d), 0.01)
+            self.final_norm = (self._ones(d), self._zeros(d))
+        else:
+            self.final_norm = self._ones(d)
+        q_lo, q_hi = shard_range(c.n_heads * D, tp, r)
+        kv_lo, kv_hi = shard_range(c.n_kv_heads * D, tp, r)
+        f_lo, f_hi = shard_range(c.ffn_dim, tp, r)
+        for i in range(c.n_layers):
+            p = f"layers.{i}."
+            L: dict = {}
+            wq = self._rand(p + "wq", (c.n_heads * D, d))
+            wk = self._rand(p + "wk", (c.n_kv_heads * D, d))
+            wv = self._rand(p + "wv", (c.n_kv_heads * D, d))
+            L["wqkv"] = torch.cat([wq[q_lo:q_hi], wk[kv_lo:kv_hi], wv[kv_lo:kv_hi]], 0).contiguous()
+            del wq, wk, wv
+            wo = self._rand(p + "wo", (d, c.n_heads * D), out_std)
+            L["wo"] = wo[:, q_lo:q_hi].contiguous()
+            del wo
+            if c.arch == "gpt2":
+                L["ln1"] = (self._ones(d), self._zeros(d))
+                L["ln2"] = (self._ones(d), self._zeros(d))
+                bqkv = self._rand(p + "bqkv", ((c.n_heads + 2 * c.n_kv_heads) * D,), 0.01)
+                nq, nk = c.n_heads * D, c.n_kv_heads * D
+                L["bqkv"] = torch.cat([bqkv[q_lo:q_hi], bqkv[nq + kv_lo:nq + kv_hi],
+                                       bqkv[nq + nk + kv_lo:nq + nk + kv_hi]]).contiguous()
+                L["bo"] = self._rand(p + "bo", (d,), 0.01)  # added once (rank 0 adds it before the reduce)
+                w1 = self._rand(p + "w1", (c.ffn_dim, d))
+                L["w1"] = w1[f_lo:f_hi].contiguous()
+                L["b1"] = self._rand(p + "b1", (c.ffn_dim,), 0.01)[f_lo:f_hi].contiguous()
+                w2 = self._rand(p + "w2", (d, c.ffn_dim), out_std)
+                L["w2"] = w2[:, f_lo:f_hi].contiguous()
+                L["b2"] = self._rand(p + "b2", (d,), 0.01)
+                del w1, w2
+            else:
+                L["attn_norm"] = self._ones(d)
+                L["mlp_norm"] = self._ones(d)
+                if c.is_moe:
+                    L["router"] = self._rand(p + "router", (c.n_experts, d))
+                    w13, w2s = [], []
+                    for e in range(self.e_lo, self.e_hi):
+                        g = self._rand(p + f"experts.{e}.w1", (c.ffn_dim, d))
+                        u = self._rand(p + f"experts.{e}.w3", (c.ffn_dim, d))
+                        w13.append(torch.cat([g, u], 0))
+                        w2s.append(self._rand(p + f"experts.{e}.w2", (d, c.ffn_dim), out_std))
+                        del g, u
+                    L["w13"] = torch.stack(w13).contiguous()  # [E_local, 2F, d]
+                    L["w2"] = torch.stack(w2s).contiguous()  # [E_local, d, F]
+                    del w13, w2s
+                else:
+                    g = self._rand(p + "w1", (c.ffn_dim, d))
+                    u = self._rand(p + "w3", (c.ffn_dim, d))
+                    L["w13"] = torch.cat([g[f_lo:f_hi], u[f_lo:f_hi]], 0).contiguous()
+                    del g, u
+                    w2 = self._rand(p + "w2", (d, c.ffn_dim), out_std)
+                    L["w2"] = w2[:, f_lo:f_hi].contiguous()
+                    del w2
+            self.layers.append(L)
+
+    def num_local_params(self) -> int:
+        n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
+        for L in self.layers:
+            for v in L.values():
+                if isinstance(v, tuple):
+                    n += sum(t.numel() for t in v)
+                else:
+                    n += v.numel()
+        return n
+
+    # ------------------------------------------------------------------ forward
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.tp == 1:
+            if ids.is_cuda:
+                return ops.embedding(ids, self.embed)
+            return self.embed[ids.long()]
+        x = ops.embedding(ids, self.embed, vocab_start=self.v_lo)
+        return tp_all_reduce(x)
+
+    def _attention(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv) -> torch.Tensor:
+        c = self.cfg
+        qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
+        k_cache, v_cache = kv if kv is not None else (None, None)
+        ops.rope_and_cache(qkv, meta.positions, self.cos_sin if self.cos_sin is not None else _dummy_cs(self),
+                           k_cache, v_cache, meta.slot_mapping if k_cache is not None else None,
+                           self.hq, self.hkv, self.D,
+                           apply_rope=c.arch == "llama")
+        if meta.is_prefill:
+            qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
+            o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb)
+        else:
+            o = ops.paged_decode(qkv, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.hq, self.hkv,
+                                 self.D, self.scale, workspace=meta.decode_ws)
+        y = F.linear(o, L["wo"])
+        if "bo" in L and self.rank == 0:
+            y += L["bo"]
+        return tp_all_reduce(y)
+
+    def _mlp(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        c = self.cfg
+        if c.arch == "gpt2":
+            h = ops.gelu_tanh(F.linear(x, L["w1"], L["b1"]))
+            y = F.linear(h, L["w2"])
+            if self.rank == 0:
+                y += L["b2"]
+            return tp_all_reduce(y)
+        if c.is_moe:
+            return tp_all_reduce(self._moe(L, x, meta))
+        h = ops.silu_mul(F.linear(x, L["w13"]))
+        return tp_all_reduce(F.linear(h, L["w2"]))
+
+    def _moe(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        """Top-k MoE over this rank's experts [e_lo, e_hi).  Prefill: tokens are sorted by expert
+        (moe_align) and each local expert runs one GEMM pair on its contiguous rows.  Decode: the
+        dense-masked form (every local expert on every token, scaled by its routing weight, 0 if
+        not selected) - no host sync, so the decode step stays graph-capturable; at decode batch
+        sizes the step is bound by reading every expert's weights either way."""
+        c = self.cfg
+        T = x.shape[0]
+        K = c.top_k_experts
+        logits = F.linear(x, L["router"]).float()
+        ids, w = ops.moe_route(logits, K, True)
+        if not meta.is_prefill:
+            wd = torch.zeros(T, c.n_experts, dtype=torch.float32, device=x.device)
+            wd.scatter_(1, ids.long(), w)
+            out = torch.zeros(T, c.d_model, dtype=torch.float32, device=x.device)
+            for j, e in enumerate(range(self.e_lo, self.e_hi)):
+                h = ops.silu_mul(F.linear(x, L["w13"][j]))
+                out += F.linear(h, L["w2"][j]).float() * wd[:, e:e + 1]
+            return out.to(x.dtype)
+        offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
+        xs = ops.gather_rows(x, sorted_idx, K)
+        ys = torch.zeros_like(xs)
+        off = offsets.tolist()  # one host sync per MoE layer in prefill
+        for j, e in enumerate(range(self.e_lo, self.e_hi)):
+            a, b = off[e], off[e + 1]
+            if b > a:
+                h = ops.silu_mul(F.linear(xs[a:b], L["w13"][j]))
+                ys[a:b] = F.linear(h, L["w2"][j])
+        return ops.moe_combine(ys, inv_idx, w, T)
+
+    def _norm(self, x: torch.Tensor, w) -> torch.Tensor:
+        if isinstance(w, tuple):
+            return ops.layer_norm(x, w[0], w[1], self.cfg.norm_eps)
+        return ops.rms_norm(x, w, self.cfg.norm_eps)
+
+    def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches: Optional[list] = None) -> torch.Tensor:
+        """Returns logits [rows, vocab_size] for the rows selected by ``meta.logits_idx`` (all rows
+        when None)."""
+        c = self.cfg
+        h = self.embed_tokens(ids)
+        if c.arch == "gpt2":
+            h = h + self.pos_embed[meta.positions.long()]
+            residual = h
+            for i, L in enumerate(self.layers):
+                kv = kv_caches[i] if kv_caches is not None else None
+                residual = residual + self._attention(L, self._norm(residual, L["ln1"]), meta, kv)
+                residual = residual + self._mlp(L, self._norm(residual, L["ln2"]), meta)
+            x = residual
+            if meta.logits_idx is not None:
+                x = x[meta.logits_idx]
+            x = self._norm(x, self.final_norm)
+        else:
+            residual = h
+            x = ops.rms_norm(h, self.layers[0]["attn_norm"], c.norm_eps)
+            n = len(self.layers)
+            for i, L in enumerate(self.layers):
+                kv = kv_caches[i] if kv_caches is not None else None
+                y = self._attention(L, x, meta, kv)
+                x = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
+                y = self._mlp(L, x, meta)
+                if i + 1 < n:
+                    x = ops.fused_add_rms_norm(y, residual, self.layers[i + 1]["attn_norm"], c.norm_eps)
+                else:
+                    if meta.logits_idx is not None:
+                        y = y[meta.logits_idx]
+                        residual = residual[meta.logits_idx].contiguous()
+                    x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
+        logits = F.linear(x, self.lm_head)
+        logits = tp_all_gather_last(logits)
+        if self.vocab_padded != c.vocab_size:
+            logits = logits[:, : c.vocab_size]
+        return logits
+
+
+_DUMMY_CS: dict = {}
+
+
+def _dummy_cs(m: CausalLM) -> torch.Tensor:
+    k = (m.device, m.D)
+    if k not in _DUMMY_CS:
+        _DUMMY_CS[k] = torch.zeros(1, m.D, dtype=torch.float32, device=m.device)
+    return _DUMMY_CS[k]

@@ -195,7 +195,8 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None, top
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Next tokens [B] int32.  temperature <= 0 (or None) is greedy."""
     if not _gpu(logits):
-        return _sample_cpu(logits, temperature, top_k, top_p, rng)
+        r = _sample_cpu(logits, temperature, top_k, top_p, rng)
+        return out.copy_(r) if out is not None else r
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
     native().sample(out, logits, temperature, top_k, top_p, rng)

@@ -1,0 +1,76 @@
+"""Tensor-parallel collectives.
+
+Every function is a no-op at tp_size 1 and is safe inside a hipGraph capture (RCCL collectives
+are capturable on the current stream).  Message sizes at Llama-3-70B TP=8 decode are
+[B, 8192] bf16 (1 MiB at B=64): latency-bound on xGMI, so the engine issues exactly two per
+layer and never splits them into buckets.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .state import get_state
+
+
+def tp_all_reduce(x: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum over the TP group (C-1 / C-2 / C-3)."""
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group or st.tp_group)
+    return x
+
+
+def tp_all_gather_last(x: torch.Tensor, group=None) -> torch.Tensor:
+    """Concatenate the last dim across the TP group, rank order (C-4: vocab-parallel logits)."""
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=group or st.tp_group)
+    return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
+
+
+def tp_broadcast_object(obj, src_tp_rank: int = 0):
+    """Broadcast a picklable control message (the step schedule, C-6) from the TP leader over the
+    CPU gloo group."""
+    st = get_state()
+    if st.tp_size == 1:
+        return obj
+    lst = [obj]
+    src = st.rank - st.tp_rank + src_tp_rank
+    dist.broadcast_object_list(lst, src=src, group=st.cpu_group)
+    return lst[0]
+
+
+def shard_range(n: int, parts: int, idx: int) -> tuple[int, int]:
+    """Contiguous shard [lo, hi) of n items; n must divide evenly (TP shapes always do)."""
+    if n % parts != 0:
+        raise ValueError(f"{n} is not divisible by tp_size {parts}")
+    s = n // parts
+    return idx * s, (idx + 1) * s
+
+
+def all_reduce_max_scalar(v: float, group: Optional[object] = None) -> float:
+    """Max of a host float over the whole world (bench timing: max over ranks)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return v
+    st = get_state()
+    dev = st.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def all_reduce_sum_scalar(v: float, group: Optional[object] = None) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return v
+    st = get_state()
+    dev = st.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t.item())

@@ -1,0 +1,123 @@
+"""Process-group state: one process per GPU, ``torch.distributed`` over RCCL (backend ``"nccl"``
+is RCCL on ROCm) for device tensors and gloo for CPU tensors / control messages.
+
+Layout of the world:
+
+* ``tp``  - tensor-parallel group: Megatron column/row-parallel linears, vocab-parallel embedding
+            and LM head; two all-reduces per layer.  On an 8-GPU MI355X node every pair of GPUs
+            has its own xGMI link, so TP=8 is a full mesh; RCCL rings are per-link bound, which is
+            why decode-sized all-reduces (<= 1 MiB) stay latency-bound and bucket sizes are chosen
+            per call site, not globally.
+* ``dp``  - independent engine replicas (``world // tp``).  No collectives on the hot path; the
+            control plane routes requests round-robin.
+* ``ep``  - expert parallel for Mixtral shares the TP group: attention activations are already
+            replicated across it, so each rank runs its local experts on the tokens routed to
+            them and the partial outputs are summed by the same all-reduce the dense MLP uses.
+
+The reference has no GPU communication at all (SURVEY.md §2.11 "There is no NCCL, MPI, Gloo").
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    tp_group: Optional[object] = None  # device collectives (RCCL on GPU, gloo on CPU)
+    cpu_group: Optional[object] = None  # gloo group spanning the TP group, for control broadcast
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_tp(self) -> bool:
+        return self.tp_size > 1
+
+    @property
+    def tp_leader(self) -> bool:
+        return self.tp_rank == 0
+
+
+_STATE = ParallelState()
+
+
+def get_state() -> ParallelState:
+    return _STATE
+
+
+def set_state(s: ParallelState) -> None:
+    global _STATE
+    _STATE = s
+
+
+def env_world() -> tuple[int, int, int]:
+    """(world_size, rank, local_rank) from torchrun-style env vars (1, 0, 0 when absent)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    lr = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, lr
+
+
+def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optional[str] = None,
+                  timeout_s: float = 600.0) -> ParallelState:
+    """Initialise torch.distributed (if WORLD_SIZE > 1) and carve the TP / DP groups.
+
+    ``device`` defaults to ``cuda:<local_rank>`` when a GPU is visible, else CPU (gloo).
+    """
+    import datetime
+
+    ws, rank, lr = env_world()
+    if device is None:
+        device = f"cuda:{lr}" if torch.cuda.is_available() else "cpu"
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    if tp_size < 1 or ws % tp_size != 0:
+        raise ValueError(f"tp_size={tp_size} must divide world_size={ws}")
+    st = ParallelState(world_size=ws, rank=rank, local_rank=lr, tp_size=tp_size, tp_rank=rank % tp_size,
+                       dp_size=ws // tp_size, dp_rank=rank // tp_size, device=dev)
+    if ws > 1:
+        if not dist.is_initialized():
+            be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            kw = {}
+            if be == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(be, rank=rank, world_size=ws,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        be = dist.get_backend()
+        # every rank must create every group, in the same order
+        for g in range(ws // tp_size):
+            ranks = list(range(g * tp_size, (g + 1) * tp_size))
+            grp = dist.new_group(ranks) if tp_size > 1 else None
+            cpu = dist.new_group(ranks, backend="gloo") if (tp_size > 1 and be != "gloo") else grp
+            if rank in ranks:
+                st.tp_group, st.cpu_group = grp, cpu
+    set_state(st)
+    return st
+
+
+def barrier_all() -> None:
+    if dist.is_available() and dist.is_initialized():
+        st = get_state()
+        if st.device.type == "cuda" and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[st.device.index])
+        else:
+            dist.barrier()
+
+
+def destroy() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    set_state(ParallelState())
