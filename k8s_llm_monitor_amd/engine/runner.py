@@ -68,7 +68,7 @@ class ModelRunner:
         self.d_topp = torch.ones(B, dtype=torch.float32, device=dev)
         self.rng = torch.tensor([cfg.seed, 0], dtype=torch.int64, device=dev)
         self.d_out = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev) \
+        self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev, model.hkv) \
             if self.is_gpu else None
         # pinned host staging
         pin = self.is_gpu

@@ -135,29 +135,43 @@ def _empty_i32(device) -> torch.Tensor:
     return t
 
 
-PARTITION = 256  # tokens per decode partition (must match paged_decode.hip kPT)
+MAX_SPLITS = 64
 
 
-def decode_workspace(max_batch: int, Hq: int, D: int, max_model_len: int, device) -> tuple[torch.Tensor, torch.Tensor]:
-    np_ = max(1, (max_model_len + PARTITION - 1) // PARTITION)
-    part_out = torch.empty(max_batch, Hq, np_, D, dtype=torch.float32, device=device)
-    part_ml = torch.empty(max_batch, Hq, np_, 2, dtype=torch.float32, device=device)
+def decode_splits(batch: int, Hkv: int, n_cu: int = 256) -> int:
+    """Splits per (sequence, kv head) for paged_decode: aim for ~one workgroup per CU in total.
+
+    Measured on MI355X (tools/bench_decode.py, ctx 1.8k-6k): batch 64 x 8 kv heads is best
+    unsplit (83 us, 5.7 TB/s - a merge launch and extra partial traffic only cost), batch 8 at 4
+    splits, batch 1 at 16-32 splits."""
+    env = os.environ.get("K8SLLM_DECODE_SPLITS")
+    if env:
+        return max(1, min(MAX_SPLITS, int(env)))
+    return max(1, min(32, round(n_cu / max(1, batch * Hkv))))
+
+
+def decode_workspace(max_batch: int, Hq: int, D: int, max_model_len: int = 0, device=None, Hkv: Optional[int] = None):
+    """fp32 partials of the split-K decode kernel: [B, Hq, MAX_SPLITS, D] and [.., 2]."""
+    part_out = torch.empty(max_batch, Hq, MAX_SPLITS, D, dtype=torch.float32, device=device)
+    part_ml = torch.empty(max_batch, Hq, MAX_SPLITS, 2, dtype=torch.float32, device=device)
     return part_out, part_ml
 
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  seq_lens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
-                 workspace: Optional[tuple] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 workspace: Optional[tuple] = None, out: Optional[torch.Tensor] = None,
+                 splits: Optional[int] = None) -> torch.Tensor:
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale)
         return out.copy_(r) if out is not None else r
     B = seq_lens.shape[0]
     if workspace is None:
-        workspace = decode_workspace(B, Hq, D, block_tables.shape[1] * k_cache.shape[3], q.device)
+        workspace = decode_workspace(B, Hq, D, device=q.device)
     if out is None:
         out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
+    S = splits or decode_splits(B, Hkv)
     native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, workspace[0], workspace[1],
-                          Hq, Hkv, D, scale)
+                          Hq, Hkv, D, scale, S)
     return out
 
 

@@ -19,7 +19,7 @@ int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const fl
                       int apply_rope, hipStream_t s);
 int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q, long q_stride,
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
-                        const int* seq_lens, int B, int Hq, int Hkv, int D, int NP, float scale, hipStream_t s);
+                        const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
 int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride, const int* cu_seqlens,
                          const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
                          hipStream_t s);
@@ -130,7 +130,7 @@ void rope_and_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor co
 
 void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                   torch::Tensor block_tables, torch::Tensor seq_lens, torch::Tensor part_out, torch::Tensor part_ml,
-                  int64_t Hq, int64_t Hkv, int64_t D, double scale) {
+                  int64_t Hq, int64_t Hkv, int64_t D, double scale, int64_t splits) {
   dev_bf16(out, "out"); dev_bf16(q, "q"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
   dev_i32(block_tables, "block_tables"); dev_i32(seq_lens, "seq_lens");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "q must be [B, >=Hq*D] rows");
@@ -138,13 +138,13 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
   TORCH_CHECK(k_cache.size(3) == 16 && v_cache.size(3) == 16, "paged_decode expects block_size 16");
   TORCH_CHECK(part_out.scalar_type() == torch::kFloat32 && part_ml.scalar_type() == torch::kFloat32, "partials fp32");
   const int B = (int)seq_lens.size(0);
-  const int NP = (int)part_out.size(2);
-  TORCH_CHECK(part_out.size(0) >= B && part_out.size(1) == Hq && part_out.size(3) == D, "part_out shape");
-  TORCH_CHECK(NP * 256 >= block_tables.size(1) * 16, "too few partitions for the block table width");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "splits must be in [1, 64]");
+  TORCH_CHECK(part_out.numel() >= (int64_t)B * Hq * splits * D && part_ml.numel() >= (int64_t)B * Hq * splits * 2,
+              "decode workspace too small for batch x splits");
   check(k8sllm_paged_decode(out.data_ptr(), out.stride(0), part_out.data_ptr<float>(), part_ml.data_ptr<float>(),
                             q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), (int)block_tables.stride(0), seq_lens.data_ptr<int>(), B,
-                            (int)Hq, (int)Hkv, (int)D, NP, (float)scale, cur()),
+                            (int)Hq, (int)Hkv, (int)D, (int)splits, (float)scale, cur()),
         "paged_decode");
 }
 

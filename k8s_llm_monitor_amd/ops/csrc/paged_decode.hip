@@ -10,27 +10,44 @@
 // score accumulator of two 16-token blocks is, element for element, the B operand of the
 // PV product (token order inside the k-step is permuted identically on both operands).
 //
-// Grid = (partitions of 256 tokens, Hkv, batch); 4 waves x 64 tokens per workgroup.  Each
-// workgroup writes an un-normalised partial (max, sum, O) that paged_decode_reduce merges.
-// Everything is static-shaped so the decode step can be captured in a hipGraph: the
-// partition count comes from the engine's max_model_len and idle partitions exit at once.
+// Work decomposition (measured on MI355X, tools/bench_decode.py):
+//  * grid = (S splits, Hkv, batch) with S chosen per batch size by the host so that the grid is
+//    ~1-4 workgroups per CU - NOT one workgroup per fixed 256-token partition: an empty
+//    workgroup still holds its CU slot for a global-load round trip, and a grid sized for
+//    max_model_len spent 130 us per layer launching empty workgroups at batch 64.
+//  * each workgroup walks its chunks of 256 tokens (4 waves x 64) with an online softmax per
+//    wave; per chunk every wave issues ALL of its K (16 x dwordx4) and V (32 x dwordx2) loads
+//    before the first MFMA (block ids past the sequence end are clamped to a valid block and
+//    masked), i.e. 32 KiB in flight per wave.
+//  * if a sequence's chunks fit one split, that workgroup writes the normalised output;
+//    otherwise each split writes (max, sum, O) partials that paged_decode_reduce_kernel merges
+//    in a second launch (an in-kernel last-arriver merge with agent release/acquire fences
+//    measured 2.3x slower at batch 64 x 1.8k context: every workgroup paid the L2 write-back).
+// Everything is static-shaped so the decode step can be captured in a hipGraph.
 #include "common.h"
 
 namespace k8sllm {
 
 constexpr int kBS = 16;   // tokens per KV-cache block
-constexpr int kPT = 256;  // tokens per partition (workgroup)
+constexpr int kCH = 256;  // tokens per chunk (4 waves x 64)
 
-__device__ __forceinline__ bf16x8 zero_bf16x8() { return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0)); }
+__device__ __forceinline__ void split_range(int seq_len, int S, int split, int* c0, int* c1, int* nvalid) {
+  const int nch = (seq_len + kCH - 1) / kCH;
+  const int per = (nch + S - 1) / S;
+  *c0 = split * per;
+  *c1 = min(nch, *c0 + per);
+  *nvalid = (nch + per - 1) / per;
+}
 
 template <int D, int G>
-__global__ __launch_bounds__(256) void paged_decode_kernel(float* __restrict__ part_out,  // [B][Hq][NP][D]
-                                                           float* __restrict__ part_ml,   // [B][Hq][NP][2]
+__global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ out, long out_stride,
+                                                           float* __restrict__ part_out,  // [B][Hq][S][D]
+                                                           float* __restrict__ part_ml,   // [B][Hq][S][2]
                                                            const bf16_t* __restrict__ q, long q_stride,
                                                            const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int bt_stride,
-                                                           const int* __restrict__ seq_lens, int Hq, int Hkv, int NP,
+                                                           const int* __restrict__ seq_lens, int Hq, int Hkv, int S,
                                                            float scale_log2) {
   constexpr int KS = D / 32;  // QK k-steps
   constexpr int DT = D / 16;  // PV output tiles (16 dims each)
@@ -38,99 +55,126 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(float* __restrict__ p
   __shared__ float s_sum[4][16];
   __shared__ float s_o[4][G][D];
 
-  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int seq_len = seq_lens[b];
-  const int tok0 = part * kPT;
-  if (tok0 >= seq_len) return;  // uniform over the workgroup: no barrier is skipped unevenly
+  if (seq_len <= 0) {  // padding row (graph bucket slack): define the output as zeros
+    if (split == 0)
+      for (int i = threadIdx.x; i < G * D; i += 256) out[(long)b * out_stride + (long)kvh * G * D + i] = 0;
+    return;
+  }
+  int c0, c1, nvalid;
+  split_range(seq_len, S, split, &c0, &c1, &nvalid);
+  if (c0 >= c1) return;  // uniform over the workgroup
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int col = lane & 15, kg = lane >> 4;
-  const int wtok0 = tok0 + wave * 64;
   const int* bt = block_tables + (long)b * bt_stride;
+  const long head_block = (long)D * kBS;  // elements of one (block, head) tile
+  const int nblk = (seq_len + kBS - 1) / kBS;
+  const int first_blk = bt[0];
 
   bf16x8 qf[KS];
-  if (col < G) {
-    const bf16_t* qp = q + (long)b * q_stride + (long)(kvh * G + col) * D;
+  {
+    const int hc = col < G ? col : 0;
+    const bf16_t* qp = q + (long)b * q_stride + (long)(kvh * G + hc) * D;
 #pragma unroll
     for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 32 * s + 8 * kg);
-  } else {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = zero_bf16x8();
   }
 
-  int phys[4];
+  float m = -1e30f, l = 0.f;  // running max / sum of this wave, for head `col`
+  f32x4 oacc[DT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) phys[i] = (wtok0 + 16 * i < seq_len) ? bt[(wtok0 >> 4) + i] : -1;
+  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const long head_block = (long)D * kBS;  // elements of one (block, head) tile
-  f32x4 sacc[4];
+  for (int c = c0; c < c1; ++c) {
+    const int wtok0 = c * kCH + wave * 64;
+    int phys[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    sacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (phys[i] >= 0) {
-      const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block;
+    for (int i = 0; i < 4; ++i) {
+      const int bi = (wtok0 >> 4) + i;
+      phys[i] = bi < nblk ? bt[bi] : first_blk;
+    }
+    // ---- issue every K and V load of this wave's 64 tokens up front
+    bf16x8 kf[4][KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(kb + ((4 * s + kg) * kBS + col) * 8);
-        sacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[s], sacc[i], 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[i][s] = *reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8);
+    }
+    uint2 vlo[2][DT], vhi[2][DT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
+      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        vlo[s][dt] = *reinterpret_cast<const uint2*>(va + 16 * dt * kBS);
+        vhi[s][dt] = *reinterpret_cast<const uint2*>(vb + 16 * dt * kBS);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep every load above: none may wait behind an MFMA
+
+    // ---- scores, online softmax (per lane: head `col`)
+    f32x4 sacc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        sacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[i][s], qf[s], sacc[i], 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = wtok0 + 16 * i + 4 * kg + r;
+        const float v = (t < seq_len) ? sacc[i][r] * scale_log2 : -INFINITY;
+        sacc[i][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = exp2f(m - mnew);
+    float ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sacc[i][r] - mnew);
+        sacc[i][r] = p;
+        ls += p;
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mnew;
+    // ---- P V  (oacc rows are dims, columns are heads: the rescale is per column = per lane)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (__bf16)sacc[2 * s][j];
+        pb[4 + j] = (__bf16)sacc[2 * s + 1][j];
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 a =
+            __builtin_bit_cast(bf16x8, make_uint4(vlo[s][dt].x, vlo[s][dt].y, vhi[s][dt].x, vhi[s][dt].y));
+        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[dt], 0, 0, 0);
       }
     }
   }
 
-  // scale + mask; sacc[i][r] = S[token 4*kg + r of block i][head col]
-  float mx = -1e30f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = wtok0 + 16 * i + 4 * kg + r;
-      const float v = (t < seq_len) ? sacc[i][r] * scale_log2 : -1e30f;
-      sacc[i][r] = v;
-      mx = fmaxf(mx, v);
-    }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  if (lane < 16) s_max[wave][lane] = mx;
-  __syncthreads();
-  const float M = fmaxf(fmaxf(s_max[0][col], s_max[1][col]), fmaxf(s_max[2][col], s_max[3][col]));
-
-  float ls = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = exp2f(sacc[i][r] - M);
-      sacc[i][r] = p;
-      ls += p;
-    }
-  ls += __shfl_xor(ls, 16, 64);
-  ls += __shfl_xor(ls, 32, 64);
-  if (lane < 16) s_sum[wave][lane] = ls;
-
-  f32x4 oacc[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (phys[2 * s] < 0) continue;  // wave-uniform
-    bf16x8 pb;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pb[j] = (__bf16)sacc[2 * s][j];
-      pb[4 + j] = (__bf16)sacc[2 * s + 1][j];
-    }
-    const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg;
-    const bool has_b = phys[2 * s + 1] >= 0;
-    const bf16_t* vb = v_cache + ((long)(has_b ? phys[2 * s + 1] : 0) * Hkv + kvh) * head_block + 4 * kg;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int d = 16 * dt + col;
-      const uint2 lo = *reinterpret_cast<const uint2*>(va + d * kBS);
-      const uint2 hi = has_b ? *reinterpret_cast<const uint2*>(vb + d * kBS) : make_uint2(0, 0);
-      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[dt], 0, 0, 0);
-    }
+  // ---- combine the 4 waves: oacc[dt][r] = O^T[d = 16*dt + 4*kg + r][head col]
+  if (lane < 16) {
+    s_max[wave][lane] = m;
+    s_sum[wave][lane] = l;
   }
-  // oacc[dt][r] = O^T[d = 16*dt + 4*kg + r][head col]
   if (col < G) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -140,57 +184,87 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(float* __restrict__ p
   __syncthreads();
   for (int i = threadIdx.x; i < G * D; i += 256) {
     const int h = i / D, d = i - h * D;
-    const float o = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
-    const long ph = ((long)b * Hq + kvh * G + h) * NP + part;
-    part_out[ph * D + d] = o;
-    if (d == 0) {
-      part_ml[ph * 2] = fmaxf(fmaxf(s_max[0][h], s_max[1][h]), fmaxf(s_max[2][h], s_max[3][h]));
-      part_ml[ph * 2 + 1] = s_sum[0][h] + s_sum[1][h] + s_sum[2][h] + s_sum[3][h];
+    const float M = fmaxf(fmaxf(s_max[0][h], s_max[1][h]), fmaxf(s_max[2][h], s_max[3][h]));
+    const float w0 = exp2f(s_max[0][h] - M), w1 = exp2f(s_max[1][h] - M);
+    const float w2 = exp2f(s_max[2][h] - M), w3 = exp2f(s_max[3][h] - M);
+    const float o = w0 * s_o[0][h][d] + w1 * s_o[1][h][d] + w2 * s_o[2][h][d] + w3 * s_o[3][h][d];
+    const float L = w0 * s_sum[0][h] + w1 * s_sum[1][h] + w2 * s_sum[2][h] + w3 * s_sum[3][h];
+    if (nvalid == 1) {
+      out[(long)b * out_stride + (long)(kvh * G + h) * D + d] = f2bf(o / L);
+    } else {
+      const long ph = ((long)b * Hq + kvh * G + h) * S + split;
+      part_out[ph * D + d] = o;
+      if (d == 0) {
+        part_ml[ph * 2] = M;
+        part_ml[ph * 2 + 1] = L;
+      }
     }
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(D) void paged_decode_reduce_kernel(bf16_t* __restrict__ out, long out_stride,
-                                                                const float* __restrict__ part_out,
-                                                                const float* __restrict__ part_ml,
-                                                                const int* __restrict__ seq_lens, int Hq, int NP) {
-  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+// Second launch: merge the split partials.  One workgroup per (kv head, sequence); the (m, l)
+// of all splits are read in one parallel step, then every thread sums its (head, dim) items with
+// independent loads.  Sequences whose chunks fit one split were finished by the main kernel.
+template <int D, int G>
+__global__ __launch_bounds__(256) void paged_decode_reduce_kernel(bf16_t* __restrict__ out, long out_stride,
+                                                                  const float* __restrict__ part_out,
+                                                                  const float* __restrict__ part_ml,
+                                                                  const int* __restrict__ seq_lens, int Hq, int S) {
+  __shared__ float s_w[G][64];
+  const int kvh = blockIdx.x, b = blockIdx.y;
   const int seq_len = seq_lens[b];
-  const int n = (seq_len + kPT - 1) / kPT;
-  bf16_t* o = out + (long)b * out_stride + (long)h * D + d;
-  if (n <= 0) {
-    *o = 0;
-    return;
+  if (seq_len <= 0) return;
+  int c0, c1, nvalid;
+  split_range(seq_len, S, 0, &c0, &c1, &nvalid);
+  if (nvalid <= 1) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int h = wave; h < G; h += 4) {
+    const long ph = ((long)b * Hq + kvh * G + h) * S;
+    const float mp = lane < nvalid ? part_ml[(ph + lane) * 2] : -1e30f;
+    const float lp = lane < nvalid ? part_ml[(ph + lane) * 2 + 1] : 0.f;
+    const float mm = wave_max(mp);
+    const float w = lane < nvalid ? exp2f(mp - mm) : 0.f;
+    const float lw = wave_sum(w * lp);
+    s_w[h][lane] = w / lw;
   }
-  const long ph = ((long)b * Hq + h) * NP;
-  float M = -1e30f;
-  for (int p = 0; p < n; ++p) M = fmaxf(M, part_ml[(ph + p) * 2]);
-  float acc = 0.f, L = 0.f;
-  for (int p = 0; p < n; ++p) {
-    const float w = exp2f(part_ml[(ph + p) * 2] - M);
-    L += w * part_ml[(ph + p) * 2 + 1];
-    acc += w * part_out[(ph + p) * D + d];
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += 256) {
+    const int h = i / D, d = i - h * D;
+    const float* po = part_out + ((long)b * Hq + kvh * G + h) * S * D + d;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int p = 0;
+    for (; p + 4 <= nvalid; p += 4) {
+      a0 += s_w[h][p] * po[(long)p * D];
+      a1 += s_w[h][p + 1] * po[(long)(p + 1) * D];
+      a2 += s_w[h][p + 2] * po[(long)(p + 2) * D];
+      a3 += s_w[h][p + 3] * po[(long)(p + 3) * D];
+    }
+    for (; p < nvalid; ++p) a0 += s_w[h][p] * po[(long)p * D];
+    out[(long)b * out_stride + (long)(kvh * G + h) * D + d] = f2bf((a0 + a1) + (a2 + a3));
   }
-  *o = f2bf(acc / L);
 }
 
 }  // namespace k8sllm
 
 using namespace k8sllm;
 
+// S = number of splits per (sequence, kv head); part buffers hold [B][Hq][S][D].
 extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q,
                                    long q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
-                                   int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int NP,
+                                   int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int S,
                                    float scale, hipStream_t s) {
   if (B <= 0) return 0;
+  if (S < 1 || S > 64) return -2;
   const int G = Hq / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid(NP, Hkv, B), blk(256);
-#define K8S_DEC(DD, GG)                                                                                         \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, blk, 0, s, part_out, part_ml, (const bf16_t*)q,       \
-                     q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, \
-                     Hq, Hkv, NP, sl2)
+  dim3 grid(S, Hkv, B), blk(256);
+#define K8S_DEC(DD, GG)                                                                                              \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, part_ml,    \
+                     (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,       \
+                     bt_stride, seq_lens, Hq, Hkv, S, sl2);                                                          \
+  if (S > 1)                                                                                                         \
+    hipLaunchKernelGGL((paged_decode_reduce_kernel<DD, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,      \
+                       part_out, part_ml, seq_lens, Hq, S);
   if (D == 128) {
     switch (G) {
       case 1: K8S_DEC(128, 1); break;
@@ -200,8 +274,6 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
       case 16: K8S_DEC(128, 16); break;
       default: return -1;
     }
-    hipLaunchKernelGGL((paged_decode_reduce_kernel<128>), dim3(Hq, B), dim3(128), 0, s, (bf16_t*)out, out_stride,
-                       part_out, part_ml, seq_lens, Hq, NP);
   } else if (D == 64) {
     switch (G) {
       case 1: K8S_DEC(64, 1); break;
@@ -210,8 +282,6 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
       case 8: K8S_DEC(64, 8); break;
       default: return -1;
     }
-    hipLaunchKernelGGL((paged_decode_reduce_kernel<64>), dim3(Hq, B), dim3(64), 0, s, (bf16_t*)out, out_stride,
-                       part_out, part_ml, seq_lens, Hq, NP);
   } else {
     return -1;
   }

@@ -93,9 +93,11 @@ def test_rope_and_cache(hq, hkv, d):
     assert torch.equal(vc.cpu(), vc0), "v_cache"
 
 
+@pytest.mark.parametrize("splits", [None, 1, 3, 16])
 @pytest.mark.parametrize("B,hq,hkv,d,maxlen", [(1, 32, 8, 128, 33), (8, 32, 8, 128, 1100), (64, 32, 8, 128, 700),
-                                                (3, 64, 8, 128, 2000), (5, 8, 8, 128, 300), (4, 16, 4, 64, 513)])
-def test_paged_decode(B, hq, hkv, d, maxlen):
+                                                (3, 64, 8, 128, 2000), (5, 8, 8, 128, 300), (4, 16, 4, 64, 513),
+                                                (2, 64, 8, 128, 5000)])
+def test_paged_decode(B, hq, hkv, d, maxlen, splits):
     bs = 16
     max_blocks = (maxlen + bs - 1) // bs + 1
     nb = B * max_blocks + 4
@@ -106,7 +108,7 @@ def test_paged_decode(B, hq, hkv, d, maxlen):
     bt = perm.to(DEV)
     q = torch.randn(B, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)  # q inside fused rows
     scale = 1.0 / math.sqrt(d)
-    y = ops.paged_decode(q, kc, vc, bt, lens.to(DEV), hq, hkv, d, scale)
+    y = ops.paged_decode(q, kc, vc, bt, lens.to(DEV), hq, hkv, d, scale, splits=splits)
     r = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), perm, lens, hq, hkv, d, scale)
     _close(y, r.to(DEV), atol=2e-2, rtol=2e-2, what="paged_decode")
 
