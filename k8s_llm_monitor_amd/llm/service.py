@@ -1,0 +1,264 @@
+"""The analysis engine the reference only planned (``internal/llm``, docs/development-guide.md:39-64).
+
+``AnalysisService`` turns questions and ``AnalysisRequest``s (types ``pod_communication`` |
+``anomaly_detection`` | ``root_cause``, pkg/models/models.go:86-90) into ``AnalysisResponse``
+records (models.go:93-99) using a text-generation backend:
+
+* ``LocalEngineBackend`` - the in-process PyTorch-ROCm engine (``llm.provider: local-rocm``):
+  continuous batching across concurrent HTTP requests, hipGraph decode, HIP kernels;
+* ``OpenAIBackend``      - the reference's intended remote call (``provider: openai``,
+  ``OPENAI_API_KEY``/``OPENAI_BASE_URL``, config.go:141-182), an OpenAI-compatible
+  ``/chat/completions`` POST with ``llm.timeout``;
+* ``RuleBackend``        - no model: a deterministic summary of the rule findings (dev mode).
+
+Records are kept by ``RecordStore`` (``storage.type: memory`` ring buffer, or ``file`` JSON lines;
+the reference's redis/postgres settings are accepted but unsupported offline).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import threading
+import time
+import urllib.request
+import uuid
+from collections import OrderedDict
+from typing import Optional
+
+from ..monitor.types import AnalysisRequest, AnalysisResponse
+from ..utils import gojson
+from ..utils.gojson import utcnow
+from . import prompt as P
+
+log = logging.getLogger("llm")
+
+
+class GenResult(dict):
+    """{text, prompt_tokens, completion_tokens, latency_ms, ttft_ms, model, provider}"""
+
+
+class LocalEngineBackend:
+    provider = "local-rocm"
+
+    def __init__(self, service, max_tokens: int = 2000, temperature: float = 0.1, top_p: float = 1.0,
+                 top_k: int = 0, timeout_s: float = 30.0):
+        from ..engine import SamplingParams
+
+        self.svc = service
+        self.model = service.engine.model_cfg.name
+        self.default = SamplingParams(max_tokens=max_tokens, temperature=temperature, top_p=top_p, top_k=top_k)
+        self.timeout_s = timeout_s
+        self.tokenizer = service.engine.tokenizer
+
+    def count_tokens(self, text: str) -> int:
+        return len(self.tokenizer.encode(text, bos=False))
+
+    def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
+                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+        from ..engine import SamplingParams
+
+        d = self.default
+        p = SamplingParams(max_tokens=max_tokens or d.max_tokens,
+                           temperature=d.temperature if temperature is None else temperature,
+                           top_k=d.top_k, top_p=d.top_p, ignore_eos=ignore_eos)
+        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id)
+        text, seq = fut.result(timeout=self.timeout_s if self.timeout_s > 0 else None)
+        t = seq.timings()
+        return GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason, **t)
+
+
+class OpenAIBackend:
+    provider = "openai"
+
+    def __init__(self, api_key: str, base_url: str, model: str, max_tokens: int, temperature: float, timeout_s: float):
+        self.api_key, self.model = api_key, model
+        self.base_url = (base_url or "https://api.openai.com/v1").rstrip("/")
+        self.max_tokens, self.temperature, self.timeout_s = max_tokens, temperature, timeout_s
+
+    def count_tokens(self, text: str) -> int:
+        return max(1, len(text.encode()) // 3)
+
+    def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
+                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+        if not self.api_key:
+            raise RuntimeError("llm.api_key / OPENAI_API_KEY not configured")
+        body = json.dumps({"model": self.model, "max_tokens": max_tokens or self.max_tokens,
+                           "temperature": self.temperature if temperature is None else temperature,
+                           "messages": [{"role": "system", "content": P.SYSTEM_PREAMBLE},
+                                        {"role": "user", "content": prompt}]}).encode()
+        req = urllib.request.Request(self.base_url + "/chat/completions", data=body, method="POST",
+                                     headers={"Content-Type": "application/json",
+                                              "Authorization": f"Bearer {self.api_key}"})
+        t0 = time.perf_counter()
+        with urllib.request.urlopen(req, timeout=self.timeout_s) as r:
+            d = json.loads(r.read())
+        usage = d.get("usage") or {}
+        return GenResult(text=d["choices"][0]["message"]["content"], model=self.model, provider=self.provider,
+                         prompt_tokens=usage.get("prompt_tokens"), completion_tokens=usage.get("completion_tokens"),
+                         latency_ms=round((time.perf_counter() - t0) * 1e3, 3), ttft_ms=None,
+                         finish_reason=d["choices"][0].get("finish_reason"))
+
+
+class RuleBackend:
+    provider = "rules"
+    model = "rule-engine"
+
+    def count_tokens(self, text: str) -> int:
+        return max(1, len(text.encode()) // 3)
+
+    def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
+                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+        flagged = [ln.strip() for ln in prompt.splitlines()
+                   if any(k in ln for k in ("[资源压力]", "[不健康]", "状态=", "接近限制", "不通", "告警", "UAV "))]
+        text = ("未发现明显异常。" if not flagged else
+                "规则引擎摘要 (未配置本地模型):\n" + "\n".join(flagged[:50]))
+        return GenResult(text=text, model=self.model, provider=self.provider, prompt_tokens=self.count_tokens(prompt),
+                         completion_tokens=self.count_tokens(text), latency_ms=0.0, ttft_ms=0.0,
+                         finish_reason="stop")
+
+
+class RecordStore:
+    """Analysis records by request id (bounded ring buffer; optional JSON-lines persistence so
+    records survive a restart - the reference keeps nothing, SURVEY.md §5 checkpoint/resume)."""
+
+    def __init__(self, kind: str = "memory", path: str = "", capacity: int = 10000):
+        self.kind, self.capacity = kind, capacity
+        self._d: OrderedDict = OrderedDict()
+        self._lock = threading.Lock()
+        self.path = None
+        if kind == "file":
+            self.path = os.path.join(path or ".", "analysis_records.jsonl")
+            os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+            if os.path.exists(self.path):
+                with open(self.path, encoding="utf-8") as fh:
+                    for line in fh:
+                        try:
+                            d = json.loads(line)
+                            self._d[d["request_id"]] = d
+                        except (ValueError, KeyError):
+                            continue
+        elif kind not in ("memory", ""):
+            log.warning("storage.type %r is not available offline; using memory", kind)
+
+    def put(self, resp: AnalysisResponse) -> None:
+        plain = gojson.to_plain(resp)
+        with self._lock:
+            self._d[resp.request_id] = plain
+            while len(self._d) > self.capacity:
+                self._d.popitem(last=False)
+            if self.path:
+                with open(self.path, "a", encoding="utf-8") as fh:
+                    fh.write(gojson.dumps(resp) + "\n")
+
+    def get(self, rid: str) -> Optional[dict]:
+        with self._lock:
+            return self._d.get(rid)
+
+    def list(self, limit: int = 50) -> list:
+        with self._lock:
+            return list(self._d.values())[-limit:]
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+
+class AnalysisService:
+    def __init__(self, backend, manager=None, client=None, analyzer=None, store: Optional[RecordStore] = None,
+                 max_context_events: int = 100, token_budget: int = 6144, max_tokens: Optional[int] = None):
+        self.backend = backend
+        self.manager = manager
+        self.client = client
+        self.analyzer = analyzer
+        self.store = store or RecordStore()
+        self.max_events = max_context_events
+        self.token_budget = token_budget
+        self.max_tokens = max_tokens
+        self._ctx_cache: tuple = (None, "")
+        self._ctx_lock = threading.Lock()
+
+    # ------------------------------------------------------------------ context
+    def _events(self) -> list:
+        if self.client is None:
+            return []
+        out = []
+        for ns in self.client.namespaces:
+            try:
+                out += self.client.get_events(ns, limit=self.max_events) or []
+            except Exception as e:  # noqa: BLE001
+                log.warning("events for %s unavailable: %s", ns, e)
+        out.sort(key=lambda e: e.timestamp or utcnow())
+        return out[-self.max_events:]
+
+    def cluster_context(self) -> str:
+        if self.manager is None:
+            return "\n(集群指标不可用: metrics manager not available)\n"
+        snap = self.manager.get_latest_snapshot()
+        key = (id(snap), snap.timestamp)
+        with self._ctx_lock:
+            if self._ctx_cache[0] == key:
+                return self._ctx_cache[1]
+        ctx = P.build_cluster_context(snap, self._events(), self.manager.get_uav_metrics(), self.max_events)
+        ctx = P.trim_to_budget(ctx, lambda s: [0] * self.backend.count_tokens(s), self.token_budget)
+        with self._ctx_lock:
+            self._ctx_cache = (key, ctx)
+        return ctx
+
+    # ------------------------------------------------------------------ entry points
+    def _respond(self, rid: str, kind: str, prompt: str, extra: dict, max_tokens: Optional[int] = None,
+                 ignore_eos: bool = False) -> AnalysisResponse:
+        try:
+            g = self.backend.generate(prompt, max_tokens=max_tokens or self.max_tokens, request_id=rid,
+                                      ignore_eos=ignore_eos)
+            result = {"type": kind, "answer": g.pop("text"), **g, **extra}
+            resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
+        except Exception as e:  # noqa: BLE001 - an engine failure becomes an error record, not a 500
+            log.error("analysis %s failed: %s", rid, e)
+            resp = AnalysisResponse(request_id=rid, status="error", result={"type": kind, **extra},
+                                    error=f"{type(e).__name__}: {e}", timestamp=utcnow())
+        self.store.put(resp)
+        return resp
+
+    def query(self, question: str, max_tokens: Optional[int] = None, ignore_eos: bool = False,
+              context_text: Optional[str] = None) -> AnalysisResponse:
+        """POST /api/v1/query (README.md:91-96; not implemented by the reference).  ``context_text``
+        lets a caller supply the cluster state itself (e.g. another collector's snapshot)."""
+        rid = uuid.uuid4().hex
+        ctx = context_text if context_text else self.cluster_context()
+        prompt = P.build_query_prompt(ctx, question)
+        return self._respond(rid, "query", prompt, {"question": question}, max_tokens, ignore_eos)
+
+    def analyze(self, req: AnalysisRequest) -> AnalysisResponse:
+        kind = req.type or "anomaly_detection"
+        params = req.parameters or {}
+        if kind == "pod_communication":
+            a, b = params.get("pod_a"), params.get("pod_b")
+            if not a or not b or self.analyzer is None:
+                raise ValueError("pod_a and pod_b are required" if self.analyzer else "K8s client not available")
+            analysis = self.analyzer.analyze_pod_communication(a, b)
+            return self.explain_pod_communication(analysis)
+        if kind not in ("anomaly_detection", "root_cause"):
+            raise ValueError(f"unknown analysis type: {kind}")
+        prompt = P.build_analysis_prompt(kind, self.cluster_context(), params)
+        return self._respond(uuid.uuid4().hex, kind, prompt, {"parameters": params},
+                             int(params.get("max_tokens") or 0) or None)
+
+    def explain_pod_communication(self, analysis) -> AnalysisResponse:
+        facts = []
+        if self.client is not None:
+            from ..monitor.analysis.network import parse_pod_name
+
+            for ref in (analysis.pod_a, analysis.pod_b):
+                try:
+                    ns, n = parse_pod_name(ref)
+                    p = self.client.get_pod(ns, n)
+                    facts.append(f"- {ns}/{n}: 状态={p.status}, 节点={p.node_name}, IP={p.ip}, 标签={p.labels or {}}")
+                except Exception as e:  # noqa: BLE001
+                    facts.append(f"- {ref}: {e}")
+        rtt = ""
+        last = getattr(self.analyzer, "last_rtt", None)
+        if last is not None:
+            rtt = (f"RTT测试: 成功率 {last.success_rate:.1f}%, 平均 {last.average_rtt:.2f}ms, "
+                   f"评级 {last.latency}\n")
+        prompt = P.build_pod_communication_prompt(analysis, "\n".join(facts), rtt)
+        return self._respond(uuid.uuid4().hex, "pod_communication", prompt, {"analysis": gojson.to_plain(analysis)})

@@ -23,6 +23,12 @@ QUESTIONS = [
 
 
 def synthetic_cluster_prompt(seed: int, n_nodes: int = 16, n_pods: int = 100, question: str | None = None) -> str:
+    ctx, q = synthetic_context(seed, n_nodes, n_pods, question)
+    return f"\n基于以下Kubernetes集群指标数据:\n\n{ctx}\n\n请回答用户问题: {q}\n"
+
+
+def synthetic_context(seed: int, n_nodes: int = 16, n_pods: int = 100, question: str | None = None) -> tuple[str, str]:
+    """(cluster-context text, question) - the two parts /api/v1/query combines."""
     r = random.Random(seed)
     healthy = sum(1 for _ in range(n_nodes) if r.random() > 0.1)
     running = int(n_pods * r.uniform(0.8, 0.97))
@@ -60,5 +66,4 @@ def synthetic_cluster_prompt(seed: int, n_nodes: int = 16, n_pods: int = 100, qu
             if r.random() < 0.3:
                 lines.append(f"- {name}: 资源使用接近限制")
     ctx = "\n".join(lines) + "\n"
-    q = question or QUESTIONS[seed % len(QUESTIONS)]
-    return f"\n基于以下Kubernetes集群指标数据:\n\n{ctx}\n\n请回答用户问题: {q}\n"
+    return ctx, question or QUESTIONS[seed % len(QUESTIONS)]

@@ -1,0 +1,186 @@
+"""Process assembly for the ``server`` binary (``cmd/server/main.go:23-172``):
+config -> cluster client (development-mode fallback) -> metrics manager -> LLM engine ->
+analysis service -> REST app.
+
+Cluster backend selection (``k8s.backend``, new): ``kube`` (REST client: kubeconfig or in-cluster
+service account), ``fake`` (the deterministic FakeCluster), ``none`` (development mode), ``auto``
+(kube if a kubeconfig / in-cluster token exists, else development mode - the reference's
+behaviour when it cannot reach a cluster, main.go:43-51).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import threading
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+from .config import Config
+
+log = logging.getLogger("server")
+
+
+@dataclass
+class Monitor:
+    cfg: Config
+    backend: object = None
+    client: object = None
+    manager: object = None
+    engine: object = None
+    engine_service: object = None
+    analysis: object = None
+    app: object = None
+    fake: object = None
+
+    def close(self) -> None:
+        if self.manager is not None and self.manager.running:
+            self.manager.stop()
+        if self.engine_service is not None:
+            self.engine_service.close()
+
+
+def make_backend(cfg: Config, fake_seed: int = 0):
+    kind = (cfg.k8s.backend or "auto").lower()
+    if kind == "none":
+        return None
+    if kind == "fake":
+        from .cluster.fake import FakeCluster
+
+        n = int(os.environ.get("FAKE_CLUSTER_NODES", "3"))
+        p = int(os.environ.get("FAKE_CLUSTER_PODS_PER_NODE", "4"))
+        return FakeCluster.build(seed=fake_seed, n_nodes=n, pods_per_node=p)
+    from .cluster.kube import KubeRESTBackend, KubeConfigError
+
+    try:
+        return KubeRESTBackend.from_config(cfg.k8s.kubeconfig)
+    except KubeConfigError as e:
+        if kind == "kube":
+            raise
+        log.warning("Failed to create k8s client: %s", e)
+        return None
+
+
+def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):
+    """Returns (backend, engine, engine_service)."""
+    from ..llm.service import LocalEngineBackend, OpenAIBackend, RuleBackend
+
+    prov = (cfg.llm.provider or "").lower()
+    if prov in ("local-rocm", "local", "rocm"):
+        from ..engine import EngineConfig, EngineService, LLMEngine
+
+        ecfg = EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch, max_model_len=cfg.llm.max_model_len,
+                            kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
+                            tp_size=cfg.llm.tp_size)
+        eng = LLMEngine(ecfg, device=device, pstate=pstate)
+        eng.warmup()
+        svc = EngineService(eng)
+        return (LocalEngineBackend(svc, cfg.llm.max_tokens, cfg.llm.temperature, cfg.llm.top_p, cfg.llm.top_k,
+                                   timeout_s=float(cfg.llm.timeout)), eng, svc)
+    if prov == "openai":
+        return OpenAIBackend(cfg.llm.api_key, cfg.llm.base_url, cfg.llm.model, cfg.llm.max_tokens,
+                             cfg.llm.temperature, float(cfg.llm.timeout)), None, None
+    return RuleBackend(), None, None
+
+
+def build_monitor(cfg: Config, backend=None, start_manager: bool = True, llm: bool = True, pstate=None,
+                  device: Optional[str] = None) -> Monitor:
+    from ..llm.service import AnalysisService, RecordStore, RuleBackend
+    from .analysis.network import RTTTester
+    from .cluster.client import K8sClient
+    from .metrics.manager import ManagerConfig, MetricsManager
+    from .server import MonitorApp
+
+    m = Monitor(cfg=cfg)
+    log.info("Starting K8s LLM Monitor...")
+    log.info("Server: %s:%d", cfg.server.host, cfg.server.port)
+    log.info("K8s Namespace: %s", cfg.k8s.namespace)
+    log.info("LLM Provider: %s", cfg.llm.provider)
+    m.backend = backend if backend is not None else make_backend(cfg)
+    if m.backend is not None:
+        client = K8sClient(m.backend, cfg.k8s)
+        try:
+            v = client.test_connection()
+            m.client = client
+            log.info("Successfully connected to Kubernetes cluster: %s", v)
+        except Exception as e:  # noqa: BLE001
+            log.warning("Failed to connect to k8s: %s", e)
+            log.warning("Running in development mode without K8s connection")
+    else:
+        log.warning("Running in development mode without K8s connection")
+    if m.client is not None and cfg.metrics.enabled:
+        mc = ManagerConfig(namespaces=list(cfg.metrics.namespaces) or ["default"],
+                           collect_interval_s=float(cfg.metrics.collect_interval or 30),
+                           enable_node=cfg.metrics.enable_node, enable_pod=cfg.metrics.enable_pod,
+                           enable_network=cfg.metrics.enable_network, enable_custom=cfg.metrics.enable_custom,
+                           enable_uav=True, network_max_pairs=5, network_test_timeout_s=10.0)
+        m.manager = MetricsManager(m.backend, mc, RTTTester(m.client))
+        if start_manager:
+            m.manager.start()
+            log.info("Metrics collection started (interval: %d seconds)", cfg.metrics.collect_interval)
+    if llm:
+        backend_llm, m.engine, m.engine_service = make_llm_backend(cfg, pstate=pstate, device=device)
+    else:
+        backend_llm = RuleBackend()
+    analyzer = None
+    m.analysis = AnalysisService(backend_llm, manager=m.manager, client=m.client, analyzer=None,
+                                 store=RecordStore(cfg.storage.type, cfg.storage.path),
+                                 max_context_events=cfg.analysis.max_context_events,
+                                 token_budget=cfg.analysis.prompt_token_budget, max_tokens=cfg.llm.max_tokens)
+    m.app = MonitorApp(m.client, m.manager, m.analysis, m.engine_service, llm_timeout_s=float(cfg.llm.timeout))
+    m.analysis.analyzer = m.app.analyzer if analyzer is None else analyzer
+    return m
+
+
+# --------------------------------------------------------------------------- bench helpers
+
+def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0):
+    """An HTTP server in this process whose /api/v1/query is served by ``engine_service``
+    (FakeCluster behind it, metrics collected once).  Returns (server, port)."""
+    from ..llm.service import AnalysisService, LocalEngineBackend
+    from .cluster.fake import FakeCluster
+    from .cluster.client import K8sClient
+    from .config import from_dict
+    from .metrics.manager import ManagerConfig, MetricsManager
+    from .server import MonitorApp, make_server
+
+    cfg = from_dict({"metrics": {"namespaces": ["default", "kube-system"]}})
+    fake = FakeCluster.build(seed=0)
+    client = K8sClient(fake, cfg.k8s)
+    mgr = MetricsManager(fake, ManagerConfig(namespaces=["default", "kube-system"]))
+    mgr.collect()
+    backend = LocalEngineBackend(engine_service, max_tokens=2000, temperature=0.1, timeout_s=600.0)
+    analysis = AnalysisService(backend, manager=mgr, client=client)
+    app = MonitorApp(client, mgr, analysis, engine_service, write_timeout_s=600.0, llm_timeout_s=600.0)
+    analysis.analyzer = app.analyzer
+    srv = make_server(app, host, port)
+    threading.Thread(target=srv.serve_forever, name="bench-http", daemon=True).start()
+    return srv, srv.server_address[1]
+
+
+def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0.0.1",
+                 concurrency: Optional[int] = None) -> list:
+    """Fire ``items`` = [(question, context_text)] as concurrent POST /api/v1/query; returns the
+    per-request result dicts (answer, timings)."""
+    import concurrent.futures as cf
+    import http.client
+
+    def one(item):
+        q, ctx = item
+        body = json.dumps({"question": q, "max_tokens": max_new_tokens, "ignore_eos": True,
+                           "context": {"cluster_state": ctx}}).encode()
+        conn = http.client.HTTPConnection(host, port, timeout=900)
+        t0 = time.perf_counter()
+        conn.request("POST", "/api/v1/query", body, {"Content-Type": "application/json"})
+        r = conn.getresponse()
+        data = json.loads(r.read())
+        conn.close()
+        if r.status != 200 or data.get("status") != "success":
+            raise RuntimeError(f"query failed: HTTP {r.status}: {data}")
+        res = data["result"]
+        res["http_latency_ms"] = (time.perf_counter() - t0) * 1e3
+        return res
+
+    with cf.ThreadPoolExecutor(max_workers=concurrency or len(items)) as ex:
+        return list(ex.map(one, items))
