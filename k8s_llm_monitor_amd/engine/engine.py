@@ -118,7 +118,7 @@ class LLMEngine:
         if plan.empty:
             return []
         if self.ps.tp_size > 1:
-            tp_broadcast_object(self._pack(plan))
+            tp_broadcast_object(self._pack(plan), ps=self.ps)
         if plan.is_prefill:
             toks = self.runner.prefill(plan.seqs)
             self.counters["prefill_steps"] += 1
@@ -179,7 +179,7 @@ class LLMEngine:
     def worker_loop(self) -> None:
         """Non-leader TP ranks: mirror the leader's steps until it broadcasts ``None``."""
         while True:
-            msg = tp_broadcast_object(None)
+            msg = tp_broadcast_object(None, ps=self.ps)
             if msg is None:
                 return
             is_prefill, items = msg
@@ -192,7 +192,7 @@ class LLMEngine:
 
     def stop_workers(self) -> None:
         if self.ps.tp_size > 1 and self.is_leader:
-            tp_broadcast_object(None)
+            tp_broadcast_object(None, ps=self.ps)
 
 
 def _params_t(p: SamplingParams) -> tuple:

@@ -190,7 +190,7 @@ class CausalLM:
                 return ops.embedding(ids, self.embed)
             return self.embed[ids.long()]
         x = ops.embedding(ids, self.embed, vocab_start=self.v_lo)
-        return tp_all_reduce(x)
+        return tp_all_reduce(x, self.ps)
 
     def _attention(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv) -> torch.Tensor:
         c = self.cfg
@@ -209,7 +209,7 @@ class CausalLM:
         y = F.linear(o, L["wo"])
         if "bo" in L and self.rank == 0:
             y += L["bo"]
-        return tp_all_reduce(y)
+        return tp_all_reduce(y, self.ps)
 
     def _mlp(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         c = self.cfg
@@ -218,11 +218,11 @@ class CausalLM:
             y = F.linear(h, L["w2"])
             if self.rank == 0:
                 y += L["b2"]
-            return tp_all_reduce(y)
+            return tp_all_reduce(y, self.ps)
         if c.is_moe:
-            return tp_all_reduce(self._moe(L, x, meta))
+            return tp_all_reduce(self._moe(L, x, meta), self.ps)
         h = ops.silu_mul(F.linear(x, L["w13"]))
-        return tp_all_reduce(F.linear(h, L["w2"]))
+        return tp_all_reduce(F.linear(h, L["w2"]), self.ps)
 
     def _moe(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         """Top-k MoE over this rank's experts [e_lo, e_hi).  Prefill: tokens are sorted by expert
@@ -292,7 +292,7 @@ class CausalLM:
                         residual = residual[meta.logits_idx].contiguous()
                     x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
         logits = F.linear(x, self.lm_head)
-        logits = tp_all_gather_last(logits)
+        logits = tp_all_gather_last(logits, self.ps)
         if self.vocab_padded != c.vocab_size:
             logits = logits[:, : c.vocab_size]
         return logits

@@ -27,7 +27,7 @@ from urllib.parse import quote, urlencode, urlparse
 
 import yaml
 
-from .backend import GVR, ApiError, ClusterBackend, ExecError
+from .backend import GVR, KINDS, ApiError, ClusterBackend, ExecError
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
@@ -190,6 +190,8 @@ class KubeRESTBackend(ClusterBackend):
         d = self._request("GET", self._path(gvr, namespace), query=q)
         items = d.get("items") or []
         kind = (d.get("kind") or "").removesuffix("List")
+        if kind in ("", "Table"):
+            kind = KINDS.get(gvr, "")
         for it in items:  # list items carry no apiVersion/kind; restore them like the dynamic client
             it.setdefault("apiVersion", gvr.api_version)
             if kind:

@@ -15,30 +15,33 @@ import torch.distributed as dist
 from .state import get_state
 
 
-def tp_all_reduce(x: torch.Tensor, group=None) -> torch.Tensor:
+def tp_all_reduce(x: torch.Tensor, ps=None) -> torch.Tensor:
     """In-place sum over the TP group (C-1 / C-2 / C-3)."""
-    st = get_state()
+    st = ps or get_state()
     if st.tp_size == 1:
         return x
-    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group or st.tp_group)
+    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=st.tp_group)
     return x
 
 
-def tp_all_gather_last(x: torch.Tensor, group=None) -> torch.Tensor:
+def tp_all_gather_last(x: torch.Tensor, ps=None) -> torch.Tensor:
     """Concatenate the last dim across the TP group, rank order (C-4: vocab-parallel logits)."""
-    st = get_state()
+    st = ps or get_state()
     if st.tp_size == 1:
         return x
     x = x.contiguous()
     out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x, group=group or st.tp_group)
+    if x.is_cuda:
+        dist.all_gather_into_tensor(out, x, group=st.tp_group)
+    else:  # gloo has no all_gather_into_tensor
+        dist.all_gather(list(out.unbind(0)), x, group=st.tp_group)
     return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
 
 
-def tp_broadcast_object(obj, src_tp_rank: int = 0):
+def tp_broadcast_object(obj, src_tp_rank: int = 0, ps=None):
     """Broadcast a picklable control message (the step schedule, C-6) from the TP leader over the
     CPU gloo group."""
-    st = get_state()
+    st = ps or get_state()
     if st.tp_size == 1:
         return obj
     lst = [obj]

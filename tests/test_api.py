@@ -1,0 +1,158 @@
+"""REST contract tests: every route, dev mode and FakeCluster."""
+import http.client
+import json
+import threading
+
+import pytest
+
+from k8s_llm_monitor_amd.monitor.app import build_monitor
+from k8s_llm_monitor_amd.monitor.cluster.fake import FakeCluster
+from k8s_llm_monitor_amd.monitor.config import from_dict
+from k8s_llm_monitor_amd.monitor.server import MonitorApp, make_server
+
+
+def J(r):
+    assert r.ctype == "application/json", r.ctype
+    assert r.body.endswith(b"\n")
+    return json.loads(r.body)
+
+
+@pytest.fixture()
+def mon():
+    cfg = from_dict({"k8s": {"watch_namespaces": "default,kube-system"},
+                     "metrics": {"namespaces": ["default", "kube-system"], "enable_network": True},
+                     "llm": {"provider": "none"}})
+    m = build_monitor(cfg, backend=FakeCluster.build(seed=2), start_manager=False, llm=True)
+    m.manager.collect()
+    return m
+
+
+def test_dev_mode_contract():
+    a = MonitorApp()
+    assert J(a.handle("GET", "/health"))["version"] == "1.0.0"
+    d = J(a.handle("GET", "/api/v1/cluster/status"))
+    assert set(d) == {"message", "status", "timestamp"} and d["status"] == "warning"
+    assert d["message"] == "K8s client not available - running in development mode"
+    d = J(a.handle("GET", "/api/v1/pods"))
+    assert d["pods"] == [] and d["status"] == "warning"
+    r = a.handle("POST", "/api/v1/analyze/pod-communication", b"{}")
+    assert r.code == 503 and r.body == b"K8s client not available - running in development mode\n"
+    for p in ("/api/v1/metrics/cluster", "/api/v1/metrics/nodes", "/api/v1/metrics/nodes/x", "/api/v1/metrics/pods",
+              "/api/v1/metrics/snapshot", "/api/v1/metrics/network", "/api/v1/metrics/uav", "/api/v1/metrics/uav/x"):
+        r = a.handle("GET", p)
+        assert (r.code, r.body, r.ctype) == (503, b"Metrics manager not available\n", "text/plain; charset=utf-8"), p
+    r = a.handle("GET", "/api/v1/crd/uav")
+    assert r.code == 503 and J(r) == {"message": "K8s client not available", "status": "error"}
+    r = a.handle("POST", "/api/v1/uav/report", b'{"node_name":"n1"}')
+    d = J(r)
+    assert r.code == 200 and d["crd_status"] == "unavailable" and d["uav_id"] == "uav-n1" and d["uav_status"] == "active"
+    assert r.headers.get("Access-Control-Allow-Origin") == "*"
+
+
+def test_methods_and_errors(mon):
+    a = mon.app
+    for p in ("/api/v1/cluster/status", "/api/v1/pods", "/api/v1/metrics/cluster", "/api/v1/crd/uav"):
+        r = a.handle("POST", p)
+        assert r.code == 405 and r.body == b"Method not allowed\n"
+    assert a.handle("GET", "/api/v1/analyze/pod-communication").code == 405
+    assert a.handle("GET", "/api/v1/uav/report").code == 405
+    r = a.handle("POST", "/api/v1/analyze/pod-communication", b"{bad")
+    assert (r.code, r.body) == (400, b"Invalid JSON body\n")
+    r = a.handle("POST", "/api/v1/analyze/pod-communication", b'{"pod_a":"x"}')
+    assert (r.code, r.body) == (400, b"pod_a and pod_b are required\n")
+    r = a.handle("POST", "/api/v1/analyze/pod-communication", b'{"pod_a":"default/x","pod_b":"default/y"}')
+    assert r.code == 500 and r.body.startswith(b"Analysis failed: failed to get pod A info")
+    assert a.handle("GET", "/api/v1/metrics/nodes/").body == b"Node name is required\n"
+    r = a.handle("GET", "/api/v1/metrics/nodes/ghost")
+    assert (r.code, r.body) == (404, b"Node not found: metrics not found for node: ghost\n")
+    r = a.handle("GET", "/api/v1/metrics/uav/ghost")
+    assert (r.code, r.body) == (404, b"UAV not found on node: ghost\n")
+    assert a.handle("POST", "/api/v1/uav/report", b"[]").body == b"Invalid JSON body\n"
+    assert a.handle("POST", "/api/v1/uav/report", b"{}").body == b"node_name is required\n"
+    assert a.handle("GET", "/api/v1//pods").code == 301
+
+
+def test_success_shapes(mon):
+    a = mon.app
+    d = J(a.handle("GET", "/api/v1/cluster/status"))
+    assert set(d["cluster_info"]) == {"namespaces", "nodes", "pods", "version"} and d["status"] == "success"
+    d = J(a.handle("GET", "/api/v1/pods"))
+    assert d["count"] == len(d["pods"]) > 5 and set(d["pods"][0]) == {"name", "namespace", "status", "node_name", "ip",
+                                                                    "labels", "start_time", "containers"}
+    d = J(a.handle("GET", "/api/v1/metrics/nodes"))
+    assert set(d) == {"count", "data", "status", "timestamp"} and d["count"] == 3
+    node = next(iter(d["data"].values()))
+    assert list(node)[:3] == ["node_name", "timestamp", "cpu_capacity"] and "custom_metrics" not in node
+    d = J(a.handle("GET", "/api/v1/metrics/snapshot"))
+    assert set(d) == {"data", "status"} and set(d["data"]) == {"timestamp", "node_metrics", "pod_metrics",
+                                                              "network_metrics", "cluster_metrics"}
+    d = J(a.handle("GET", "/api/v1/metrics/pods"))
+    assert all("/" in k for k in d["data"])
+    d = J(a.handle("GET", "/api/v1/metrics/network"))
+    assert d["count"] == 5 and set(d["data"][0]) >= {"source_pod", "target_pod", "connected", "rtt_ms", "test_method"}
+    d = J(a.handle("GET", "/api/v1/metrics/uav"))
+    e = next(iter(d["data"].values()))
+    assert set(e) == {"node_name", "status", "source", "timestamp", "last_heartbeat", "state"} and e["source"] == "pull"
+    node = next(iter(d["data"]))
+    assert J(a.handle("GET", f"/api/v1/metrics/uav/{node}"))["data"]["node_name"] == node
+    d = J(a.handle("POST", "/api/v1/analyze/pod-communication",
+                   b'{"pod_a":"default/frontend-5c7d8f9b4-kq2lp","pod_b":"default/nginx-web-6d4cf56db6-8v2mz","explain":false}'))
+    assert set(d) == {"analysis", "status", "timestamp"}
+    assert list(d["analysis"]) == ["pod_a", "pod_b", "status", "issues", "solutions", "confidence"]
+
+
+def test_uav_report_to_crd_to_scheduler(mon):
+    from k8s_llm_monitor_amd.monitor.cluster.backend import SCHEDULING_REQUESTS
+    from k8s_llm_monitor_amd.monitor.scheduler.controller import SchedulerController
+    from k8s_llm_monitor_amd.monitor.uav.agent import UAVAgent
+    from k8s_llm_monitor_amd.utils import gojson
+
+    a = mon.app
+    agent = UAVAgent("edge-1", "10.9.9.9", report_interval_s=10)
+    r = a.handle("POST", "/api/v1/uav/report", gojson.dumps(agent.build_report()).encode())
+    d = J(r)
+    assert d["crd_status"] == "updated" and d["uav_id"] == "UAV-edge-1" and d["heartbeat_interval_seconds"] == 10
+    assert J(a.handle("GET", "/api/v1/metrics/uav/edge-1"))["data"]["source"] == "agent"
+    crd = J(a.handle("GET", "/api/v1/crd/uav?namespace=all"))
+    assert crd["count"] == 1 and crd["data"][0]["spec"]["node_name"] == "edge-1"
+    fc = mon.backend
+    fc.create(SCHEDULING_REQUESTS, {"metadata": {"name": "job"}, "spec": {"workload": {"name": "w", "namespace": "default"},
+                                                                          "minBatteryPercent": 50}}, "default")
+    SchedulerController(fc).reconcile()
+    st = fc.get(SCHEDULING_REQUESTS, "job", "default")["status"]
+    assert st["phase"] == "Assigned" and st["assignedNode"] == "edge-1" and st["assignedUAV"] == "UAV-edge-1"
+
+
+def test_query_and_analysis_records(mon):
+    a = mon.app
+    assert a.handle("POST", "/api/v1/query", b"{}").body == b"question is required\n"
+    d = J(a.handle("POST", "/api/v1/query", "{\"question\":\"为什么我的pod频繁重启？\"}".encode()))
+    assert d["status"] == "success" and d["result"]["question"] == "为什么我的pod频繁重启？" and d["request_id"]
+    rec = J(a.handle("GET", f"/api/v1/analysis/{d['request_id']}"))
+    assert rec["data"]["request_id"] == d["request_id"]
+    d = J(a.handle("POST", "/api/v1/analyze", b'{"type":"anomaly_detection"}'))
+    assert d["result"]["type"] == "anomaly_detection"
+    assert a.handle("POST", "/api/v1/analyze", b'{"type":"bogus"}').code == 400
+    assert J(a.handle("GET", "/api/v1/analysis"))["count"] == 2
+
+
+def test_real_http_roundtrip(mon):
+    srv = make_server(mon.app, "127.0.0.1", 0)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    try:
+        c = http.client.HTTPConnection("127.0.0.1", srv.server_address[1], timeout=10)
+        c.request("GET", "/api/v1/metrics/cluster")
+        r = c.getresponse()
+        body = r.read()
+        assert r.status == 200 and r.getheader("Content-Type") == "application/json"
+        assert r.getheader("Access-Control-Allow-Origin") == "*" and json.loads(body)["status"] == "success"
+        c.request("GET", "/")
+        r = c.getresponse()
+        assert r.status == 200 and b"K8s LLM Monitor" in r.read()
+        c.request("POST", "/api/v1/pods", b"")
+        r = c.getresponse()
+        assert r.status == 405 and r.read() == b"Method not allowed\n"
+        assert r.getheader("X-Content-Type-Options") == "nosniff"
+    finally:
+        srv.shutdown()
