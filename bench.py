@@ -37,7 +37,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--kv-cache-gb", type=float, default=48.0)
-    ap.add_argument("--path", choices=["http", "engine"], default="engine")
+    ap.add_argument("--path", choices=["http", "engine"], default="http")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
@@ -46,7 +46,7 @@ def main() -> None:
     import torch
 
     from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
-    from k8s_llm_monitor_amd.llm.synthetic import synthetic_cluster_prompt
+    from k8s_llm_monitor_amd.llm.synthetic import synthetic_cluster_prompt, synthetic_context
     from k8s_llm_monitor_amd.parallel import comm
     from k8s_llm_monitor_amd.parallel.state import barrier_all, init_parallel
 
@@ -72,22 +72,21 @@ def main() -> None:
     params = SamplingParams(max_tokens=a.max_new_tokens, temperature=0.1, ignore_eos=True)
 
     def wave(w: int) -> tuple[list[float], int, int]:
-        prompts = [synthetic_cluster_prompt(seed=(rank * 1_000_003 + w * a.batch + i)) for i in range(a.batch)]
-        t0 = time.perf_counter()
+        seeds = [rank * 1_000_003 + w * a.batch + i for i in range(a.batch)]
         if a.path == "http":
             from k8s_llm_monitor_amd.monitor.app import post_queries
 
-            res = post_queries(port, [p for p in prompts], a.max_new_tokens)
-            lat = [r["latency_ms"] for r in res]
+            items = [synthetic_context(s)[::-1] for s in seeds]  # (question, cluster context)
+            res = post_queries(port, items, a.max_new_tokens)
+            lat = [r["http_latency_ms"] for r in res]
             ptok = sum(r["prompt_tokens"] for r in res)
             gtok = sum(r["completion_tokens"] for r in res)
         else:
-            futs = [svc.submit(p, params) for p in prompts]
+            futs = [svc.submit(synthetic_cluster_prompt(s), params) for s in seeds]
             outs = [f.result() for f in futs]
             lat = [s.timings()["latency_ms"] for _, s in outs]
             ptok = sum(len(s.prompt_ids) for _, s in outs)
             gtok = sum(len(s.output_ids) for _, s in outs)
-        del t0
         return lat, ptok, gtok
 
     for w in range(a.warmup):
