@@ -11,6 +11,11 @@ hipGraph:
   -> flash_prefill | paged_decode (HIP MFMA) -> o_proj GEMM (+ RCCL all-reduce at TP>1)
   -> fused_add_rms_norm (HIP) -> gate_up GEMM -> silu_mul (HIP) -> down GEMM (+ all-reduce)
 
+Dense decode at TP=1 runs all four projections through the skinny MFMA GEMM over
+fragment-packed weights (ops/csrc/gemm_skinny.hip; ``_init_skinny``): split-K slabs reduced by
+the next kernel (rope_and_cache, reduce_add_rms_norm) and SwiGLU in the gate_up epilogue -
+7 launches per layer instead of 9.
+
 Weights are stored fused and pre-sharded: ``wqkv`` [(Hq+2Hkv)/tp * D, d] (column-parallel),
 ``wo`` [d, Hq/tp * D] (row-parallel), ``w13`` [2F/tp, d] (gate rows then up rows of this rank's
 shard), ``w2`` [d, F/tp].  Random init is seeded per tensor name, and every rank generates the
@@ -20,6 +25,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -82,6 +88,7 @@ class CausalLM:
             self.e_lo, self.e_hi = shard_range(cfg.n_experts, tp, r)
         self.layers: list[dict] = []
         self._build()
+        self._init_skinny()
         self.cos_sin = None
         if cfg.arch == "llama":
             self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, cfg.rope_scaling,
@@ -176,7 +183,9 @@ class CausalLM:
     def num_local_params(self) -> int:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
         for L in self.layers:
-            for v in L.values():
+            for k, v in L.items():
+                if k.endswith("_p"):  # decode-layout copies (_init_skinny) are not extra parameters
+                    continue
                 if isinstance(v, tuple):
                     n += sum(t.numel() for t in v)
                 else:
@@ -193,23 +202,37 @@ class CausalLM:
         return tp_all_reduce(x, self.ps)
 
     def _attention(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv) -> torch.Tensor:
+        o = self._attn_core(L, x, meta, kv)
+        y = F.linear(o, L["wo"])
+        if "bo" in L and self.rank == 0:
+            y += L["bo"]
+        return tp_all_reduce(y, self.ps)
+
+    def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None) -> torch.Tensor:
+        """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
+        ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM, reduced inside
+        rope_and_cache."""
         c = self.cfg
-        qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
         k_cache, v_cache = kv if kv is not None else (None, None)
+        partial, ns = None, 0
+        if slabs is not None:
+            ws, splits = slabs
+            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits)
+            partial = ws
+            qkv = torch.empty(x.shape[0], L["wqkv_p"].shape[0] * 16, dtype=x.dtype, device=x.device)
+        else:
+            qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
         ops.rope_and_cache(qkv, meta.positions, self.cos_sin if self.cos_sin is not None else _dummy_cs(self),
                            k_cache, v_cache, meta.slot_mapping if k_cache is not None else None,
                            self.hq, self.hkv, self.D,
-                           apply_rope=c.arch == "llama")
+                           apply_rope=c.arch == "llama", partial=partial, nslabs=ns)
         if meta.is_prefill:
             qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
             o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb)
         else:
             o = ops.paged_decode(qkv, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.hq, self.hkv,
                                  self.D, self.scale, workspace=meta.decode_ws)
-        y = F.linear(o, L["wo"])
-        if "bo" in L and self.rank == 0:
-            y += L["bo"]
-        return tp_all_reduce(y, self.ps)
+        return o
 
     def _mlp(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         c = self.cfg
@@ -279,6 +302,8 @@ class CausalLM:
             residual = h
             x = ops.rms_norm(h, self.layers[0]["attn_norm"], c.norm_eps)
             n = len(self.layers)
+            if self._use_skinny(meta, h):
+                return self._decode_layers_skinny(x, residual, meta, kv_caches)
             for i, L in enumerate(self.layers):
                 kv = kv_caches[i] if kv_caches is not None else None
                 y = self._attention(L, x, meta, kv)
@@ -291,11 +316,66 @@ class CausalLM:
                         y = y[meta.logits_idx]
                         residual = residual[meta.logits_idx].contiguous()
                     x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
+        return self._logits(x)
+
+    def _logits(self, x: torch.Tensor) -> torch.Tensor:
         logits = F.linear(x, self.lm_head)
         logits = tp_all_gather_last(logits, self.ps)
-        if self.vocab_padded != c.vocab_size:
-            logits = logits[:, : c.vocab_size]
+        if self.vocab_padded != self.cfg.vocab_size:
+            logits = logits[:, : self.cfg.vocab_size]
         return logits
+
+    # ------------------------------------------------------------------ fused decode tail
+    def _use_skinny(self, meta: AttnMeta, h: torch.Tensor) -> bool:
+        """Dense Llama decode at TP=1 on the GPU with <= 64 rows runs every projection through
+        gemm_skinny over fragment-packed weights (see _init_skinny)."""
+        return (self._skinny_ws is not None and not meta.is_prefill and h.shape[0] <= ops.SKINNY_MAX_M
+                and meta.logits_idx is None and os.environ.get("K8SLLM_SKINNY", "1") != "0")
+
+    def _init_skinny(self) -> None:
+        """Decode-path weights: a fragment-packed copy of wqkv / wo / w13 (gate/up interleaved per
+        64-row tile) / w2 for gemm_skinny (ops/csrc/gemm_skinny.hip); prefill keeps hipBLASLt on
+        the row-major tensors.  Costs one extra copy of the layer weights (16 GB for Llama-3-8B on
+        a 288 GB MI355X) and buys whole-line weight streaming for every decode projection.
+
+        Per layer at decode (7 launches): qkv skinny (split-K slabs) -> rope_and_cache (reduces
+        the slabs, RoPE, KV write) -> paged_decode -> o skinny (slabs) -> reduce_add_rms_norm
+        (residual add + mlp norm) -> gate_up skinny with the SwiGLU epilogue -> down skinny
+        (slabs) -> reduce_add_rms_norm (residual add + next layer's attn norm).
+        TP>1 keeps hipBLASLt + RCCL all-reduce (row-parallel partial sums must be reduced across
+        ranks before the residual add)."""
+        self._skinny_ws = None
+        c = self.cfg
+        if (self.device.type != "cuda" or self.tp != 1 or c.arch != "llama" or c.is_moe
+                or os.environ.get("K8SLLM_SKINNY", "1") == "0"):
+            return
+        d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
+        if d % 64 or nq % 64 or (self.hq * self.D) % 32 or self.f_local % 32:
+            return
+        for L in self.layers:
+            L["wqkv_p"] = ops.pack_skinny(L["wqkv"])
+            L["wo_p"] = ops.pack_skinny(L["wo"])
+            L["w13_p"] = ops.pack_skinny(ops.interleave_gate_up(L["w13"]))
+            L["w2_p"] = ops.pack_skinny(L["w2"])
+        self._split_qkv = ops.skinny_splits(nq, d)
+        self._split_o = ops.skinny_splits(d, self.hq * self.D)
+        self._split_d = ops.skinny_splits(d, self.f_local)
+        n = max(self._split_qkv * nq, self._split_o * d, self._split_d * d)
+        self._skinny_ws = torch.empty(n * ops.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
+
+    def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
+                              kv_caches: Optional[list]) -> torch.Tensor:
+        c, ws, n = self.cfg, self._skinny_ws, len(self.layers)
+        for i, L in enumerate(self.layers):
+            kv = kv_caches[i] if kv_caches is not None else None
+            o = self._attn_core(L, x, meta, kv, slabs=(ws, self._split_qkv))
+            x = ops.proj_add_rms_norm(o, L["wo_p"], residual, L["mlp_norm"], c.norm_eps, workspace=ws,
+                                      splits=self._split_o)
+            act = ops.skinny_swiglu(x, L["w13_p"])
+            nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
+            x = ops.proj_add_rms_norm(act, L["w2_p"], residual, nw, c.norm_eps, workspace=ws,
+                                      splits=self._split_d)
+        return self._logits(x)
 
 
 _DUMMY_CS: dict = {}

@@ -70,6 +70,108 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     return out
 
 
+# ---------------------------------------------------------------- decode projections (skinny GEMM)
+
+SKINNY_MAX_M = 64
+
+
+def pack_skinny(w: torch.Tensor) -> torch.Tensor:
+    """Row-major weight [N, K] -> the fragment-packed [N/16, K/32, 64, 8] layout of gemm_skinny:
+    block (n-tile j, k-step s) holds, for lane l = 16 q + r, elements W[16 j + r, 32 s + 8 q : +8]
+    (the v_mfma_f32_16x16x32_bf16 B operand), 1 KiB contiguous per block."""
+    N, K = w.shape
+    if N % 16 or K % 32:
+        raise ValueError(f"pack_skinny: [{N}, {K}] needs N % 16 == 0 and K % 32 == 0")
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 32, 64, 8).contiguous()
+
+
+def unpack_skinny(wp: torch.Tensor) -> torch.Tensor:
+    nt, ks = wp.shape[0], wp.shape[1]
+    return wp.reshape(nt, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, ks * 32)
+
+
+def interleave_gate_up(w13: torch.Tensor) -> torch.Tensor:
+    """[gate (F rows); up (F rows)] -> per 64-row tile [32 gate | 32 up] rows (the SWIGLU epilogue)."""
+    F2, K = w13.shape
+    F = F2 // 2
+    if F % 32:
+        raise ValueError("interleave_gate_up: F must be a multiple of 32")
+    return w13.reshape(2, F // 32, 32, K).permute(1, 0, 2, 3).reshape(F2, K)
+
+
+def skinny_splits(N: int, K: int, target_wgs: int = 512) -> int:
+    """Split-K factor for a slab-epilogue gemm_skinny: (N/64) x S workgroups ~ two per CU, each K
+    slice at least 512 deep.  ``K8SLLM_SKINNY_SPLITS`` overrides."""
+    env = os.environ.get("K8SLLM_SKINNY_SPLITS")
+    if env:
+        return max(1, int(env))
+    tiles = max(1, N // 64)
+    return max(1, min(K // 512, round(target_wgs / tiles)))
+
+
+def skinny_workspace(max_m: int, N: int, splits: int, device) -> torch.Tensor:
+    """fp32 split-K partial slabs [splits, max_m, N]."""
+    return torch.empty(splits * min(max_m, SKINNY_MAX_M) * N, dtype=torch.float32, device=device)
+
+
+def _skinny_ntl() -> bool:
+    return os.environ.get("K8SLLM_SKINNY_NT", "1") != "0"
+
+
+def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  nt_tiles: int = 4) -> torch.Tensor:
+    """``a @ W^T`` (bf16) for <= 64 rows over the fragment-packed weight, one K slice."""
+    N = wp.shape[0] * 16
+    if out is None:
+        out = torch.empty(a.shape[0], N, dtype=a.dtype, device=a.device)
+    native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, _skinny_ntl())
+    return out
+
+
+def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F]."""
+    F = wp13.shape[0] * 8
+    if out is None:
+        out = torch.empty(a.shape[0], F, dtype=a.dtype, device=a.device)
+    native().gemm_skinny(a, wp13, None, out, 1, 2, 4, _skinny_ntl())
+    return out
+
+
+def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, splits: int,
+                 nt_tiles: int = 4) -> int:
+    """Split-K ``a @ W^T`` into fp32 slabs [S', M, N] in ``workspace``; returns S'."""
+    return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, _skinny_ntl())
+
+
+def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                      workspace: Optional[torch.Tensor] = None, splits: Optional[int] = None,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The decode tail of an attention or MLP block in one GEMM + one reduce:
+    ``residual <- bf16(residual + a @ W^T)``; returns ``rms_norm(residual) * norm_w``.
+    GPU only: gemm_skinny (packed ``wp``, split-K fp32 slabs) then reduce_add_rms_norm."""
+    M, N, K = a.shape[0], wp.shape[0] * 16, wp.shape[1] * 32
+    if splits is None:
+        splits = skinny_splits(N, K)
+    if workspace is None:
+        workspace = skinny_workspace(M, N, splits, a.device)
+    s = skinny_slabs(a, wp, workspace, splits)
+    if out is None:
+        out = torch.empty(M, N, dtype=residual.dtype, device=a.device)
+    native().reduce_add_rms_norm(out, residual, workspace, s, norm_w, eps)
+    return out
+
+
+def gemm_skinny(a: torch.Tensor, w: torch.Tensor, splits: int = 1) -> torch.Tensor:
+    """``a @ w^T`` through the skinny kernel from a row-major weight (tests / tools); bf16."""
+    wp = pack_skinny(w)
+    if splits == 1:
+        return skinny_linear(a, wp)
+    M, N = a.shape[0], w.shape[0]
+    ws = skinny_workspace(M, N, splits, a.device)
+    s = skinny_slabs(a, wp, ws, splits)
+    return ws[: s * M * N].view(s, M, N).sum(0).to(a.dtype)
+
+
 def layer_norm(x, w, b, eps):
     if not _gpu(x):
         return ref.layer_norm(x, w, b, eps)
@@ -112,8 +214,10 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int = 0,
 def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                    k_cache: Optional[torch.Tensor], v_cache: Optional[torch.Tensor],
                    slot_mapping: Optional[torch.Tensor], Hq: int, Hkv: int, D: int,
-                   apply_rope: bool = True) -> None:
-    """In place: rotate q and k inside the fused QKV rows; write k, v into the paged cache."""
+                   apply_rope: bool = True, partial: Optional[torch.Tensor] = None, nslabs: int = 0) -> None:
+    """In place: rotate q and k inside the fused QKV rows; write k, v into the paged cache.
+    With ``partial`` (GPU), the QKV values are first reduced from ``nslabs`` fp32 split-K slabs
+    [nslabs, T, (Hq+2Hkv)*D] (skinny_slabs) and the reduced rows are written to ``qkv``."""
     if not _gpu(qkv):
         ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, Hq, Hkv, D, apply_rope)
         return
@@ -122,7 +226,7 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
                             k_cache if k_cache is not None else empty,
                             v_cache if v_cache is not None else empty,
                             slot_mapping if slot_mapping is not None else empty,
-                            Hq, Hkv, D, apply_rope)
+                            Hq, Hkv, D, apply_rope, partial, nslabs)
 
 
 _EMPTY = {}

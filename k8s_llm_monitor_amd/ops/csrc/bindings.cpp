@@ -16,7 +16,7 @@ int k8sllm_embedding(void* out, const int* ids, const void* weight, long T, int 
                      hipStream_t s);
 int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, void* k_cache,
                       void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D, int block_size,
-                      int apply_rope, hipStream_t s);
+                      int apply_rope, const float* partial, int S, hipStream_t s);
 int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q, long q_stride,
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
@@ -24,7 +24,8 @@ int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_s
                          const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
                          hipStream_t s);
 int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V, const float* temps,
-                  const int* top_k, const float* top_p, const int64_t* rng, hipStream_t s);
+                  const int* top_k, const float* top_p, const int64_t* rng, float* pv, int* pi, hipStream_t s);
+int k8sllm_sample_parts(long B, int V);
 int k8sllm_moe_route(const void* logits, long T, int E, int K, int renorm, int* topk_ids, float* topk_w,
                      hipStream_t s);
 int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, int* sorted_idx, int* inv_idx,
@@ -32,6 +33,11 @@ int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, in
 int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
+int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
+                       int S, int epi, int nt_tiles, int ntl, hipStream_t s);
+int k8sllm_gemm_skinny_slabs(int K, int S);
+int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
+                              float eps, hipStream_t s);
 }
 
 namespace {
@@ -106,7 +112,7 @@ void embedding(torch::Tensor out, torch::Tensor ids, torch::Tensor weight, int64
 
 void rope_and_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, torch::Tensor k_cache,
                     torch::Tensor v_cache, torch::Tensor slot_mapping, int64_t Hq, int64_t Hkv, int64_t D,
-                    bool apply_rope) {
+                    bool apply_rope, c10::optional<torch::Tensor> partial, int64_t S) {
   dev_bf16(qkv, "qkv"); dev_i32(positions, "positions");
   TORCH_CHECK(qkv.stride(-1) == 1 && qkv.dim() == 2, "qkv must be [T, (Hq+2Hkv)*D] with unit inner stride");
   TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv width");
@@ -121,10 +127,16 @@ void rope_and_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor co
     TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == Hkv && v_cache.size(2) == D, "v_cache layout");
     block_size = (int)k_cache.size(3);
   }
+  const float* pp = nullptr;
+  if (partial.has_value()) {  // qkv = sum of S fp32 split-K slabs [S][T][(Hq+2Hkv)*D]
+    TORCH_CHECK(partial->is_cuda() && partial->scalar_type() == torch::kFloat32 && partial->is_contiguous(), "partial");
+    TORCH_CHECK(partial->numel() >= S * qkv.size(0) * (Hq + 2 * Hkv) * D, "partial too small");
+    pp = partial->data_ptr<float>();
+  }
   check(k8sllm_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
                           has_cache ? k_cache.data_ptr() : nullptr, has_cache ? v_cache.data_ptr() : nullptr,
                           has_cache ? slot_mapping.data_ptr<int>() : nullptr, qkv.size(0), (int)Hq, (int)Hkv, (int)D,
-                          block_size, apply_rope ? 1 : 0, cur()),
+                          block_size, apply_rope ? 1 : 0, pp, (int)S, cur()),
         "rope_and_cache");
 }
 
@@ -170,8 +182,14 @@ void sample(torch::Tensor out, torch::Tensor logits, c10::optional<torch::Tensor
   const int* k = top_k && top_k->numel() ? top_k->data_ptr<int>() : nullptr;
   const float* p = top_p && top_p->numel() ? top_p->data_ptr<float>() : nullptr;
   const int64_t* r = rng && rng->numel() ? rng->data_ptr<int64_t>() : nullptr;
-  check(k8sllm_sample(out.data_ptr<int>(), logits.data_ptr(), f32 ? 1 : 0, logits.size(0), logits.stride(0),
-                      (int)logits.size(1), t, k, p, r, cur()),
+  const long B = logits.size(0);
+  const int V = (int)logits.size(1);
+  const int64_t np = B * k8sllm_sample_parts(B, V);
+  // partial (value, index) workspace: stream-ordered caching allocator (graph-pool safe)
+  auto pv = torch::empty({np}, logits.options().dtype(torch::kFloat32));
+  auto pi = torch::empty({np}, logits.options().dtype(torch::kInt32));
+  check(k8sllm_sample(out.data_ptr<int>(), logits.data_ptr(), f32 ? 1 : 0, B, logits.stride(0), V, t, k, p, r,
+                      pv.data_ptr<float>(), pi.data_ptr<int>(), cur()),
         "sample");
 }
 
@@ -216,6 +234,58 @@ void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t 
 
 }  // namespace
 
+// Skinny decode GEMM over a fragment-packed weight wp [N/16][K/32][64][8] (gemm_skinny.hip).
+// epi 0: fp32 split-K slabs partial[S'][M][N], returns S'; epi 1: y = bf16(a . W^T);
+// epi 2: y[M, N/2] = silu(gate) * up over a [32 gate | 32 up]-interleaved weight.  Returns the
+// number of slabs written (1 for epi 1/2).
+int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
+                    c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, bool ntl) {
+  dev_bf16(a, "a"); dev_bf16(wp, "wp");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
+              "gemm_skinny: wp must be fragment-packed [N/16, K/32, 64, 8]");
+  TORCH_CHECK(a.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 8 == 0, "gemm_skinny: a layout");
+  const int M = (int)a.size(0), N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32;
+  TORCH_CHECK(a.size(1) == K, "gemm_skinny: a has ", a.size(1), " columns, weight K=", K);
+  TORCH_CHECK(M <= 64, "gemm_skinny: at most 64 rows");
+  TORCH_CHECK(N % (16 * nt_tiles) == 0, "gemm_skinny: N not divisible by the workgroup tile");
+  const int S = epi == 0 ? k8sllm_gemm_skinny_slabs(K, (int)splits) : 1;
+  float* pp = nullptr;
+  void* yp = nullptr;
+  long ldy = 0;
+  if (epi == 0) {
+    TORCH_CHECK(partial.has_value(), "gemm_skinny: split-K needs a partial buffer");
+    TORCH_CHECK(partial->is_cuda() && partial->scalar_type() == torch::kFloat32 && partial->is_contiguous(),
+                "partial must be contiguous fp32 on the GPU");
+    TORCH_CHECK(partial->numel() >= (int64_t)S * M * N, "partial buffer too small");
+    pp = partial->data_ptr<float>();
+  } else {
+    TORCH_CHECK(y.has_value(), "gemm_skinny: output tensor required");
+    dev_bf16(*y, "y");
+    const int ncol = epi == 2 ? N / 2 : N;
+    TORCH_CHECK(y->dim() == 2 && y->size(0) >= M && y->size(1) == ncol && y->stride(1) == 1, "gemm_skinny: y shape");
+    yp = y->data_ptr();
+    ldy = y->stride(0);
+  }
+  check(k8sllm_gemm_skinny(a.data_ptr(), a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
+                           epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, ntl ? 1 : 0, cur()),
+        "gemm_skinny");
+  return S;
+}
+
+void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, torch::Tensor partial, int64_t S,
+                         torch::Tensor w, double eps) {
+  dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
+  TORCH_CHECK(residual.is_contiguous() && out.is_contiguous() && w.is_contiguous(), "reduce_add_rms_norm layout");
+  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == torch::kFloat32 && partial.is_contiguous(), "partial");
+  const int d = (int)residual.size(-1);
+  const int M = (int)(residual.numel() / d);
+  TORCH_CHECK(partial.numel() >= S * M * d && out.numel() == (int64_t)M * d, "reduce_add_rms_norm shapes");
+  check(k8sllm_reduce_add_rmsnorm(out.data_ptr(), residual.data_ptr(), partial.data_ptr<float>(), (int)S, M,
+                                  w.data_ptr(), d, (float)eps, cur()),
+        "reduce_add_rms_norm");
+}
+
+
 PYBIND11_MODULE(_k8sllm_ops, m) {
   m.doc() = "gfx950 HIP kernels for k8s-llm-monitor-amd";
   m.def("rms_norm", &rms_norm);
@@ -232,4 +302,6 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_combine", &moe_combine);
   m.def("gather_rows", &gather_rows);
+  m.def("gemm_skinny", &gemm_skinny);
+  m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
 }

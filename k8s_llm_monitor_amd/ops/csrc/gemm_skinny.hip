@@ -1,0 +1,253 @@
+// Decode-time "skinny" GEMM on gfx950 MFMA: Y[M, N] = A[M, K] . W[N, K]^T for M <= 64 rows (the
+// decode batch), bf16 in, fp32 accumulate.  Every decode projection of a dense Llama layer runs
+// here (qkv, o, gate_up, down); prefill keeps hipBLASLt on the row-major copy of the weights.
+//
+// Weight layout - "fragment-packed" [N/16][K/32][64 lanes][8] bf16 (pack_weight_for_skinny in
+// ops/__init__.py): the 16x32 B fragment of v_mfma_f32_16x16x32_bf16 for n-tile j, k-step s is one
+// contiguous 1 KiB block in lane order, so every weight load instruction of a wave reads 1 KiB
+// contiguous straight into MFMA operand registers.  Measured on MI355X (tools/membw.hip): reading
+// a row-major [N][K] weight in MFMA-fragment order (16 rows x 64 B per instruction) streams at
+// 1.1-3.9 TB/s; whole-line orders reach 4.7-5.7 TB/s - the packed layout gets the latter with no
+// LDS round trip.  Weights are read once per step (14 GB for Llama-3-8B), so loads are
+// non-temporal (MI355X_MICROARCH.md "nt-weights").
+//
+// Decomposition: workgroup = 4 waves, NT n-tiles (16 NT output columns) x one K slice; grid =
+// (N / (16 NT), slices).  The waves take interleaved groups of U consecutive k-steps of the slice
+// and combine through LDS at the end.  Epilogues:
+//   SLAB   - fp32 split-K partials partial[slice][m][n], summed by the NEXT kernel
+//            (reduce_add_rmsnorm below, or rope_and_cache for qkv): the launch-boundary reduce of
+//            cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2 - no in-launch fences
+//   BF16   - one slice: Y = bf16(acc)
+//   SWIGLU - one slice, NT = 4, weight rows interleaved per 64-column tile as [32 gate | 32 up]:
+//            Y[m, f] = silu(gate) * up - the gate_up projection writes the MLP activation directly
+//            (no silu_mul pass, and the down projection reads F, not 2F, columns)
+#include "common.h"
+
+namespace k8sllm {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2 };
+constexpr int kU = 4;  // consecutive k-steps per wave group (4 KiB per n-tile in flight per wave)
+
+template <int MT, int NT, int EPI, bool NTL>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
+                                                          const bf16_t* __restrict__ Wp, float* __restrict__ partial,
+                                                          bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
+                                                          int kchunk) {
+  __shared__ __attribute__((aligned(16))) float red[4][MT][NT][64][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ntile0 = blockIdx.x * NT;
+  const int s = blockIdx.y;
+  const int kbeg = s * kchunk;
+  const int nsteps = (min(K, kbeg + kchunk) - kbeg) >> 5;  // host guarantees 32 | K and 32 | kchunk
+  const int ksteps = K >> 5;
+
+  const u32x4* wp[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    wp[nt] = reinterpret_cast<const u32x4*>(Wp) + ((long)(ntile0 + nt) * ksteps + (kbeg >> 5)) * 64 + lane;
+  const bf16_t* ap[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ap[mt] = A + (long)min(mt * 16 + (lane & 15), M - 1) * lda + kbeg + 8 * (lane >> 4);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int i0 = wave * kU; i0 < nsteps; i0 += 4 * kU) {
+    u32x4 bf[kU][NT];
+    bf16x8 af[kU][MT];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int st = min(i0 + u, nsteps - 1);  // tail steps re-read a valid step; their MFMAs are skipped
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if constexpr (NTL)
+          bf[u][nt] = __builtin_nontemporal_load(wp[nt] + st * 64);
+        else
+          bf[u][nt] = wp[nt][st * 64];
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[u][mt] = *reinterpret_cast<const bf16x8*>(ap[mt] + st * 32);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (i0 + u < nsteps) {  // wave-uniform
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u][mt], __builtin_bit_cast(bf16x8, bf[u][nt]),
+                                                                   acc[mt][nt], 0, 0, 0);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(&red[wave][mt][nt][lane][0]) = acc[mt][nt];
+  __syncthreads();
+
+  // C/D layout of the 16x16 tile: col = lane & 15, rows (lane >> 4) * 4 + r
+  constexpr int NOUT = EPI == EPI_SWIGLU ? NT / 2 : NT;
+  for (int idx = threadIdx.x; idx < NOUT * 64; idx += 256) {
+    const int nt = idx >> 6, l = idx & 63;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][mt][nt][l][0]);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][mt][nt][l][0]);
+      if constexpr (EPI == EPI_SWIGLU) {
+        f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][mt][nt + NT / 2][l][0]);
+#pragma unroll
+        for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][mt][nt + NT / 2][l][0]);
+        const int f = blockIdx.x * (NT * 8) + nt * 16 + (l & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + (l >> 4) * 4 + r;
+          // the gate and up values are rounded to bf16 first, as the unfused GEMM -> silu_mul does
+          const float g = bf2f(f2bf(v[r]));
+          const float uu = bf2f(f2bf(u[r]));
+          if (row < M) Y[(long)row * ldy + f] = f2bf(g * uu / (1.f + __expf(-g)));
+        }
+      } else {
+        const int col = (ntile0 + nt) * 16 + (l & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + (l >> 4) * 4 + r;
+          if (row < M) {
+            if constexpr (EPI == EPI_BF16)
+              Y[(long)row * ldy + col] = f2bf(v[r]);
+            else
+              partial[((long)s * M + row) * N + col] = v[r];
+          }
+        }
+      }
+    }
+  }
+}
+
+// residual[m] <- bf16(residual[m] + sum_s partial[s][m]); out[m] <- rmsnorm(residual[m]) * w
+// One workgroup per row, 256 threads x 8 columns per chunk (d <= 2048 * NC).
+template <int NC>
+__global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restrict__ out,
+                                                                 bf16_t* __restrict__ residual,
+                                                                 const float* __restrict__ partial, int S, int M,
+                                                                 const bf16_t* __restrict__ w, int d, float eps) {
+  __shared__ float sred[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  bf16_t* rr = residual + (long)row * d;
+  float v[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < d) {
+      float acc[8];
+      unpack8(*reinterpret_cast<const uint4*>(rr + idx), acc);
+      for (int s = 0; s < S; ++s) {
+        const float* p = partial + ((long)s * M + row) * d + idx;
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+      const uint4 q = pack8(acc);  // the residual stream is bf16 (HF semantics): round, then norm
+      *reinterpret_cast<uint4*>(rr + idx) = q;
+      unpack8(q, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  const float inv = rsqrtf(block_sum<256>(ss, sred) / (float)d + eps);
+  bf16_t* orow = out + (long)row * d;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < d) {
+      float wf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
+      *reinterpret_cast<uint4*>(orow + idx) = pack8(o);
+    }
+  }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+// kchunk: K split into `S` slices rounded up to whole wave groups (128 k) where that keeps the
+// slice count, else to whole k-steps.
+static int skinny_kchunk(int K, int S) {
+  int kc = (K + S - 1) / S;
+  const int kc128 = (kc + 127) / 128 * 128;
+  if ((K + kc128 - 1) / kc128 == S) return kc128;
+  return (kc + 31) / 32 * 32;
+}
+
+extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
+  const int kc = skinny_kchunk(K, S);
+  return (K + kc - 1) / kc;
+}
+
+// epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; ntl: non-temporal W loads
+extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
+                                  int N, int K, int S, int epi, int nt_tiles, int ntl, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (M > 64 || K % 32 != 0 || S < 1 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
+  const int kc = skinny_kchunk(K, S);
+  const int slabs = (K + kc - 1) / kc;
+  if (epi != EPI_SLAB && slabs != 1) return -3;
+  if (epi == EPI_SWIGLU && nt_tiles != 4) return -4;
+  dim3 grid(N / (16 * nt_tiles), slabs), blk(256);
+  const int MT = (M + 15) / 16;
+#define K8S_SK(MTV, NTV, EPV, NTLV)                                                                            \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, NTLV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc)
+#define K8S_SK_M(NTV, EPV, NTLV)             \
+  switch (MT) {                              \
+    case 1: K8S_SK(1, NTV, EPV, NTLV); break; \
+    case 2: K8S_SK(2, NTV, EPV, NTLV); break; \
+    case 3: K8S_SK(3, NTV, EPV, NTLV); break; \
+    default: K8S_SK(4, NTV, EPV, NTLV); break; \
+  }
+#define K8S_SK_NTL(NTV, EPV)  \
+  if (ntl) {                  \
+    K8S_SK_M(NTV, EPV, true)  \
+  } else {                    \
+    K8S_SK_M(NTV, EPV, false) \
+  }
+  if (epi == EPI_SWIGLU) {
+    K8S_SK_NTL(4, EPI_SWIGLU)
+  } else if (epi == EPI_BF16) {
+    if (nt_tiles == 4) { K8S_SK_NTL(4, EPI_BF16) } else { K8S_SK_NTL(2, EPI_BF16) }
+  } else {
+    if (nt_tiles == 4) { K8S_SK_NTL(4, EPI_SLAB) } else { K8S_SK_NTL(2, EPI_SLAB) }
+  }
+#undef K8S_SK_NTL
+#undef K8S_SK_M
+#undef K8S_SK
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M,
+                                         const void* w, int d, float eps, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (d % 8 != 0 || d > 256 * 8 * 4) return -1;
+  const int nc = (d + 2047) / 2048;
+#define K8S_RAR(NC)                                                                                           \
+  hipLaunchKernelGGL((reduce_add_rmsnorm_kernel<NC>), dim3(M), dim3(256), 0, s, (bf16_t*)out,                 \
+                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, eps)
+  if (nc <= 1) K8S_RAR(1);
+  else if (nc <= 2) K8S_RAR(2);
+  else K8S_RAR(4);
+#undef K8S_RAR
+  return (int)hipGetLastError();
+}

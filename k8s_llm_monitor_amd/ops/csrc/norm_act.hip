@@ -107,11 +107,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(bf16_t* __restrict__ out
 // SwiGLU: x = [gate | up] per row (width 2F), out = silu(gate) * up (width F).
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
                                                        long rows, int F) {
-  const int fv = F >> 3;
-  const long total = rows * fv;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long r = i / fv;
-    const int c = (int)(i - r * fv) * 8;
+  // grid (ceil(F/8 / 256), min(rows, 65535)): 2-D indexing, no 64-bit division per element
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= F) return;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y) {
     const bf16_t* xr = x + r * 2 * F;
     float g[8], u[8], o[8];
     unpack8(*reinterpret_cast<const uint4*>(xr + c), g);
@@ -203,8 +202,9 @@ int k8sllm_layernorm(void* out, const void* x, const void* w, const void* b, lon
 
 int k8sllm_silu_mul(void* out, const void* x, long rows, int F, hipStream_t s) {
   if (F % 8 != 0) return -1;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(rows * (F / 8))), dim3(256), 0, s, (bf16_t*)out,
-                     (const bf16_t*)x, rows, F);
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3((F / 8 + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535)), dim3(256), 0,
+                     s, (bf16_t*)out, (const bf16_t*)x, rows, F);
   return (int)hipGetLastError();
 }
 

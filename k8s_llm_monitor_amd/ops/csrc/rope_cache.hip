@@ -11,75 +11,116 @@
 
 namespace k8sllm {
 
-// One workgroup per token.  Work items: (Hq + Hkv) heads x D/8 "quads" of rotary pairs
-// (each item rotates 4 pairs = 8 B of the lower half and 8 B of the upper half), then
-// Hkv heads x D/8 value chunks of 8 dims (16 B) that are only copied into the cache.
-template <int D>
-__global__ __launch_bounds__(256) void rope_cache_kernel(bf16_t* __restrict__ qkv, long qkv_stride,
+// Sum of the split-K slabs of the qkv projection (gemm_skinny EPI_SLAB) for N consecutive columns.
+template <int N>
+__device__ __forceinline__ void slab_sum(const float* __restrict__ p, long slab_stride, int S, float* out) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = 0.f;
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int j = 0; j < N; j += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p + s * slab_stride + j);
+      out[j] += v.x; out[j + 1] += v.y; out[j + 2] += v.z; out[j + 3] += v.w;
+    }
+  }
+}
+
+// grid = (T, ceil(items / 128)), 128 threads, one work item per thread.  Items: (Hq + Hkv) heads
+// x D/8 "quads" of rotary pairs (each rotates 4 pairs = 8 B of the lower half and 8 B of the upper
+// half), then Hkv heads x D/8 value chunks of 8 dims (16 B) that are only copied into the cache.
+// SLAB: the qkv values are the sum of S fp32 split-K slabs partial[s][t][col] (the decode qkv
+// projection's launch-boundary reduce); the reduced, rotated q/k are written back to the bf16 qkv
+// row (the attention reads q from there).
+template <int D, bool SLAB>
+__global__ __launch_bounds__(128) void rope_cache_kernel(bf16_t* __restrict__ qkv, long qkv_stride,
                                                          const int* __restrict__ positions,
                                                          const float* __restrict__ cos_sin,  // [max_pos][D]: cos | sin
                                                          bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
                                                          const int* __restrict__ slot_mapping, int Hq, int Hkv,
-                                                         int block_size, int apply_rope) {
+                                                         int block_size, int apply_rope, const float* __restrict__ partial,
+                                                         int S, int T) {
   constexpr int HALF = D / 2;
   constexpr int QPH = D / 8;  // items per head
   const int t = blockIdx.x;
-  const int pos = positions[t];
+  const int n_rope = (Hq + Hkv) * QPH;
+  const int n_total = n_rope + Hkv * QPH;
+  const int w = blockIdx.y * 128 + threadIdx.x;
+  if (w >= n_total) return;
   const int slot = slot_mapping ? slot_mapping[t] : -1;
   const int blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot - blk * block_size : 0;
   bf16_t* row = qkv + (long)t * qkv_stride;
-  const float* cs = cos_sin + (long)pos * D;
-  const int n_rope = (Hq + Hkv) * QPH;
-  const int n_total = n_rope + Hkv * QPH;
-  for (int w = threadIdx.x; w < n_total; w += 256) {
-    if (w < n_rope) {
-      const int head = w / QPH;
-      const int p = (w - head * QPH) * 4;  // first of 4 pairs, p in [0, HALF)
-      bf16_t* hp = row + head * D;
-      uint2 a = *reinterpret_cast<const uint2*>(hp + p);
-      uint2 b = *reinterpret_cast<const uint2*>(hp + HALF + p);
-      float x1[4] = {lo_bf(a.x), hi_bf(a.x), lo_bf(a.y), hi_bf(a.y)};
-      float x2[4] = {lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
-      if (apply_rope) {
-        const float4 c = *reinterpret_cast<const float4*>(cs + p);
-        const float4 s = *reinterpret_cast<const float4*>(cs + HALF + p);
-        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float o1 = x1[j] * cc[j] - x2[j] * ss[j];
-          const float o2 = x2[j] * cc[j] + x1[j] * ss[j];
-          x1[j] = o1;
-          x2[j] = o2;
-        }
-      }
-      a.x = pack2(x1[0], x1[1]);
-      a.y = pack2(x1[2], x1[3]);
-      b.x = pack2(x2[0], x2[1]);
-      b.y = pack2(x2[2], x2[3]);
-      *reinterpret_cast<uint2*>(hp + p) = a;
-      *reinterpret_cast<uint2*>(hp + HALF + p) = b;
-      if (head >= Hq && slot >= 0) {
-        const int kh = head - Hq;
-        bf16_t* kb = k_cache + ((long)blk * Hkv + kh) * (D * block_size);
-        // dims p..p+3 live in piece p/8 at inner offset p%8 (4-aligned)
-        *reinterpret_cast<uint2*>(kb + ((p >> 3) * block_size + off) * 8 + (p & 7)) = a;
-        const int p2 = HALF + p;
-        *reinterpret_cast<uint2*>(kb + ((p2 >> 3) * block_size + off) * 8 + (p2 & 7)) = b;
-      }
-    } else if (slot >= 0) {
-      const int i = w - n_rope;
-      const int vh = i / QPH;
-      const int c = (i - vh * QPH) * 8;
-      const bf16_t* vp = row + (Hq + Hkv + vh) * D + c;
-      const uint4 v = *reinterpret_cast<const uint4*>(vp);
-      bf16_t* vb = v_cache + ((long)blk * Hkv + vh) * (D * block_size) + off;
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  const int ncols = (Hq + 2 * Hkv) * D;
+  const float* prow = SLAB ? partial + (long)t * ncols : nullptr;
+  const long slab_stride = (long)T * ncols;
+  if (w < n_rope) {
+    const int head = w / QPH;
+    const int p = (w - head * QPH) * 4;  // first of 4 pairs, p in [0, HALF)
+    bf16_t* hp = row + head * D;
+    float x1[4], x2[4];
+    if constexpr (SLAB) {
+      slab_sum<4>(prow + head * D + p, slab_stride, S, x1);
+      slab_sum<4>(prow + head * D + HALF + p, slab_stride, S, x2);
+    } else {
+      const uint2 a = *reinterpret_cast<const uint2*>(hp + p);
+      const uint2 b = *reinterpret_cast<const uint2*>(hp + HALF + p);
+      x1[0] = lo_bf(a.x); x1[1] = hi_bf(a.x); x1[2] = lo_bf(a.y); x1[3] = hi_bf(a.y);
+      x2[0] = lo_bf(b.x); x2[1] = hi_bf(b.x); x2[2] = lo_bf(b.y); x2[3] = hi_bf(b.y);
+    }
+    if constexpr (SLAB) {  // round to bf16 first, as an unfused GEMM output would be
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        vb[(long)(c + 2 * j) * block_size] = (bf16_t)(wv[j] & 0xffff);
-        vb[(long)(c + 2 * j + 1) * block_size] = (bf16_t)(wv[j] >> 16);
+        x1[j] = bf2f(f2bf(x1[j]));
+        x2[j] = bf2f(f2bf(x2[j]));
       }
+    }
+    if (apply_rope) {
+      const float* cs = cos_sin + (long)positions[t] * D;
+      const float4 c = *reinterpret_cast<const float4*>(cs + p);
+      const float4 s = *reinterpret_cast<const float4*>(cs + HALF + p);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float o1 = x1[j] * cc[j] - x2[j] * ss[j];
+        const float o2 = x2[j] * cc[j] + x1[j] * ss[j];
+        x1[j] = o1;
+        x2[j] = o2;
+      }
+    }
+    uint2 a, b;
+    a.x = pack2(x1[0], x1[1]);
+    a.y = pack2(x1[2], x1[3]);
+    b.x = pack2(x2[0], x2[1]);
+    b.y = pack2(x2[2], x2[3]);
+    *reinterpret_cast<uint2*>(hp + p) = a;
+    *reinterpret_cast<uint2*>(hp + HALF + p) = b;
+    if (head >= Hq && slot >= 0) {
+      const int kh = head - Hq;
+      bf16_t* kb = k_cache + ((long)blk * Hkv + kh) * (D * block_size);
+      // dims p..p+3 live in piece p/8 at inner offset p%8 (4-aligned)
+      *reinterpret_cast<uint2*>(kb + ((p >> 3) * block_size + off) * 8 + (p & 7)) = a;
+      const int p2 = HALF + p;
+      *reinterpret_cast<uint2*>(kb + ((p2 >> 3) * block_size + off) * 8 + (p2 & 7)) = b;
+    }
+  } else if (slot >= 0) {
+    const int i = w - n_rope;
+    const int vh = i / QPH;
+    const int c = (i - vh * QPH) * 8;
+    uint32_t wv[4];
+    if constexpr (SLAB) {
+      float f[8];
+      slab_sum<8>(prow + (Hq + Hkv + vh) * D + c, slab_stride, S, f);
+      const uint4 v = pack8(f);
+      wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + vh) * D + c);
+      wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+    }
+    bf16_t* vb = v_cache + ((long)blk * Hkv + vh) * (D * block_size) + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vb[(long)(c + 2 * j) * block_size] = (bf16_t)(wv[j] & 0xffff);
+      vb[(long)(c + 2 * j + 1) * block_size] = (bf16_t)(wv[j] >> 16);
     }
   }
 }
@@ -90,15 +131,21 @@ using namespace k8sllm;
 
 extern "C" int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, void* k_cache,
                                  void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D,
-                                 int block_size, int apply_rope, hipStream_t s) {
+                                 int block_size, int apply_rope, const float* partial, int S, hipStream_t s) {
   if (T <= 0) return 0;
-  if (D == 128)
-    hipLaunchKernelGGL((rope_cache_kernel<128>), dim3(T), dim3(256), 0, s, (bf16_t*)qkv, qkv_stride, positions,
-                       cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
-  else if (D == 64)
-    hipLaunchKernelGGL((rope_cache_kernel<64>), dim3(T), dim3(256), 0, s, (bf16_t*)qkv, qkv_stride, positions,
-                       cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
-  else
+  const int items = (Hq + 2 * Hkv) * (D / 8);
+  dim3 grid((unsigned)T, (items + 127) / 128);
+#define K8S_ROPE(DV, SL)                                                                                       \
+  hipLaunchKernelGGL((rope_cache_kernel<DV, SL>), grid, dim3(128), 0, s, (bf16_t*)qkv, qkv_stride, positions,  \
+                     cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope, \
+                     partial, S, (int)T)
+  if (D == 128) {
+    if (partial) K8S_ROPE(128, true); else K8S_ROPE(128, false);
+  } else if (D == 64) {
+    if (partial) K8S_ROPE(64, true); else K8S_ROPE(64, false);
+  } else {
     return -1;
+  }
+#undef K8S_ROPE
   return (int)hipGetLastError();
 }

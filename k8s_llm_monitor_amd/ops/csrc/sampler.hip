@@ -1,10 +1,18 @@
-// Token sampler over logits[B][V]: one 1024-thread workgroup per row.
+// Token sampler over logits[B][V].
 //   temperature <= 0        -> greedy argmax (first index on ties, like torch.argmax)
 //   temperature  > 0        -> Gumbel-max over logits/T  (exact sample from softmax(logits/T))
 //   top_k > 0 / top_p < 1   -> the kept set {x >= thr} is found by bisection on the threshold
 //                              (count for top-k, probability mass for top-p); no sort needed.
 // Randomness is a counter hash of (seed, offset, row, index); `rng` lives in device memory so a
 // hipGraph-captured decode step draws fresh numbers on every replay (the engine bumps offset).
+//
+// Decomposition: a decode batch has only B <= 64 rows, and Gumbel-max over a 128K vocabulary is
+// VALU-bound (hash + two logs per element), so one workgroup per row used 64 of 256 CUs and took
+// 125 us at B = 64.  Rows are split into P parts: grid (B, P) of 1024-thread workgroups each
+// produce a partial (value, index) argmax, and a one-wave kernel picks the winner per row.  Rows
+// with top-k / top-p need a row-wide threshold; part 0 of such a row runs the whole-row bisection
+// path and its answer is taken as is.  The per-element hash is 32-bit (two murmur3 finalisers of
+// a per-row 64-bit key) - 64-bit multiplies are multi-instruction sequences on CDNA.
 #include "common.h"
 
 namespace k8sllm {
@@ -25,9 +33,24 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ float gumbel(uint64_t seed, uint64_t off, int row, int i) {
-  const uint64_t h = mix64(seed ^ mix64(off * 0x100000001b3ull + (uint64_t)row * 0x9e3779b97ull + (uint64_t)i));
-  const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint64_t row_key(const int64_t* rng, int row) {
+  const uint64_t seed = rng ? (uint64_t)rng[0] : 0ull;
+  const uint64_t off = rng ? (uint64_t)rng[1] : 0ull;
+  return mix64(seed ^ mix64(off * 0x100000001b3ull + (uint64_t)row * 0x9e3779b97ull));
+}
+
+__device__ __forceinline__ float gumbel(uint64_t key, int i) {
+  const uint32_t h = fmix32(fmix32((uint32_t)i * 0x9e3779b9u ^ (uint32_t)key) + (uint32_t)(key >> 32));
+  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
   return -__logf(-__logf(u));
 }
 
@@ -59,29 +82,12 @@ __device__ __forceinline__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   return r;
 }
 
+// Whole-row path for rows with top-k / top-p (one workgroup); returns the token on every thread.
 template <typename T>
-__global__ __launch_bounds__(kST) void sample_kernel(int* __restrict__ out, const T* __restrict__ logits, long stride,
-                                                     int V, const float* __restrict__ temps,
-                                                     const int* __restrict__ top_k, const float* __restrict__ top_p,
-                                                     const int64_t* __restrict__ rng) {
-  __shared__ float sv[kST / 64];
-  __shared__ int si[kST / 64];
-  const int row = blockIdx.x;
-  const T* x = logits + (long)row * stride;
-  const float temp = temps ? temps[row] : 0.f;
+__device__ int sample_row_filtered(const T* __restrict__ x, int V, float temp, int k, float p, uint64_t key,
+                                   float* sv, int* si) {
   const int tid = threadIdx.x;
-
-  if (!(temp > 0.f)) {
-    ArgMax a{-INFINITY, 0x7fffffff};
-    for (int i = tid; i < V; i += kST) a = better(a, ArgMax{ld<T>(x, i), i});
-    a = block_argmax(a, sv, si);
-    if (tid == 0) out[row] = a.i;
-    return;
-  }
-
   const float itemp = 1.f / temp;
-  const int k = top_k ? top_k[row] : 0;
-  const float p = top_p ? top_p[row] : 1.f;
   float mx = -INFINITY, mn = INFINITY;
   for (int i = tid; i < V; i += kST) {
     const float v = ld<T>(x, i) * itemp;
@@ -120,30 +126,102 @@ __global__ __launch_bounds__(kST) void sample_kernel(int* __restrict__ out, cons
     }
     thr = fmaxf(thr, lo);
   }
-  const uint64_t seed = rng ? (uint64_t)rng[0] : 0ull;
-  const uint64_t off = rng ? (uint64_t)rng[1] : 0ull;
   ArgMax a{-INFINITY, 0x7fffffff};
   for (int i = tid; i < V; i += kST) {
     const float v = ld<T>(x, i) * itemp;
-    if (v >= thr) a = better(a, ArgMax{v + gumbel(seed, off, row, i), i});
+    if (v >= thr) a = better(a, ArgMax{v + gumbel(key, i), i});
+  }
+  return block_argmax(a, sv, si).i;
+}
+
+__device__ __forceinline__ bool row_filtered(int V, float temp, int k, float p) {
+  return temp > 0.f && ((k > 0 && k < V) || p < 1.f);
+}
+
+// grid (B, P): partial argmax of part `blockIdx.y` of row `blockIdx.x` -> pv/pi[row * P + part]
+template <typename T>
+__global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__ pv, int* __restrict__ pi,
+                                                             const T* __restrict__ logits, long stride, int V, int P,
+                                                             const float* __restrict__ temps,
+                                                             const int* __restrict__ top_k,
+                                                             const float* __restrict__ top_p,
+                                                             const int64_t* __restrict__ rng) {
+  __shared__ float sv[kST / 64];
+  __shared__ int si[kST / 64];
+  const int row = blockIdx.x, part = blockIdx.y, tid = threadIdx.x;
+  const T* x = logits + (long)row * stride;
+  const float temp = temps ? temps[row] : 0.f;
+  const int k = top_k ? top_k[row] : 0;
+  const float p = top_p ? top_p[row] : 1.f;
+  if (row_filtered(V, temp, k, p)) {
+    if (part != 0) return;
+    const int tok = sample_row_filtered<T>(x, V, temp, k, p, row_key(rng, row), sv, si);
+    if (tid == 0) pi[row * P] = tok;
+    return;
+  }
+  const int chunk = (V + P - 1) / P;
+  const int lo = part * chunk, hi = min(V, lo + chunk);
+  ArgMax a{-INFINITY, 0x7fffffff};
+  if (!(temp > 0.f)) {
+    for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i), i});
+  } else {
+    const float itemp = 1.f / temp;
+    const uint64_t key = row_key(rng, row);
+    for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i) * itemp + gumbel(key, i), i});
   }
   a = block_argmax(a, sv, si);
-  if (tid == 0) out[row] = a.i;
+  if (tid == 0) {
+    pv[row * P + part] = a.v;
+    pi[row * P + part] = a.i;
+  }
+}
+
+// one thread per row: the best of the P partials (or part 0's answer for a filtered row)
+__global__ __launch_bounds__(64) void sample_final_kernel(int* __restrict__ out, const float* __restrict__ pv,
+                                                          const int* __restrict__ pi, int B, int V, int P,
+                                                          const float* __restrict__ temps,
+                                                          const int* __restrict__ top_k,
+                                                          const float* __restrict__ top_p) {
+  const int row = blockIdx.x * 64 + threadIdx.x;
+  if (row >= B) return;
+  const float temp = temps ? temps[row] : 0.f;
+  const int k = top_k ? top_k[row] : 0;
+  const float p = top_p ? top_p[row] : 1.f;
+  if (row_filtered(V, temp, k, p)) {
+    out[row] = pi[row * P];
+    return;
+  }
+  ArgMax a{pv[row * P], pi[row * P]};
+  for (int j = 1; j < P; ++j) a = better(a, ArgMax{pv[row * P + j], pi[row * P + j]});
+  out[row] = a.i;
 }
 
 }  // namespace k8sllm
 
 using namespace k8sllm;
 
+extern "C" int k8sllm_sample_parts(long B, int V) {
+  // ~2 workgroups per CU in total, at least 8K vocabulary entries per part
+  long p = (512 + B - 1) / B;
+  p = p < 1 ? 1 : p;
+  const long pmax = V / 8192 > 1 ? V / 8192 : 1;
+  return (int)(p < pmax ? p : pmax);
+}
+
+// pv/pi: workspace of at least B * k8sllm_sample_parts(B, V) entries
 extern "C" int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V,
                              const float* temps, const int* top_k, const float* top_p, const int64_t* rng,
-                             hipStream_t s) {
+                             float* pv, int* pi, hipStream_t s) {
   if (B <= 0) return 0;
+  const int P = k8sllm_sample_parts(B, V);
+  dim3 grid((unsigned)B, P);
   if (is_fp32)
-    hipLaunchKernelGGL((sample_kernel<float>), dim3(B), dim3(kST), 0, s, out, (const float*)logits, stride, V, temps,
-                       top_k, top_p, rng);
+    hipLaunchKernelGGL((sample_partial_kernel<float>), grid, dim3(kST), 0, s, pv, pi, (const float*)logits, stride,
+                       V, P, temps, top_k, top_p, rng);
   else
-    hipLaunchKernelGGL((sample_kernel<bf16_t>), dim3(B), dim3(kST), 0, s, out, (const bf16_t*)logits, stride, V,
-                       temps, top_k, top_p, rng);
+    hipLaunchKernelGGL((sample_partial_kernel<bf16_t>), grid, dim3(kST), 0, s, pv, pi, (const bf16_t*)logits,
+                       stride, V, P, temps, top_k, top_p, rng);
+  hipLaunchKernelGGL(sample_final_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, out, pv, pi, (int)B, V, P,
+                     temps, top_k, top_p);
   return (int)hipGetLastError();
 }

@@ -206,3 +206,94 @@ def test_moe_route_align_combine():
     assert torch.equal(xs.cpu(), x.cpu()[srt.cpu().long() // K])
     y = ops.moe_combine(xs, inv, w, T)
     _close(y, ref.moe_combine(xs.cpu(), inv.cpu(), w.cpu(), T).to(DEV), atol=2e-2, rtol=1e-2, what="combine")
+
+
+@pytest.mark.parametrize("splits", [1, 4, 7])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 512), (7, 4096, 4096), (16, 128, 1024), (33, 640, 14336),
+                                   (64, 4096, 4096), (50, 6144, 4096)])
+def test_gemm_skinny(M, N, K, splits):
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    y = ops.gemm_skinny(a, w, splits=splits)
+    y_ref = torch.nn.functional.linear(a.cpu().float(), w.cpu().float())
+    _close(y.cpu(), y_ref, atol=3e-2, rtol=2e-2, what=f"gemm_skinny M{M} N{N} K{K} s{splits}")
+
+
+@pytest.mark.parametrize("nt_tiles", [2, 4])
+def test_gemm_skinny_nt_tiles(nt_tiles):
+    a = torch.randn(24, 1024, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(96, 1024, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    if 96 % (16 * nt_tiles):
+        pytest.skip("tile does not divide N")
+    y = ops.skinny_linear(a, ops.pack_skinny(w), nt_tiles=nt_tiles)
+    _close(y.cpu(), torch.nn.functional.linear(a.cpu().float(), w.cpu().float()), atol=3e-2, rtol=2e-2,
+           what="nt_tiles")
+
+
+@pytest.mark.parametrize("M", [1, 9, 64])
+def test_skinny_swiglu(M):
+    K, F = 1024, 448
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    act = ops.skinny_swiglu(x, ops.pack_skinny(ops.interleave_gate_up(w13)))
+    gu = torch.nn.functional.linear(x.cpu().float(), w13.cpu().float()).to(torch.bfloat16)
+    _close(act.cpu(), ref.silu_mul(gu), atol=3e-2, rtol=2e-2, what="swiglu")
+
+
+@pytest.mark.parametrize("M", [1, 24, 64])
+def test_proj_add_rms_norm(M):
+    d, K = 4096, 1024
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(d, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    r = torch.randn(M, d, device=DEV, dtype=torch.bfloat16)
+    nw = torch.randn(d, device=DEV, dtype=torch.bfloat16)
+    s_ref = (r.cpu().float() + torch.nn.functional.linear(a.cpu().float(), w.cpu().float())).to(torch.bfloat16)
+    y_ref = ref.rms_norm(s_ref, nw.cpu(), 1e-5)
+    y = ops.proj_add_rms_norm(a, ops.pack_skinny(w), r, nw, 1e-5, splits=4)
+    _close(r.cpu(), s_ref, atol=3e-2, rtol=1e-2, what="residual")
+    _close(y.cpu(), y_ref, atol=5e-2, rtol=2e-2, what="normed")
+
+
+def test_rope_and_cache_from_slabs():
+    """rope_and_cache reducing split-K qkv slabs == rope_and_cache on the summed bf16 qkv."""
+    hq, hkv, D, T, S, bs = 32, 8, 128, 19, 5, 16
+    ncol = (hq + 2 * hkv) * D
+    part = torch.randn(S, T, ncol, device=DEV, dtype=torch.float32) * 0.3
+    pos = torch.randint(0, 500, (T,), dtype=torch.int32, device=DEV)
+    cs = ref.rope_cos_sin(2048, D, 500000.0, None, device=DEV)
+    slots = torch.randperm(4 * bs, device=DEV)[:T].to(torch.int32)
+    caches = [(torch.zeros(4, hkv, D // 8, bs, 8, device=DEV, dtype=torch.bfloat16),
+               torch.zeros(4, hkv, D, bs, device=DEV, dtype=torch.bfloat16)) for _ in range(2)]
+    qkv_a = torch.empty(T, ncol, device=DEV, dtype=torch.bfloat16)
+    ops.rope_and_cache(qkv_a, pos, cs, caches[0][0], caches[0][1], slots, hq, hkv, D, partial=part.reshape(-1),
+                       nslabs=S)
+    qkv_b = part.sum(0).to(torch.bfloat16)
+    ops.rope_and_cache(qkv_b, pos, cs, caches[1][0], caches[1][1], slots, hq, hkv, D)
+    _close(qkv_a[:, : (hq + hkv) * D], qkv_b[:, : (hq + hkv) * D], atol=2e-2, rtol=1e-2, what="qk")
+    _close(caches[0][0], caches[1][0], atol=2e-2, rtol=1e-2, what="k cache")
+    _close(caches[0][1], caches[1][1], atol=2e-2, rtol=1e-2, what="v cache")
+
+
+def test_llama_decode_skinny_matches_generic(monkeypatch):
+    """The fused decode tail must give the same logits as the hipBLASLt + fused_add_rms_norm path."""
+    from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
+
+    cfg = get_config("llama-tiny-d128")
+    m = CausalLM(cfg, device=DEV, seed=3)
+    assert m._skinny_ws is not None
+    B, bs = 5, 16
+    nb = 8
+    kv = [(torch.randn(nb, m.hkv, m.D // 8, bs, 8, device=DEV, dtype=torch.bfloat16),
+           torch.randn(nb, m.hkv, m.D, bs, device=DEV, dtype=torch.bfloat16)) for _ in m.layers]
+    lens = torch.tensor([3, 17, 1, 30, 9], dtype=torch.int32, device=DEV)
+    bt = torch.arange(B * 2, dtype=torch.int32, device=DEV).view(B, 2) % nb
+    ids = torch.randint(0, cfg.vocab_size, (B,), dtype=torch.int32, device=DEV)
+    meta = AttnMeta(is_prefill=False, positions=lens - 1, slot_mapping=torch.full((B,), -1, dtype=torch.int32,
+                                                                                 device=DEV),
+                    block_tables=bt, seq_lens=lens,
+                    decode_ws=ops.decode_workspace(B, m.hq, m.D, device=DEV, Hkv=m.hkv))
+    a = m.forward(ids, meta, kv).float()
+    monkeypatch.setenv("K8SLLM_SKINNY", "0")
+    b = m.forward(ids, meta, kv).float()
+    assert (a - b).abs().max().item() < 0.1 * b.abs().max().item() + 0.05
+    assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.8

@@ -1,0 +1,37 @@
+"""Host-side layout helpers of the decode skinny GEMM (the GPU numerics are in test_ops_gpu.py)."""
+import torch
+
+from k8s_llm_monitor_amd import ops
+
+
+def test_pack_roundtrip_and_fragment_order():
+    N, K = 48, 96
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K)
+    wp = ops.pack_skinny(w)
+    assert wp.shape == (N // 16, K // 32, 64, 8)
+    assert torch.equal(ops.unpack_skinny(wp), w)
+    # block (j, s), lane l = 16 q + r holds W[16 j + r, 32 s + 8 q : +8]
+    j, s, q, r = 2, 1, 3, 5
+    assert torch.equal(wp[j, s, 16 * q + r], w[16 * j + r, 32 * s + 8 * q: 32 * s + 8 * q + 8])
+
+
+def test_interleave_gate_up():
+    F, K = 64, 32
+    g = torch.full((F, K), 1.0)
+    u = torch.full((F, K), 2.0)
+    g[:, 0] = torch.arange(F)
+    u[:, 0] = torch.arange(F)
+    w = ops.interleave_gate_up(torch.cat([g, u]))
+    # tile t (64 rows) = gate rows 32t..32t+31 then up rows 32t..32t+31
+    assert torch.equal(w[:32, 1], torch.ones(32)) and torch.equal(w[32:64, 1], torch.full((32,), 2.0))
+    assert torch.equal(w[64:96, 0], torch.arange(32, 64, dtype=torch.float32))
+
+
+def test_skinny_splits_bounds(monkeypatch):
+    monkeypatch.delenv("K8SLLM_SKINNY_SPLITS", raising=False)
+    assert ops.skinny_splits(4096, 4096) == 8
+    assert ops.skinny_splits(4096, 14336) == 8
+    assert ops.skinny_splits(6144, 4096) == 5
+    assert ops.skinny_splits(64, 256) == 1
+    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")
+    assert ops.skinny_splits(4096, 4096) == 3
