@@ -37,11 +37,13 @@ def main(argv=None) -> int:
             pstate = init_parallel(tp_size=cfg.llm.tp_size)
             if pstate.tp_rank != 0:  # TP worker: no HTTP, mirror the leader's engine steps
                 from ..engine import EngineConfig, LLMEngine
+                from ..monitor.app import torch_dtype_name
 
                 eng = LLMEngine(EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch,
                                              max_model_len=cfg.llm.max_model_len, kv_cache_gb=cfg.llm.kv_cache_gb,
                                              use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
-                                             tp_size=cfg.llm.tp_size), pstate=pstate)
+                                             tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype)),
+                                pstate=pstate)
                 eng.warmup()
                 log.info("TP worker rank %d ready", pstate.rank)
                 eng.worker_loop()

@@ -46,6 +46,7 @@ class EngineConfig:
     use_graphs: bool = True
     seed: int = 0
     tp_size: int = 1
+    dtype: str = "bfloat16"  # compute / weight dtype ("float32" for CPU parity tests)
     model_overrides: dict = field(default_factory=dict)
 
 
@@ -73,7 +74,7 @@ class LLMEngine:
             mc = mc.replace(**cfg.model_overrides)
         self.model_cfg = mc
         t0 = time.perf_counter()
-        self.model = CausalLM(mc, device=self.device, seed=cfg.seed, pstate=self.ps)
+        self.model = CausalLM(mc, device=self.device, dtype=getattr(torch, cfg.dtype), seed=cfg.seed, pstate=self.ps)
         self.runner = ModelRunner(self.model, RunnerConfig(
             max_num_seqs=cfg.max_num_seqs, max_model_len=cfg.max_model_len, kv_cache_gb=cfg.kv_cache_gb,
             num_blocks=cfg.num_blocks, use_graphs=cfg.use_graphs, seed=cfg.seed))

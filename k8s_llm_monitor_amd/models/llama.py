@@ -342,12 +342,13 @@ class CausalLM:
         the slabs, RoPE, KV write) -> paged_decode -> o skinny (slabs) -> reduce_add_rms_norm
         (residual add + mlp norm) -> gate_up skinny with the SwiGLU epilogue -> down skinny
         (slabs) -> reduce_add_rms_norm (residual add + next layer's attn norm).
-        TP>1 keeps hipBLASLt + RCCL all-reduce (row-parallel partial sums must be reduced across
-        ranks before the residual add)."""
+        TP>1: the column-parallel qkv / gate_up are unchanged; the row-parallel o / down sum their
+        slabs to bf16 (reduce_slabs), all-reduce over RCCL, then fused_add_rms_norm.
+        On the CPU the same ops run as fp32 references with the kernels' split-K slicing, so the
+        control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         c = self.cfg
-        if (self.device.type != "cuda" or self.tp != 1 or c.arch != "llama" or c.is_moe
-                or os.environ.get("K8SLLM_SKINNY", "1") == "0"):
+        if c.arch != "llama" or c.is_moe or os.environ.get("K8SLLM_SKINNY", "1") == "0":
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
         if d % 64 or nq % 64 or (self.hq * self.D) % 32 or self.f_local % 32:
@@ -369,13 +370,20 @@ class CausalLM:
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
             o = self._attn_core(L, x, meta, kv, slabs=(ws, self._split_qkv))
-            x = ops.proj_add_rms_norm(o, L["wo_p"], residual, L["mlp_norm"], c.norm_eps, workspace=ws,
-                                      splits=self._split_o)
+            x = self._row_parallel_tail(o, L["wo_p"], residual, L["mlp_norm"], self._split_o)
             act = ops.skinny_swiglu(x, L["w13_p"])
             nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
-            x = ops.proj_add_rms_norm(act, L["w2_p"], residual, nw, c.norm_eps, workspace=ws,
-                                      splits=self._split_d)
+            x = self._row_parallel_tail(act, L["w2_p"], residual, nw, self._split_d)
         return self._logits(x)
+
+    def _row_parallel_tail(self, a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w,
+                           splits: int) -> torch.Tensor:
+        eps, ws = self.cfg.norm_eps, self._skinny_ws
+        if self.tp == 1:
+            return ops.proj_add_rms_norm(a, wp, residual, norm_w, eps, workspace=ws, splits=splits)
+        ns = ops.skinny_slabs(a, wp, ws, splits)
+        y = ops.reduce_slabs(ws, ns, a.shape[0], wp.shape[0] * 16, dtype=residual.dtype)
+        return ops.fused_add_rms_norm(tp_all_reduce(y, self.ps), residual, norm_w, eps)
 
 
 _DUMMY_CS: dict = {}

@@ -72,7 +72,7 @@ def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):
 
         ecfg = EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch, max_model_len=cfg.llm.max_model_len,
                             kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
-                            tp_size=cfg.llm.tp_size)
+                            tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype))
         eng = LLMEngine(ecfg, device=device, pstate=pstate)
         eng.warmup()
         svc = EngineService(eng)
@@ -184,3 +184,14 @@ def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0
 
     with cf.ThreadPoolExecutor(max_workers=concurrency or len(items)) as ex:
         return list(ex.map(one, items))
+
+
+def torch_dtype_name(s: str) -> str:
+    """``llm.dtype`` ("bf16" / "bfloat16" / "fp16" / "fp32" ...) -> torch dtype attribute name."""
+    m = {"bf16": "bfloat16", "bfloat16": "bfloat16", "fp16": "float16", "float16": "float16", "half": "float16",
+         "fp32": "float32", "float32": "float32", "float": "float32"}
+    try:
+        return m[(s or "bf16").lower()]
+    except KeyError:
+        raise ValueError(f"unsupported llm.dtype {s!r}") from None
+

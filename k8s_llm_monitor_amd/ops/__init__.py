@@ -118,9 +118,38 @@ def _skinny_ntl() -> bool:
     return os.environ.get("K8SLLM_SKINNY_NT", "1") != "0"
 
 
+def skinny_kchunk(K: int, S: int) -> int:
+    """The K slice of each split (mirror of skinny_kchunk in gemm_skinny.hip): rounded up to whole
+    128-deep wave groups where that keeps S slices, else to whole 32-deep k-steps."""
+    kc = -(-K // S)
+    kc128 = -(-kc // 128) * 128
+    if -(-K // kc128) == S:
+        return kc128
+    return -(-kc // 32) * 32
+
+
+def skinny_nslabs(K: int, S: int) -> int:
+    return -(-K // skinny_kchunk(K, S))
+
+
+# CPU forms of the skinny ops: the same packed layouts, split-K slicing and roundings as the
+# kernels, so the decode control flow (and TP over gloo) is exercised by the CPU test suite.
+def _cpu_w(wp: torch.Tensor) -> torch.Tensor:
+    return unpack_skinny(wp).float()
+
+
+def _cpu_deinterleave(gu: torch.Tensor) -> tuple:
+    M, F2 = gu.shape
+    t = gu.reshape(M, F2 // 64, 2, 32)
+    return t[:, :, 0].reshape(M, F2 // 2), t[:, :, 1].reshape(M, F2 // 2)
+
+
 def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,
                   nt_tiles: int = 4) -> torch.Tensor:
-    """``a @ W^T`` (bf16) for <= 64 rows over the fragment-packed weight, one K slice."""
+    """``a @ W^T`` for <= 64 rows over the fragment-packed weight, one K slice."""
+    if not _gpu(a):
+        y = (a.float() @ _cpu_w(wp).t()).to(a.dtype)
+        return out.copy_(y) if out is not None else y
     N = wp.shape[0] * 16
     if out is None:
         out = torch.empty(a.shape[0], N, dtype=a.dtype, device=a.device)
@@ -130,6 +159,10 @@ def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor]
 
 def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F]."""
+    if not _gpu(a):
+        g, u = _cpu_deinterleave((a.float() @ _cpu_w(wp13).t()).to(a.dtype).float())
+        y = (torch.nn.functional.silu(g) * u).to(a.dtype)
+        return out.copy_(y) if out is not None else y
     F = wp13.shape[0] * 8
     if out is None:
         out = torch.empty(a.shape[0], F, dtype=a.dtype, device=a.device)
@@ -140,15 +173,48 @@ def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tenso
 def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, splits: int,
                  nt_tiles: int = 4) -> int:
     """Split-K ``a @ W^T`` into fp32 slabs [S', M, N] in ``workspace``; returns S'."""
+    if not _gpu(a):
+        M, N, K = a.shape[0], wp.shape[0] * 16, wp.shape[1] * 32
+        kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
+        w = _cpu_w(wp)
+        slabs = workspace[: ns * M * N].view(ns, M, N)
+        for s in range(ns):
+            slabs[s] = a[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].t()
+        return ns
     return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, _skinny_ntl())
+
+
+def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=torch.bfloat16,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum of ``nslabs`` split-K slabs [nslabs, M, N] -> [M, N] in ``dtype`` (TP>1 tails, before
+    the all-reduce)."""
+    if not _gpu(workspace):
+        y = workspace[: nslabs * M * N].view(nslabs, M, N).sum(0).to(dtype)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(M, N, dtype=dtype, device=workspace.device)
+    native().reduce_slabs(out, workspace, nslabs)
+    return out
+
+
+def reduce_add_rms_norm(out: torch.Tensor, residual: torch.Tensor, workspace: torch.Tensor, nslabs: int,
+                        norm_w: torch.Tensor, eps: float) -> torch.Tensor:
+    """``residual <- residual + sum of slabs`` (rounded to the residual dtype), ``out <- rms_norm``."""
+    if not _gpu(residual):
+        M, N = residual.shape
+        s = workspace[: nslabs * M * N].view(nslabs, M, N).sum(0)
+        residual.copy_((residual.float() + s).to(residual.dtype))
+        return out.copy_(ref.rms_norm(residual, norm_w, eps))
+    native().reduce_add_rms_norm(out, residual, workspace, nslabs, norm_w, eps)
+    return out
 
 
 def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
                       workspace: Optional[torch.Tensor] = None, splits: Optional[int] = None,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The decode tail of an attention or MLP block in one GEMM + one reduce:
-    ``residual <- bf16(residual + a @ W^T)``; returns ``rms_norm(residual) * norm_w``.
-    GPU only: gemm_skinny (packed ``wp``, split-K fp32 slabs) then reduce_add_rms_norm."""
+    ``residual <- residual + a @ W^T``; returns ``rms_norm(residual) * norm_w``.  GPU: gemm_skinny
+    (packed ``wp``, split-K fp32 slabs) then reduce_add_rms_norm."""
     M, N, K = a.shape[0], wp.shape[0] * 16, wp.shape[1] * 32
     if splits is None:
         splits = skinny_splits(N, K)
@@ -157,19 +223,18 @@ def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor,
     s = skinny_slabs(a, wp, workspace, splits)
     if out is None:
         out = torch.empty(M, N, dtype=residual.dtype, device=a.device)
-    native().reduce_add_rms_norm(out, residual, workspace, s, norm_w, eps)
-    return out
+    return reduce_add_rms_norm(out, residual, workspace, s, norm_w, eps)
 
 
 def gemm_skinny(a: torch.Tensor, w: torch.Tensor, splits: int = 1) -> torch.Tensor:
-    """``a @ w^T`` through the skinny kernel from a row-major weight (tests / tools); bf16."""
+    """``a @ w^T`` through the skinny kernel from a row-major weight (tests / tools)."""
     wp = pack_skinny(w)
     if splits == 1:
         return skinny_linear(a, wp)
     M, N = a.shape[0], w.shape[0]
     ws = skinny_workspace(M, N, splits, a.device)
     s = skinny_slabs(a, wp, ws, splits)
-    return ws[: s * M * N].view(s, M, N).sum(0).to(a.dtype)
+    return reduce_slabs(ws, s, M, N, a.dtype)
 
 
 def layer_norm(x, w, b, eps):
@@ -219,6 +284,9 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
     With ``partial`` (GPU), the QKV values are first reduced from ``nslabs`` fp32 split-K slabs
     [nslabs, T, (Hq+2Hkv)*D] (skinny_slabs) and the reduced rows are written to ``qkv``."""
     if not _gpu(qkv):
+        if partial is not None:
+            T, n = qkv.shape[0], qkv.shape[1]
+            qkv.copy_(partial[: nslabs * T * n].view(nslabs, T, n).sum(0).to(qkv.dtype))
         ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, Hq, Hkv, D, apply_rope)
         return
     empty = _empty_i32(qkv.device)

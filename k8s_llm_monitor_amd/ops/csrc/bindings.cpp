@@ -36,6 +36,7 @@ int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, 
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int ntl, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
+int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
                               float eps, hipStream_t s);
 }
@@ -272,6 +273,14 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   return S;
 }
 
+void reduce_slabs(torch::Tensor out, torch::Tensor partial, int64_t S) {
+  dev_bf16(out, "out");
+  TORCH_CHECK(out.is_contiguous(), "reduce_slabs: out must be contiguous");
+  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == torch::kFloat32 && partial.is_contiguous(), "partial");
+  TORCH_CHECK(partial.numel() >= S * out.numel(), "reduce_slabs: partial too small");
+  check(k8sllm_reduce_slabs(out.data_ptr(), partial.data_ptr<float>(), (int)S, out.numel(), cur()), "reduce_slabs");
+}
+
 void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, torch::Tensor partial, int64_t S,
                          torch::Tensor w, double eps) {
   dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
@@ -304,4 +313,5 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
+  m.def("reduce_slabs", &reduce_slabs);
 }

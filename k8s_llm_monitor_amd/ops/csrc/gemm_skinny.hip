@@ -179,9 +179,33 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
   }
 }
 
+// out[i] = bf16(sum_s partial[s][i]) over n elements (n % 8 == 0): the TP>1 decode tails sum
+// the split-K slabs before the RCCL all-reduce.
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(bf16_t* __restrict__ out,
+                                                           const float* __restrict__ partial, int S, long n) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const float4 a = *reinterpret_cast<const float4*>(partial + s * n + i);
+    const float4 b = *reinterpret_cast<const float4*>(partial + s * n + i + 4);
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  }
+  *reinterpret_cast<uint4*>(out + i) = pack8(acc);
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+extern "C" int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 8 != 0 || S < 1) return -1;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, s, (bf16_t*)out,
+                     partial, S, n);
+  return (int)hipGetLastError();
+}
 
 // kchunk: K split into `S` slices rounded up to whole wave groups (128 k) where that keeps the
 // slice count, else to whole k-steps.

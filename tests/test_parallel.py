@@ -40,7 +40,8 @@ def _worker(rank, world, port, model, q):
         b = ref_model.forward(ids, meta, None)
         err = (a - b).abs().max().item()
         # engine: leader generates, worker mirrors; compare with a TP=1 engine in the same process
-        ecfg = EngineConfig(model=model, max_num_seqs=4, max_model_len=128, num_blocks=64, use_graphs=False, seed=5)
+        ecfg = EngineConfig(model=model, max_num_seqs=4, max_model_len=128, num_blocks=64, use_graphs=False, seed=5,
+                            dtype="float32")  # fp32: TP vs TP=1 rounding must not flip greedy ties
         eng = LLMEngine(ecfg, device="cpu", pstate=ps)
         toks = None
         if ps.tp_rank == 0:

@@ -35,3 +35,26 @@ def test_skinny_splits_bounds(monkeypatch):
     assert ops.skinny_splits(64, 256) == 1
     monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")
     assert ops.skinny_splits(4096, 4096) == 3
+
+
+def test_decode_skinny_path_matches_generic_cpu(monkeypatch):
+    """The decode control flow over packed weights (split-K slabs reduced in rope / the norm tail,
+    SwiGLU epilogue) equals the generic path, on the CPU forms of the ops (fp32)."""
+    from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
+
+    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")  # force real split-K slicing on tiny shapes
+    cfg = get_config("llama-tiny-d128")
+    m = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
+    assert m._skinny_ws is not None and m._split_d == 3
+    B, bs, nb = 3, 16, 8
+    g = torch.Generator().manual_seed(0)
+    kv = [(torch.randn(nb, m.hkv, m.D // 8, bs, 8, generator=g), torch.randn(nb, m.hkv, m.D, bs, generator=g))
+          for _ in m.layers]
+    lens = torch.tensor([3, 17, 9], dtype=torch.int32)
+    meta = AttnMeta(is_prefill=False, positions=lens - 1, slot_mapping=torch.full((B,), -1, dtype=torch.int32),
+                    block_tables=torch.arange(B * 2, dtype=torch.int32).view(B, 2) % nb, seq_lens=lens)
+    ids = torch.tensor([5, 77, 300], dtype=torch.int32)
+    a = m.forward(ids, meta, kv)
+    monkeypatch.setenv("K8SLLM_SKINNY", "0")
+    b = m.forward(ids, meta, kv)
+    assert (a - b).abs().max().item() < 1e-4
