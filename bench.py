@@ -37,7 +37,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--kv-cache-gb", type=float, default=48.0)
-    ap.add_argument("--path", choices=["http", "engine"], default="http")
+    ap.add_argument("--path", choices=["http", "engine", "podcomm"], default="http",
+                    help="http: POST /api/v1/query (headline); podcomm: POST /api/v1/analyze/pod-communication "
+                         "with the LLM explanation (BASELINE config 3); engine: the engine queue directly")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
@@ -65,7 +67,7 @@ def main() -> None:
     eng.warmup()
     svc = EngineService(eng)
     server = None
-    if a.path == "http":
+    if a.path in ("http", "podcomm"):
         from k8s_llm_monitor_amd.monitor.app import build_app_for_bench
 
         server, port = build_app_for_bench(svc)
@@ -78,6 +80,14 @@ def main() -> None:
 
             items = [synthetic_context(s)[::-1] for s in seeds]  # (question, cluster context)
             res = post_queries(port, items, a.max_new_tokens)
+            lat = [r["http_latency_ms"] for r in res]
+            ptok = sum(r["prompt_tokens"] for r in res)
+            gtok = sum(r["completion_tokens"] for r in res)
+        elif a.path == "podcomm":
+            from k8s_llm_monitor_amd.monitor.app import bench_pod_pairs, post_pod_communication
+
+            pairs = bench_pod_pairs(a.batch * (w + 1))[a.batch * w:]
+            res = post_pod_communication(port, pairs, a.max_new_tokens)
             lat = [r["http_latency_ms"] for r in res]
             ptok = sum(r["prompt_tokens"] for r in res)
             gtok = sum(r["completion_tokens"] for r in res)
@@ -116,8 +126,10 @@ def main() -> None:
         server.shutdown()
     if rank == 0:
         qps = total_q / t_max
+        metric = ("pod-communication analyses/sec (Llama-3-8B TP=1, /api/v1/analyze/pod-communication)"
+                  if a.path == "podcomm" else "diagnostic queries/sec (Llama-3-8B TP=1, /api/v1/query)")
         res = {
-            "metric": "diagnostic queries/sec (Llama-3-8B TP=1, /api/v1/query)",
+            "metric": metric,
             "value": round(qps, 4),
             "unit": "queries/s",
             "n_gpus": world,

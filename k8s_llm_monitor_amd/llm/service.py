@@ -243,7 +243,8 @@ class AnalysisService:
         return self._respond(uuid.uuid4().hex, kind, prompt, {"parameters": params},
                              int(params.get("max_tokens") or 0) or None)
 
-    def explain_pod_communication(self, analysis) -> AnalysisResponse:
+    def explain_pod_communication(self, analysis, max_tokens: Optional[int] = None,
+                                  ignore_eos: bool = False) -> AnalysisResponse:
         facts = []
         if self.client is not None:
             from ..monitor.analysis.network import parse_pod_name
@@ -261,4 +262,5 @@ class AnalysisService:
             rtt = (f"RTT测试: 成功率 {last.success_rate:.1f}%, 平均 {last.average_rtt:.2f}ms, "
                    f"评级 {last.latency}\n")
         prompt = P.build_pod_communication_prompt(analysis, "\n".join(facts), rtt)
-        return self._respond(uuid.uuid4().hex, "pod_communication", prompt, {"analysis": gojson.to_plain(analysis)})
+        return self._respond(uuid.uuid4().hex, "pod_communication", prompt, {"analysis": gojson.to_plain(analysis)},
+                             max_tokens, ignore_eos)

@@ -186,6 +186,44 @@ def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0
         return list(ex.map(one, items))
 
 
+def post_pod_communication(port: int, pairs: list, max_new_tokens: int, host: str = "127.0.0.1") -> list:
+    """Fire ``pairs`` = [(pod_a, pod_b)] as concurrent POST /api/v1/analyze/pod-communication with
+    the LLM explanation (BASELINE config 3: the KV-cache + scheduler path); returns per-request
+    dicts with the explanation's token counts and the HTTP latency."""
+    import concurrent.futures as cf
+    import http.client
+
+    def one(pair):
+        body = json.dumps({"pod_a": pair[0], "pod_b": pair[1], "max_tokens": max_new_tokens,
+                           "ignore_eos": True}).encode()
+        conn = http.client.HTTPConnection(host, port, timeout=900)
+        t0 = time.perf_counter()
+        conn.request("POST", "/api/v1/analyze/pod-communication", body, {"Content-Type": "application/json"})
+        r = conn.getresponse()
+        data = json.loads(r.read())
+        conn.close()
+        llm = data.get("llm") or {}
+        if r.status != 200 or llm.get("status") != "success":
+            raise RuntimeError(f"pod-communication failed: HTTP {r.status}: {data}")
+        res = dict(llm["result"])
+        res.pop("analysis", None)
+        res["http_latency_ms"] = (time.perf_counter() - t0) * 1e3
+        return res
+
+    with cf.ThreadPoolExecutor(max_workers=len(pairs)) as ex:
+        return list(ex.map(one, pairs))
+
+
+def bench_pod_pairs(n: int, seed: int = 0) -> list:
+    """n (pod_a, pod_b) pairs of the bench FakeCluster (build_app_for_bench uses seed 0)."""
+    from .cluster.backend import PODS
+    from .cluster.fake import FakeCluster
+
+    fake = FakeCluster.build(seed=seed)
+    pods = [f"{p['metadata']['namespace']}/{p['metadata']['name']}" for p in fake.list(PODS, "default")]
+    return [(pods[i % len(pods)], pods[(i * 7 + 3) % len(pods)]) for i in range(n)]
+
+
 def torch_dtype_name(s: str) -> str:
     """``llm.dtype`` ("bf16" / "bfloat16" / "fp16" / "fp32" ...) -> torch dtype attribute name."""
     m = {"bf16": "bfloat16", "bfloat16": "bfloat16", "fp16": "float16", "float16": "float16", "half": "float16",

@@ -160,7 +160,11 @@ class MonitorApp:
         resp = {"status": "success", "analysis": analysis, "timestamp": utcnow()}
         if self._llm_enabled() and req.get("explain", True) is not False:
             try:
-                rec = self._bounded(lambda: self.analysis.explain_pod_communication(analysis))
+                mt = req.get("max_tokens")  # extension keys (ignored by the reference's decoder)
+                mt = int(mt) if isinstance(mt, (int, float)) and not isinstance(mt, bool) and mt > 0 else None
+                ie = bool(req.get("ignore_eos", False))
+                rec = self._bounded(lambda: self.analysis.explain_pod_communication(analysis, max_tokens=mt,
+                                                                                  ignore_eos=ie))
                 resp["llm"] = rec
             except FutTimeout:
                 resp["llm"] = {"status": "error", "error": "llm timeout"}

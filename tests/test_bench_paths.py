@@ -1,0 +1,38 @@
+"""The HTTP paths bench.py drives, end to end on the CPU with a tiny model: POST /api/v1/query
+and POST /api/v1/analyze/pod-communication (LLM explanation) through the in-process server, the
+engine thread and continuous batching."""
+import pytest
+
+from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine
+from k8s_llm_monitor_amd.llm.synthetic import synthetic_context
+from k8s_llm_monitor_amd.monitor.app import (bench_pod_pairs, build_app_for_bench, post_pod_communication,
+                                             post_queries)
+
+
+@pytest.fixture(scope="module")
+def served():
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_model_len=8192, num_blocks=2048,
+                                 use_graphs=False, seed=1), device="cpu")
+    svc = EngineService(eng)
+    srv, port = build_app_for_bench(svc)
+    yield svc, port
+    svc.close()
+    srv.shutdown()
+
+
+def test_query_path(served):
+    svc, port = served
+    # llama-tiny's 1024-position window: keep the synthetic cluster context short
+    items = [(q, ctx[:500]) for ctx, q in (synthetic_context(s) for s in range(3))]
+    res = post_queries(port, items, 6)
+    assert len(res) == 3
+    assert all(r["completion_tokens"] == 6 and r["prompt_tokens"] > 100 for r in res)
+
+
+def test_pod_communication_path(served):
+    svc, port = served
+    pairs = bench_pod_pairs(3)
+    assert all("/" in a and "/" in b for a, b in pairs)
+    res = post_pod_communication(port, pairs, 5)
+    assert len(res) == 3
+    assert all(r["completion_tokens"] == 5 and r["type"] == "pod_communication" for r in res)
