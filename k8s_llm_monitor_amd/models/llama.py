@@ -208,18 +208,21 @@ class CausalLM:
             y += L["bo"]
         return tp_all_reduce(y, self.ps)
 
-    def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None) -> torch.Tensor:
+    def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None,
+                   rows: Optional[int] = None) -> torch.Tensor:
         """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
-        ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM, reduced inside
-        rope_and_cache."""
+        ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM over ``x`` (row-major
+        or fragment-packed with ``rows`` valid rows), reduced inside rope_and_cache; the attention
+        output is then written fragment-packed for the o_proj skinny GEMM."""
         c = self.cfg
         k_cache, v_cache = kv if kv is not None else (None, None)
         partial, ns = None, 0
+        T = rows if rows is not None else x.shape[0]
         if slabs is not None:
             ws, splits = slabs
-            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits)
+            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T)
             partial = ws
-            qkv = torch.empty(x.shape[0], L["wqkv_p"].shape[0] * 16, dtype=x.dtype, device=x.device)
+            qkv = torch.empty(T, L["wqkv_p"].shape[0] * 16, dtype=self.dtype, device=self.device)
         else:
             qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
         ops.rope_and_cache(qkv, meta.positions, self.cos_sin if self.cos_sin is not None else _dummy_cs(self),
@@ -230,8 +233,9 @@ class CausalLM:
             qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
             o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb)
         else:
+            out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device) if slabs is not None else None
             o = ops.paged_decode(qkv, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.hq, self.hkv,
-                                 self.D, self.scale, workspace=meta.decode_ws)
+                                 self.D, self.scale, workspace=meta.decode_ws, out=out)
         return o
 
     def _mlp(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
@@ -300,10 +304,10 @@ class CausalLM:
             x = self._norm(x, self.final_norm)
         else:
             residual = h
+            if self._use_skinny(meta, h):
+                return self._decode_layers_skinny(None, residual, meta, kv_caches)
             x = ops.rms_norm(h, self.layers[0]["attn_norm"], c.norm_eps)
             n = len(self.layers)
-            if self._use_skinny(meta, h):
-                return self._decode_layers_skinny(x, residual, meta, kv_caches)
             for i, L in enumerate(self.layers):
                 kv = kv_caches[i] if kv_caches is not None else None
                 y = self._attention(L, x, meta, kv)
@@ -366,24 +370,33 @@ class CausalLM:
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list]) -> torch.Tensor:
+        """Activations between the skinny GEMMs travel fragment-packed (whole-line A loads):
+        x_norm (reduce_add_rms_norm), the attention output (paged_decode) and the MLP activation
+        (SwiGLU epilogue) are all written in the A-operand layout."""
         c, ws, n = self.cfg, self._skinny_ws, len(self.layers)
+        M = residual.shape[0]
+        xp = ops.reduce_add_rms_norm(ops.packed_empty(M, c.d_model, self.dtype, self.device), residual, None, 0,
+                                     self.layers[0]["attn_norm"], c.norm_eps)
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
-            o = self._attn_core(L, x, meta, kv, slabs=(ws, self._split_qkv))
-            x = self._row_parallel_tail(o, L["wo_p"], residual, L["mlp_norm"], self._split_o)
-            act = ops.skinny_swiglu(x, L["w13_p"])
-            nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
-            x = self._row_parallel_tail(act, L["w2_p"], residual, nw, self._split_d)
-        return self._logits(x)
+            op = self._attn_core(L, xp, meta, kv, slabs=(ws, self._split_qkv), rows=M)
+            xp = self._row_parallel_tail(op, L["wo_p"], residual, L["mlp_norm"], self._split_o, M, packed_out=True)
+            act = ops.skinny_swiglu(xp, L["w13_p"], rows=M, packed_out=True)
+            last = i + 1 == n
+            nw = self.final_norm if last else self.layers[i + 1]["attn_norm"]
+            xp = self._row_parallel_tail(act, L["w2_p"], residual, nw, self._split_d, M, packed_out=not last)
+        return self._logits(xp)
 
     def _row_parallel_tail(self, a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w,
-                           splits: int) -> torch.Tensor:
+                           splits: int, rows: int, packed_out: bool) -> torch.Tensor:
         eps, ws = self.cfg.norm_eps, self._skinny_ws
         if self.tp == 1:
-            return ops.proj_add_rms_norm(a, wp, residual, norm_w, eps, workspace=ws, splits=splits)
-        ns = ops.skinny_slabs(a, wp, ws, splits)
-        y = ops.reduce_slabs(ws, ns, a.shape[0], wp.shape[0] * 16, dtype=residual.dtype)
-        return ops.fused_add_rms_norm(tp_all_reduce(y, self.ps), residual, norm_w, eps)
+            return ops.proj_add_rms_norm(a, wp, residual, norm_w, eps, workspace=ws, splits=splits, rows=rows,
+                                         packed_out=packed_out)
+        ns = ops.skinny_slabs(a, wp, ws, splits, rows=rows)
+        y = ops.reduce_slabs(ws, ns, rows, wp.shape[0] * 16, dtype=residual.dtype)
+        x = ops.fused_add_rms_norm(tp_all_reduce(y, self.ps), residual, norm_w, eps)
+        return ops.pack_activation(x) if packed_out else x
 
 
 _DUMMY_CS: dict = {}

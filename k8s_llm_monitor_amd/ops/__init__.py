@@ -114,10 +114,6 @@ def skinny_workspace(max_m: int, N: int, splits: int, device) -> torch.Tensor:
     return torch.empty(splits * min(max_m, SKINNY_MAX_M) * N, dtype=torch.float32, device=device)
 
 
-def _skinny_ntl() -> bool:
-    return os.environ.get("K8SLLM_SKINNY_NT", "1") != "0"
-
-
 def skinny_kchunk(K: int, S: int) -> int:
     """The K slice of each split (mirror of skinny_kchunk in gemm_skinny.hip): rounded up to whole
     128-deep wave groups where that keeps S slices, else to whole 32-deep k-steps."""
@@ -144,44 +140,80 @@ def _cpu_deinterleave(gu: torch.Tensor) -> tuple:
     return t[:, :, 0].reshape(M, F2 // 2), t[:, :, 1].reshape(M, F2 // 2)
 
 
+def _rows(a: torch.Tensor, rows: Optional[int] = None) -> int:
+    """Valid rows of an activation: row-major [M, K], or fragment-packed [ceil(M/16), K/32, 64, 8]
+    (then ``rows`` must be given)."""
+    if a.dim() == 4:
+        if rows is None:
+            raise ValueError("a fragment-packed activation needs its row count")
+        return rows
+    return a.shape[0]
+
+
+def _cpu_a(a: torch.Tensor, rows: Optional[int]) -> torch.Tensor:
+    return unpack_skinny(a)[: _rows(a, rows)] if a.dim() == 4 else a
+
+
+def pack_activation(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row-major [M, K] (M <= 64) -> fragment-packed [ceil(M/16), K/32, 64, 8] (rows padded with
+    zeros), the A-operand layout gemm_skinny reads with whole-line loads."""
+    M, K = x.shape
+    mt = -(-M // 16)
+    if M % 16:
+        x = torch.cat([x, x.new_zeros(mt * 16 - M, K)])
+    p = pack_skinny(x)
+    return out.copy_(p) if out is not None else p
+
+
 def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  nt_tiles: int = 4) -> torch.Tensor:
+                  nt_tiles: int = 4, rows: Optional[int] = None) -> torch.Tensor:
     """``a @ W^T`` for <= 64 rows over the fragment-packed weight, one K slice."""
+    M = _rows(a, rows)
     if not _gpu(a):
-        y = (a.float() @ _cpu_w(wp).t()).to(a.dtype)
+        x = _cpu_a(a, rows)
+        y = (x.float() @ _cpu_w(wp).t()).to(x.dtype)
         return out.copy_(y) if out is not None else y
     N = wp.shape[0] * 16
     if out is None:
-        out = torch.empty(a.shape[0], N, dtype=a.dtype, device=a.device)
-    native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, _skinny_ntl())
+        out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, M)
     return out
 
 
-def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F]."""
-    if not _gpu(a):
-        g, u = _cpu_deinterleave((a.float() @ _cpu_w(wp13).t()).to(a.dtype).float())
-        y = (torch.nn.functional.silu(g) * u).to(a.dtype)
-        return out.copy_(y) if out is not None else y
+def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  rows: Optional[int] = None, packed_out: bool = False) -> torch.Tensor:
+    """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F], or with
+    ``packed_out`` the fragment-packed [ceil(M/16), F/32, 64, 8] (the down projection's A)."""
+    M = _rows(a, rows)
     F = wp13.shape[0] * 8
+    if not _gpu(a):
+        x = _cpu_a(a, rows)
+        g, u = _cpu_deinterleave((x.float() @ _cpu_w(wp13).t()).to(x.dtype).float())
+        y = (torch.nn.functional.silu(g) * u).to(x.dtype)
+        if packed_out:
+            y = pack_activation(y)
+        return out.copy_(y) if out is not None else y
     if out is None:
-        out = torch.empty(a.shape[0], F, dtype=a.dtype, device=a.device)
-    native().gemm_skinny(a, wp13, None, out, 1, 2, 4, _skinny_ntl())
+        shape = (-(-M // 16), F // 32, 64, 8) if packed_out else (M, F)
+        out = torch.empty(shape, dtype=a.dtype, device=a.device)
+    native().gemm_skinny(a, wp13, None, out, 1, 3 if packed_out else 2, 4, M)
     return out
 
 
 def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, splits: int,
-                 nt_tiles: int = 4) -> int:
+                 nt_tiles: int = 4, rows: Optional[int] = None) -> int:
     """Split-K ``a @ W^T`` into fp32 slabs [S', M, N] in ``workspace``; returns S'."""
+    M = _rows(a, rows)
     if not _gpu(a):
-        M, N, K = a.shape[0], wp.shape[0] * 16, wp.shape[1] * 32
+        x = _cpu_a(a, rows)
+        N, K = wp.shape[0] * 16, wp.shape[1] * 32
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
         w = _cpu_w(wp)
         slabs = workspace[: ns * M * N].view(ns, M, N)
         for s in range(ns):
-            slabs[s] = a[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].t()
+            slabs[s] = x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].t()
         return ns
-    return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, _skinny_ntl())
+    return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, M)
 
 
 def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=torch.bfloat16,
@@ -197,32 +229,44 @@ def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=tor
     return out
 
 
-def reduce_add_rms_norm(out: torch.Tensor, residual: torch.Tensor, workspace: torch.Tensor, nslabs: int,
+def reduce_add_rms_norm(out: torch.Tensor, residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int,
                         norm_w: torch.Tensor, eps: float) -> torch.Tensor:
-    """``residual <- residual + sum of slabs`` (rounded to the residual dtype), ``out <- rms_norm``."""
+    """``residual <- residual + sum of slabs`` (rounded to the residual dtype), ``out <- rms_norm``.
+    ``nslabs = 0``: a plain RMSNorm of ``residual``.  A 4-D ``out`` is written fragment-packed
+    ([ceil(M/16), d/32, 64, 8], the next skinny GEMM's A operand)."""
     if not _gpu(residual):
         M, N = residual.shape
-        s = workspace[: nslabs * M * N].view(nslabs, M, N).sum(0)
-        residual.copy_((residual.float() + s).to(residual.dtype))
-        return out.copy_(ref.rms_norm(residual, norm_w, eps))
+        if nslabs:
+            s = workspace[: nslabs * M * N].view(nslabs, M, N).sum(0)
+            residual.copy_((residual.float() + s).to(residual.dtype))
+        y = ref.rms_norm(residual, norm_w, eps)
+        return out.copy_(pack_activation(y) if out.dim() == 4 else y)
     native().reduce_add_rms_norm(out, residual, workspace, nslabs, norm_w, eps)
     return out
 
 
+def packed_empty(M: int, K: int, dtype, device) -> torch.Tensor:
+    """Uninitialised fragment-packed activation buffer [ceil(M/16), K/32, 64, 8]."""
+    return torch.empty(-(-M // 16), K // 32, 64, 8, dtype=dtype, device=device)
+
+
 def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
                       workspace: Optional[torch.Tensor] = None, splits: Optional[int] = None,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, rows: Optional[int] = None,
+                      packed_out: bool = False) -> torch.Tensor:
     """The decode tail of an attention or MLP block in one GEMM + one reduce:
-    ``residual <- residual + a @ W^T``; returns ``rms_norm(residual) * norm_w``.  GPU: gemm_skinny
-    (packed ``wp``, split-K fp32 slabs) then reduce_add_rms_norm."""
-    M, N, K = a.shape[0], wp.shape[0] * 16, wp.shape[1] * 32
+    ``residual <- residual + a @ W^T``; returns ``rms_norm(residual) * norm_w`` (row-major, or
+    fragment-packed with ``packed_out``).  GPU: gemm_skinny (packed ``wp``, split-K fp32 slabs)
+    then reduce_add_rms_norm."""
+    M, N, K = _rows(a, rows), wp.shape[0] * 16, wp.shape[1] * 32
     if splits is None:
         splits = skinny_splits(N, K)
     if workspace is None:
         workspace = skinny_workspace(M, N, splits, a.device)
-    s = skinny_slabs(a, wp, workspace, splits)
+    s = skinny_slabs(a, wp, workspace, splits, rows=M)
     if out is None:
-        out = torch.empty(M, N, dtype=residual.dtype, device=a.device)
+        out = (packed_empty(M, N, residual.dtype, a.device) if packed_out
+               else torch.empty(M, N, dtype=residual.dtype, device=a.device))
     return reduce_add_rms_norm(out, residual, workspace, s, norm_w, eps)
 
 
@@ -335,6 +379,8 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
                  splits: Optional[int] = None) -> torch.Tensor:
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale)
+        if out is not None and out.dim() == 4:  # fragment-packed output (gemm_skinny A operand)
+            r = pack_activation(r)
         return out.copy_(r) if out is not None else r
     B = seq_lens.shape[0]
     if workspace is None:

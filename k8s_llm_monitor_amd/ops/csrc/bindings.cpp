@@ -34,11 +34,11 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
-                       int S, int epi, int nt_tiles, int ntl, hipStream_t s);
+                       int S, int epi, int nt_tiles, int a_packed, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
 int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
-                              float eps, hipStream_t s);
+                              float eps, long out_stride, hipStream_t s);
 }
 
 namespace {
@@ -147,14 +147,22 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
   dev_bf16(out, "out"); dev_bf16(q, "q"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
   dev_i32(block_tables, "block_tables"); dev_i32(seq_lens, "seq_lens");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "q must be [B, >=Hq*D] rows");
-  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [B, Hq*D]");
+  const bool packed = out.dim() == 4;  // fragment-packed [ceil(B/16), Hq*D/32, 64, 8] for gemm_skinny
+  if (packed) {
+    TORCH_CHECK(out.is_contiguous() && out.size(1) * 32 == Hq * D && out.size(2) == 64 && out.size(3) == 8 &&
+                    out.size(0) * 16 >= seq_lens.size(0),
+                "packed out must be [ceil(B/16), Hq*D/32, 64, 8]");
+  } else {
+    TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [B, Hq*D]");
+  }
   TORCH_CHECK(k_cache.size(3) == 16 && v_cache.size(3) == 16, "paged_decode expects block_size 16");
   TORCH_CHECK(part_out.scalar_type() == torch::kFloat32 && part_ml.scalar_type() == torch::kFloat32, "partials fp32");
   const int B = (int)seq_lens.size(0);
   TORCH_CHECK(splits >= 1 && splits <= 64, "splits must be in [1, 64]");
   TORCH_CHECK(part_out.numel() >= (int64_t)B * Hq * splits * D && part_ml.numel() >= (int64_t)B * Hq * splits * 2,
               "decode workspace too small for batch x splits");
-  check(k8sllm_paged_decode(out.data_ptr(), out.stride(0), part_out.data_ptr<float>(), part_ml.data_ptr<float>(),
+  check(k8sllm_paged_decode(out.data_ptr(), packed ? -(long)(Hq * D / 32) : (long)out.stride(0),
+                            part_out.data_ptr<float>(), part_ml.data_ptr<float>(),
                             q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), (int)block_tables.stride(0), seq_lens.data_ptr<int>(), B,
                             (int)Hq, (int)Hkv, (int)D, (int)splits, (float)scale, cur()),
@@ -237,16 +245,27 @@ void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t 
 
 // Skinny decode GEMM over a fragment-packed weight wp [N/16][K/32][64][8] (gemm_skinny.hip).
 // epi 0: fp32 split-K slabs partial[S'][M][N], returns S'; epi 1: y = bf16(a . W^T);
-// epi 2: y[M, N/2] = silu(gate) * up over a [32 gate | 32 up]-interleaved weight.  Returns the
+// epi 2: y[M, N/2] = silu(gate) * up over a [32 gate | 32 up]-interleaved weight; epi 3: the same
+// written fragment-packed.  Returns the
 // number of slabs written (1 for epi 1/2).
 int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
-                    c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, bool ntl) {
+                    c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
               "gemm_skinny: wp must be fragment-packed [N/16, K/32, 64, 8]");
-  TORCH_CHECK(a.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 8 == 0, "gemm_skinny: a layout");
-  const int M = (int)a.size(0), N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32;
-  TORCH_CHECK(a.size(1) == K, "gemm_skinny: a has ", a.size(1), " columns, weight K=", K);
+  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32;
+  const bool a_packed = a.dim() == 4;
+  int M;
+  if (a_packed) {  // fragment-packed activations [ceil(M/16), K/32, 64, 8]; `rows` = valid rows
+    TORCH_CHECK(a.is_contiguous() && a.size(1) * 32 == K && a.size(2) == 64 && a.size(3) == 8,
+                "gemm_skinny: packed a must be [ceil(M/16), K/32, 64, 8]");
+    M = (int)rows;
+    TORCH_CHECK(M > 0 && (M + 15) / 16 <= a.size(0), "gemm_skinny: rows exceed the packed a");
+  } else {
+    TORCH_CHECK(a.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 8 == 0, "gemm_skinny: a layout");
+    TORCH_CHECK(a.size(1) == K, "gemm_skinny: a has ", a.size(1), " columns, weight K=", K);
+    M = (int)a.size(0);
+  }
   TORCH_CHECK(M <= 64, "gemm_skinny: at most 64 rows");
   TORCH_CHECK(N % (16 * nt_tiles) == 0, "gemm_skinny: N not divisible by the workgroup tile");
   const int S = epi == 0 ? k8sllm_gemm_skinny_slabs(K, (int)splits) : 1;
@@ -262,13 +281,21 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   } else {
     TORCH_CHECK(y.has_value(), "gemm_skinny: output tensor required");
     dev_bf16(*y, "y");
-    const int ncol = epi == 2 ? N / 2 : N;
-    TORCH_CHECK(y->dim() == 2 && y->size(0) >= M && y->size(1) == ncol && y->stride(1) == 1, "gemm_skinny: y shape");
+    if (epi == 3) {  // SwiGLU written fragment-packed [ceil(M/16), F/32, 64, 8]
+      TORCH_CHECK(y->dim() == 4 && y->is_contiguous() && y->size(0) * 16 >= M && y->size(1) * 64 == N &&
+                      y->size(2) == 64 && y->size(3) == 8,
+                  "gemm_skinny: packed SwiGLU output must be [ceil(M/16), F/32, 64, 8]");
+      TORCH_CHECK(y->size(0) == (M + 15) / 16, "gemm_skinny: packed output m-tiles");
+    } else {
+      const int ncol = epi == 2 ? N / 2 : N;
+      TORCH_CHECK(y->dim() == 2 && y->size(0) >= M && y->size(1) == ncol && y->stride(1) == 1,
+                  "gemm_skinny: y shape");
+      ldy = y->stride(0);
+    }
     yp = y->data_ptr();
-    ldy = y->stride(0);
   }
-  check(k8sllm_gemm_skinny(a.data_ptr(), a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
-                           epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, ntl ? 1 : 0, cur()),
+  check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
+                           epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, cur()),
         "gemm_skinny");
   return S;
 }
@@ -281,16 +308,29 @@ void reduce_slabs(torch::Tensor out, torch::Tensor partial, int64_t S) {
   check(k8sllm_reduce_slabs(out.data_ptr(), partial.data_ptr<float>(), (int)S, out.numel(), cur()), "reduce_slabs");
 }
 
-void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, torch::Tensor partial, int64_t S,
+void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, c10::optional<torch::Tensor> partial, int64_t S,
                          torch::Tensor w, double eps) {
   dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
   TORCH_CHECK(residual.is_contiguous() && out.is_contiguous() && w.is_contiguous(), "reduce_add_rms_norm layout");
-  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == torch::kFloat32 && partial.is_contiguous(), "partial");
   const int d = (int)residual.size(-1);
   const int M = (int)(residual.numel() / d);
-  TORCH_CHECK(partial.numel() >= S * M * d && out.numel() == (int64_t)M * d, "reduce_add_rms_norm shapes");
-  check(k8sllm_reduce_add_rmsnorm(out.data_ptr(), residual.data_ptr(), partial.data_ptr<float>(), (int)S, M,
-                                  w.data_ptr(), d, (float)eps, cur()),
+  const float* pp = nullptr;
+  if (S > 0) {
+    TORCH_CHECK(partial.has_value() && partial->is_cuda() && partial->scalar_type() == torch::kFloat32 &&
+                    partial->is_contiguous(), "partial");
+    TORCH_CHECK(partial->numel() >= S * M * d, "reduce_add_rms_norm: partial too small");
+    pp = partial->data_ptr<float>();
+  }
+  long ostride = d;
+  if (out.dim() == 4) {  // fragment-packed [ceil(M/16), d/32, 64, 8] for the next gemm_skinny
+    TORCH_CHECK(out.size(0) == (M + 15) / 16 && out.size(1) * 32 == d && out.size(2) == 64 && out.size(3) == 8,
+                "packed out must be [ceil(M/16), d/32, 64, 8]");
+    ostride = -(long)(d / 32);
+  } else {
+    TORCH_CHECK(out.numel() == (int64_t)M * d, "reduce_add_rms_norm shapes");
+  }
+  check(k8sllm_reduce_add_rmsnorm(out.data_ptr(), residual.data_ptr(), pp, (int)S, M, w.data_ptr(), d, (float)eps,
+                                  ostride, cur()),
         "reduce_add_rms_norm");
 }
 

@@ -52,6 +52,14 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// Element (row, col) of an activation matrix: row-major [rows][stride] when stride > 0, or the
+// fragment-packed [ceil(rows/16)][K/32][64][8] layout of gemm_skinny's A operand when
+// stride == -(K/32) (lane = 16 * ((col / 8) % 4) + row % 16; 8 consecutive cols are contiguous).
+__device__ __forceinline__ long act_index(int row, int col, long stride) {
+  if (stride > 0) return (long)row * stride + col;
+  return (((long)(row >> 4) * (-stride) + (col >> 5)) * 64 + ((col >> 3) & 3) * 16 + (row & 15)) * 8 + (col & 7);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

@@ -9,7 +9,8 @@
 // a row-major [N][K] weight in MFMA-fragment order (16 rows x 64 B per instruction) streams at
 // 1.1-3.9 TB/s; whole-line orders reach 4.7-5.7 TB/s - the packed layout gets the latter with no
 // LDS round trip.  Weights are read once per step (14 GB for Llama-3-8B), so loads are
-// non-temporal (MI355X_MICROARCH.md "nt-weights").
+// non-temporal (MI355X_MICROARCH.md "nt-weights"; measured 2-10 % faster than default-policy
+// loads here, tools/bench_skinny.py).
 //
 // Decomposition: workgroup = 4 waves, NT n-tiles (16 NT output columns) x one K slice; grid =
 // (N / (16 NT), slices).  The waves take interleaved groups of U consecutive k-steps of the slice
@@ -21,21 +22,33 @@
 //   SWIGLU - one slice, NT = 4, weight rows interleaved per 64-column tile as [32 gate | 32 up]:
 //            Y[m, f] = silu(gate) * up - the gate_up projection writes the MLP activation directly
 //            (no silu_mul pass, and the down projection reads F, not 2F, columns)
+//   SWIGLU_PACKED - the same, written fragment-packed ([ceil(M/16)][F/32][64][8]) as the down
+//            projection's A operand
+// A (activations) is row-major or fragment-packed like W; the packed form turns the A loads into
+// whole-line reads too (at M = 64 the A bytes per workgroup equal the W bytes).
 #include "common.h"
 
 namespace k8sllm {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2 };
-constexpr int kU = 4;  // consecutive k-steps per wave group (4 KiB per n-tile in flight per wave)
+enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2, EPI_SWIGLU_PACKED = 3 };
 
-template <int MT, int NT, int EPI, bool NTL>
+// Loads of one wave group: U consecutive k-steps, NT weight and MT activation fragments each.
+template <int U, int MT, int NT>
+struct SkinnyBatch {
+  u32x4 b[U][NT];
+  bf16x8 a[U][MT];
+};
+
+template <int MT, int NT, int EPI, bool APK>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
                                                           int kchunk) {
-  __shared__ __attribute__((aligned(16))) float red[4][MT][NT][64][4];
+  // U k-steps per wave group; two groups in flight per wave (register double buffer)
+  constexpr int U = MT <= 2 ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) float red[4][NT][64][4];  // one m-tile at a time: 16 KiB at NT 4
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ntile0 = blockIdx.x * NT;
   const int s = blockIdx.y;
@@ -47,9 +60,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
     wp[nt] = reinterpret_cast<const u32x4*>(Wp) + ((long)(ntile0 + nt) * ksteps + (kbeg >> 5)) * 64 + lane;
+  // A: row-major [M][lda] (fragment-shaped loads, padding rows clamped) or, APK, fragment-packed
+  // like W ([ceil(M/16)][K/32][64][8], padding rows present) so A loads are 1 KiB contiguous too
   const bf16_t* ap[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) ap[mt] = A + (long)min(mt * 16 + (lane & 15), M - 1) * lda + kbeg + 8 * (lane >> 4);
+  for (int mt = 0; mt < MT; ++mt) {
+    if constexpr (APK)
+      ap[mt] = A + (((long)mt * ksteps + (kbeg >> 5)) * 64 + lane) * 8;
+    else
+      ap[mt] = A + (long)min(mt * 16 + (lane & 15), M - 1) * lda + kbeg + 8 * (lane >> 4);
+  }
+  constexpr int ASTEP = APK ? 512 : 32;  // bf16 elements between consecutive k-steps
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -57,55 +78,70 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int i0 = wave * kU; i0 < nsteps; i0 += 4 * kU) {
-    u32x4 bf[kU][NT];
-    bf16x8 af[kU][MT];
+  auto load = [&](SkinnyBatch<U, MT, NT>& bt, int i0) {
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int st = min(i0 + u, nsteps - 1);  // tail steps re-read a valid step; their MFMAs are skipped
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        if constexpr (NTL)
-          bf[u][nt] = __builtin_nontemporal_load(wp[nt] + st * 64);
-        else
-          bf[u][nt] = wp[nt][st * 64];
-      }
+      for (int nt = 0; nt < NT; ++nt) bt.b[u][nt] = __builtin_nontemporal_load(wp[nt] + st * 64);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) af[u][mt] = *reinterpret_cast<const bf16x8*>(ap[mt] + st * 32);
+      for (int mt = 0; mt < MT; ++mt) bt.a[u][mt] = *reinterpret_cast<const bf16x8*>(ap[mt] + st * ASTEP);
     }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto compute = [&](const SkinnyBatch<U, MT, NT>& bt, int i0) {
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (i0 + u < nsteps) {  // wave-uniform
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u][mt], __builtin_bit_cast(bf16x8, bf[u][nt]),
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bt.a[u][mt], __builtin_bit_cast(bf16x8, bt.b[u][nt]),
                                                                    acc[mt][nt], 0, 0, 0);
       }
     }
+  };
+
+  // software pipeline: the next group's loads are issued before this group's MFMAs, so every
+  // wave keeps two groups of weight lines in flight instead of stalling once per group
+  constexpr int STRIDE = 4 * U;
+  int i0 = wave * U;
+  if (i0 < nsteps) {
+    SkinnyBatch<U, MT, NT> b0, b1;
+    load(b0, i0);
+    while (true) {
+      const int i1 = i0 + STRIDE;
+      if (i1 < nsteps) load(b1, i1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(b0, i0);
+      if (i1 >= nsteps) break;
+      const int i2 = i1 + STRIDE;
+      if (i2 < nsteps) load(b0, i2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(b1, i1);
+      if (i2 >= nsteps) break;
+      i0 = i2;
+    }
   }
 
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(&red[wave][mt][nt][lane][0]) = acc[mt][nt];
-  __syncthreads();
-
+  // cross-wave combine, one m-tile per round (keeps LDS at 16 KiB so occupancy is VGPR-bound).
   // C/D layout of the 16x16 tile: col = lane & 15, rows (lane >> 4) * 4 + r
-  constexpr int NOUT = EPI == EPI_SWIGLU ? NT / 2 : NT;
-  for (int idx = threadIdx.x; idx < NOUT * 64; idx += 256) {
-    const int nt = idx >> 6, l = idx & 63;
+  constexpr int NOUT = EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED ? NT / 2 : NT;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][mt][nt][l][0]);
+  for (int mt = 0; mt < MT; ++mt) {
+    if (mt > 0) __syncthreads();  // previous round's reads done
 #pragma unroll
-      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][mt][nt][l][0]);
-      if constexpr (EPI == EPI_SWIGLU) {
-        f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][mt][nt + NT / 2][l][0]);
+    for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(&red[wave][nt][lane][0]) = acc[mt][nt];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < NOUT * 64; idx += 256) {
+      const int nt = idx >> 6, l = idx & 63;
+      f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][nt][l][0]);
 #pragma unroll
-        for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][mt][nt + NT / 2][l][0]);
+      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
+      if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
+        f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][nt + NT / 2][l][0]);
+#pragma unroll
+        for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
         const int f = blockIdx.x * (NT * 8) + nt * 16 + (l & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -113,7 +149,14 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
           // the gate and up values are rounded to bf16 first, as the unfused GEMM -> silu_mul does
           const float g = bf2f(f2bf(v[r]));
           const float uu = bf2f(f2bf(u[r]));
-          if (row < M) Y[(long)row * ldy + f] = f2bf(g * uu / (1.f + __expf(-g)));
+          const bf16_t o = f2bf(g * uu / (1.f + __expf(-g)));
+          if constexpr (EPI == EPI_SWIGLU_PACKED) {
+            // fragment-packed activation for the down projection's A operand: [MT][F/32][64][8]
+            const int F = N >> 1;
+            Y[(((long)mt * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 + (row & 15)) * 8 + (f & 7)] = o;
+          } else if (row < M) {
+            Y[(long)row * ldy + f] = o;
+          }
         }
       } else {
         const int col = (ntile0 + nt) * 16 + (l & 15);
@@ -133,12 +176,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 }
 
 // residual[m] <- bf16(residual[m] + sum_s partial[s][m]); out[m] <- rmsnorm(residual[m]) * w
-// One workgroup per row, 256 threads x 8 columns per chunk (d <= 2048 * NC).
+// One workgroup per row, 256 threads x 8 columns per chunk (d <= 2048 * NC).  S = 0 is a plain
+// RMSNorm of the residual.  out_stride < 0: out is written fragment-packed (act_index) as the next
+// skinny GEMM's A operand.
 template <int NC>
 __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restrict__ out,
                                                                  bf16_t* __restrict__ residual,
                                                                  const float* __restrict__ partial, int S, int M,
-                                                                 const bf16_t* __restrict__ w, int d, float eps) {
+                                                                 const bf16_t* __restrict__ w, int d, float eps,
+                                                                 long out_stride) {
   __shared__ float sred[4];
   const int row = blockIdx.x, tid = threadIdx.x;
   bf16_t* rr = residual + (long)row * d;
@@ -165,7 +211,6 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
     }
   }
   const float inv = rsqrtf(block_sum<256>(ss, sred) / (float)d + eps);
-  bf16_t* orow = out + (long)row * d;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int idx = (c * 256 + tid) * 8;
@@ -174,7 +219,7 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
       unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
-      *reinterpret_cast<uint4*>(orow + idx) = pack8(o);
+      *reinterpret_cast<uint4*>(out + act_index(row, idx, out_stride)) = pack8(o);
     }
   }
 }
@@ -221,19 +266,20 @@ extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
   return (K + kc - 1) / kc;
 }
 
-// epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; ntl: non-temporal W loads
+// epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; a_packed: A in the
+// fragment-packed layout (lda ignored)
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
-                                  int N, int K, int S, int epi, int nt_tiles, int ntl, hipStream_t s) {
+                                  int N, int K, int S, int epi, int nt_tiles, int a_packed, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > 64 || K % 32 != 0 || S < 1 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   const int kc = skinny_kchunk(K, S);
   const int slabs = (K + kc - 1) / kc;
   if (epi != EPI_SLAB && slabs != 1) return -3;
-  if (epi == EPI_SWIGLU && nt_tiles != 4) return -4;
+  if ((epi == EPI_SWIGLU || epi == EPI_SWIGLU_PACKED) && nt_tiles != 4) return -4;
   dim3 grid(N / (16 * nt_tiles), slabs), blk(256);
   const int MT = (M + 15) / 16;
-#define K8S_SK(MTV, NTV, EPV, NTLV)                                                                            \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, NTLV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
+#define K8S_SK(MTV, NTV, EPV, APKV)                                                                            \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
                      (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc)
 #define K8S_SK_M(NTV, EPV, NTLV)             \
   switch (MT) {                              \
@@ -243,13 +289,15 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
     default: K8S_SK(4, NTV, EPV, NTLV); break; \
   }
 #define K8S_SK_NTL(NTV, EPV)  \
-  if (ntl) {                  \
+  if (a_packed) {             \
     K8S_SK_M(NTV, EPV, true)  \
   } else {                    \
     K8S_SK_M(NTV, EPV, false) \
   }
   if (epi == EPI_SWIGLU) {
     K8S_SK_NTL(4, EPI_SWIGLU)
+  } else if (epi == EPI_SWIGLU_PACKED) {
+    K8S_SK_NTL(4, EPI_SWIGLU_PACKED)
   } else if (epi == EPI_BF16) {
     if (nt_tiles == 4) { K8S_SK_NTL(4, EPI_BF16) } else { K8S_SK_NTL(2, EPI_BF16) }
   } else {
@@ -262,13 +310,13 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
 }
 
 extern "C" int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M,
-                                         const void* w, int d, float eps, hipStream_t s) {
+                                         const void* w, int d, float eps, long out_stride, hipStream_t s) {
   if (M <= 0) return 0;
   if (d % 8 != 0 || d > 256 * 8 * 4) return -1;
   const int nc = (d + 2047) / 2048;
 #define K8S_RAR(NC)                                                                                           \
   hipLaunchKernelGGL((reduce_add_rmsnorm_kernel<NC>), dim3(M), dim3(256), 0, s, (bf16_t*)out,                 \
-                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, eps)
+                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, eps, out_stride)
   if (nc <= 1) K8S_RAR(1);
   else if (nc <= 2) K8S_RAR(2);
   else K8S_RAR(4);

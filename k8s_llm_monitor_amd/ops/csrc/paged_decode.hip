@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   const int seq_len = seq_lens[b];
   if (seq_len <= 0) {  // padding row (graph bucket slack): define the output as zeros
     if (split == 0)
-      for (int i = threadIdx.x; i < G * D; i += 256) out[(long)b * out_stride + (long)kvh * G * D + i] = 0;
+      for (int i = threadIdx.x; i < G * D; i += 256) out[act_index(b, kvh * G * D + i, out_stride)] = 0;
     return;
   }
   int c0, c1, nvalid;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
     const float o = w0 * s_o[0][h][d] + w1 * s_o[1][h][d] + w2 * s_o[2][h][d] + w3 * s_o[3][h][d];
     const float L = w0 * s_sum[0][h] + w1 * s_sum[1][h] + w2 * s_sum[2][h] + w3 * s_sum[3][h];
     if (nvalid == 1) {
-      out[(long)b * out_stride + (long)(kvh * G + h) * D + d] = f2bf(o / L);
+      out[act_index(b, (kvh * G + h) * D + d, out_stride)] = f2bf(o / L);
     } else {
       const long ph = ((long)b * Hq + kvh * G + h) * S + split;
       part_out[ph * D + d] = o;
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void paged_decode_reduce_kernel(bf16_t* __rest
       a3 += s_w[h][p + 3] * po[(long)(p + 3) * D];
     }
     for (; p < nvalid; ++p) a0 += s_w[h][p] * po[(long)p * D];
-    out[(long)b * out_stride + (long)(kvh * G + h) * D + d] = f2bf((a0 + a1) + (a2 + a3));
+    out[act_index(b, (kvh * G + h) * D + d, out_stride)] = f2bf((a0 + a1) + (a2 + a3));
   }
 }
 
@@ -249,6 +249,7 @@ __global__ __launch_bounds__(256) void paged_decode_reduce_kernel(bf16_t* __rest
 using namespace k8sllm;
 
 // S = number of splits per (sequence, kv head); part buffers hold [B][Hq][S][D].
+// out_stride < 0: write the output fragment-packed for gemm_skinny (common.h act_index).
 extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q,
                                    long q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                                    int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int S,

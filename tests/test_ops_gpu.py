@@ -297,3 +297,32 @@ def test_llama_decode_skinny_matches_generic(monkeypatch):
     b = m.forward(ids, meta, kv).float()
     assert (a - b).abs().max().item() < 0.1 * b.abs().max().item() + 0.05
     assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.8
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+def test_gemm_skinny_packed_activation(M):
+    K, N = 1024, 256
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    wp, ap = ops.pack_skinny(w), ops.pack_activation(a)
+    y_ref = torch.nn.functional.linear(a.cpu().float(), w.cpu().float())
+    _close(ops.skinny_linear(ap, wp, rows=M).cpu(), y_ref, atol=3e-2, rtol=2e-2, what="packed A, bf16 epi")
+    ws = ops.skinny_workspace(M, N, 3, DEV)
+    ns = ops.skinny_slabs(ap, wp, ws, 3, rows=M)
+    _close(ops.reduce_slabs(ws, ns, M, N).cpu(), y_ref, atol=3e-2, rtol=2e-2, what="packed A, slabs")
+
+
+@pytest.mark.parametrize("M", [3, 40])
+def test_skinny_swiglu_packed_out_feeds_down(M):
+    K, F, d = 512, 448, 256
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(d, F, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    actp = ops.skinny_swiglu(ops.pack_activation(x), ops.pack_skinny(ops.interleave_gate_up(w13)), rows=M,
+                             packed_out=True)
+    gu = torch.nn.functional.linear(x.cpu().float(), w13.cpu().float()).to(torch.bfloat16)
+    act_ref = ref.silu_mul(gu)
+    _close(ops.unpack_skinny(actp)[:M].cpu(), act_ref, atol=3e-2, rtol=2e-2, what="packed act")
+    y = ops.skinny_linear(actp, ops.pack_skinny(w2), rows=M)
+    _close(y.cpu(), torch.nn.functional.linear(act_ref.float(), w2.cpu().float()), atol=5e-2, rtol=3e-2,
+           what="down from packed act")

@@ -53,7 +53,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=320)
     ap.add_argument("--ms", default="1,16,32,64")
-    ap.add_argument("--splits", default="2,4,6,8,12")
+    ap.add_argument("--splits", default="4,6,8")
     ap.add_argument("--ops", default="qkv,o,gate_up,down")
     a = ap.parse_args()
     dev = "cuda"
@@ -68,6 +68,7 @@ def main() -> None:
         gb = N * K * 2 / 1e9
         for M in map(int, a.ms.split(",")):
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            xp = ops.pack_activation(x)
             r = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             ob = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
@@ -87,26 +88,25 @@ def main() -> None:
             rep("hipblaslt" + ("+silu_mul" if name == "gate_up" else "+norm" if name in ("o", "down") else ""),
                 timeit(base, a.iters))
             if name == "gate_up":
-                for ntl in (True, False):
-                    os.environ["K8SLLM_SKINNY_NT"] = "1" if ntl else "0"
-                    rep(f"skinny swiglu nt={int(ntl)}", timeit(lambda i: ops.skinny_swiglu(x, wps[i % ncopy], out=act),
-                                                           a.iters))
+                rep("skinny swiglu", timeit(lambda i: ops.skinny_swiglu(x, wps[i % ncopy], out=act), a.iters))
+                rep("skinny swiglu packedA", timeit(lambda i: ops.skinny_swiglu(xp, wps[i % ncopy], out=act, rows=M),
+                                                    a.iters))
                 continue
             if name == "qkv":
                 for nt_tiles in (2, 4):
-                    rep(f"skinny bf16 1slice nt{nt_tiles}",
-                        timeit(lambda i: ops.skinny_linear(x, wps[i % ncopy], out=y, nt_tiles=nt_tiles), a.iters))
+                    rep(f"skinny bf16 1slice nt{nt_tiles} packedA",
+                        timeit(lambda i: ops.skinny_linear(xp, wps[i % ncopy], out=y, nt_tiles=nt_tiles, rows=M),
+                               a.iters))
             for s in map(int, a.splits.split(",")):
                 wsp = ops.skinny_workspace(M, N, s, dev)
-                for ntl in (True, False):
-                    os.environ["K8SLLM_SKINNY_NT"] = "1" if ntl else "0"
+                for tag, xa in (("", x), (" packedA", xp)):
                     if name == "qkv":
-                        fn = lambda i, s=s, wsp=wsp: ops.skinny_slabs(x, wps[i % ncopy], wsp, s)  # noqa: E731
+                        fn = lambda i, s=s, wsp=wsp, xa=xa: ops.skinny_slabs(xa, wps[i % ncopy], wsp, s,  # noqa: E731
+                                                                             rows=M)
                     else:
-                        fn = lambda i, s=s, wsp=wsp: ops.proj_add_rms_norm(  # noqa: E731
-                            x, wps[i % ncopy], r, nw, eps, workspace=wsp, splits=s, out=ob)
-                    rep(f"skinny s{s} nt={int(ntl)}", timeit(fn, a.iters))
-            os.environ["K8SLLM_SKINNY_NT"] = "1"
+                        fn = lambda i, s=s, wsp=wsp, xa=xa: ops.proj_add_rms_norm(  # noqa: E731
+                            xa, wps[i % ncopy], r, nw, eps, workspace=wsp, splits=s, out=ob, rows=M)
+                    rep(f"skinny s{s}{tag}", timeit(fn, a.iters))
         del ws, wps
         torch.cuda.empty_cache()
 
