@@ -46,6 +46,7 @@ class EngineConfig:
     use_graphs: bool = True
     seed: int = 0
     tp_size: int = 1
+    pipeline: bool = True  # overlap the host's per-step work with the GPU's decode step
     dtype: str = "bfloat16"  # compute / weight dtype ("float32" for CPU parity tests)
     model_overrides: dict = field(default_factory=dict)
 
@@ -88,6 +89,8 @@ class LLMEngine:
         self.counters = {"requests": 0, "finished": 0, "prompt_tokens": 0, "generated_tokens": 0,
                          "prefill_steps": 0, "decode_steps": 0, "preemptions": 0}
         self.is_leader = self.ps.tp_rank == 0
+        self._inflight = None  # (seqs, DecodeHandle) of the enqueued, not yet read back decode step
+        self._inflight_rows: dict = {}
 
     # ----------------------------------------------------------------- public API
     def warmup(self) -> None:
@@ -111,13 +114,101 @@ class LLMEngine:
         return seq
 
     def has_work(self) -> bool:
-        return self.sched.has_work()
+        return self.sched.has_work() or self._inflight is not None
+
+    PENDING = -1  # placeholder for a token sampled by the in-flight decode step
 
     def step(self) -> list[Sequence]:
+        """One engine step; returns the sequences that finished.
+
+        Pipelined decode (``EngineConfig.pipeline``): a decode step is enqueued on the GPU before the
+        previous one's tokens are read back, and each row whose input is such a not-yet-read token
+        takes it from the device (``ModelRunner.decode_launch`` ``src_rows``).  The host's per-step
+        work (scheduling, block bookkeeping, staging, stop checks, HTTP completions) then overlaps
+        the GPU's step instead of sitting between steps.  A sequence that stops on EOS therefore
+        runs one extra (discarded) step; length stops are predicted and never overrun.  Prefill
+        steps resolve the in-flight decode first (they change the batch)."""
+        if not self.cfg.pipeline:
+            return self._step_sync()
+        done: list[Sequence] = []
+        s = self.sched
+        if self._inflight is not None and (not s.running or (s.waiting and len(s.running) < self.cfg.max_num_seqs)):
+            done += self._resolve()
+        plan = s.schedule()
+        self.counters["preemptions"] += len(plan.preempted)
+        if plan.empty:
+            if self._inflight is not None:
+                done += self._resolve()
+            return done
+        if plan.is_prefill:
+            return done + self._run_sync(plan)
+        # length-limited sequences whose last token is already in flight stop on resolve: skip them
+        seqs = [q for q in plan.seqs if not self._length_done(q)]
+        if not seqs:
+            return done + (self._resolve() if self._inflight is not None else [])
+        prev_rows = self._inflight_rows
+        src = [prev_rows.get(q.seq_id, -1) for q in seqs]
+        if self.ps.tp_size > 1:
+            tp_broadcast_object((False, [(q.last_token, q.num_tokens, q.block_table, _params_t(q.params))
+                                         for q in seqs], src), ps=self.ps)
+        handle = self.runner.decode_launch(seqs, src)
+        self.counters["decode_steps"] += 1
+        for q in seqs:
+            q.output_ids.append(self.PENDING)
+        prev = self._inflight
+        self._inflight = (seqs, handle)
+        self._inflight_rows = {q.seq_id: i for i, q in enumerate(seqs)}
+        if prev is not None:
+            done += self._resolve_step(*prev)
+        return done
+
+    def _length_done(self, q: Sequence) -> bool:
+        return len(q.output_ids) >= q.params.max_tokens or q.num_tokens >= self.runner.max_len
+
+    def _resolve(self) -> list[Sequence]:
+        seqs, handle = self._inflight
+        self._inflight = None
+        self._inflight_rows = {}
+        return self._resolve_step(seqs, handle)
+
+    def _resolve_step(self, seqs: list, handle) -> list[Sequence]:
+        toks = self.runner.decode_collect(handle)
+        now = time.perf_counter()
+        done = []
+        for q, tok in zip(seqs, toks):
+            if q.status in (SeqStatus.FINISHED, SeqStatus.ABORTED):
+                continue  # stopped on the previous step; this step's token is discarded
+            tok = int(tok)
+            i = q.output_ids.index(self.PENDING)
+            q.output_ids[i] = tok
+            self.counters["generated_tokens"] += 1
+            if q.t_first_token is None:
+                q.t_first_token = now
+            reason = self._stop_reason(q, tok, n_out=i + 1)
+            if reason:
+                del q.output_ids[i + 1:]  # drop the token of a step launched past the stop
+                q.t_finish = now
+                self._finish(q, reason)
+                done.append(q)
+        return done
+
+    def _finish(self, q: Sequence, reason: str) -> None:
+        if q.status == SeqStatus.WAITING:  # preempted while its last token was in flight
+            try:
+                self.sched.waiting.remove(q)
+            except ValueError:
+                pass
+        self.sched.finish(q, reason)
+        self.counters["finished"] += 1
+
+    def _step_sync(self) -> list[Sequence]:
         plan = self.sched.schedule()
         self.counters["preemptions"] += len(plan.preempted)
         if plan.empty:
             return []
+        return self._run_sync(plan)
+
+    def _run_sync(self, plan) -> list[Sequence]:
         if self.ps.tp_size > 1:
             tp_broadcast_object(self._pack(plan), ps=self.ps)
         if plan.is_prefill:
@@ -136,18 +227,18 @@ class LLMEngine:
             reason = self._stop_reason(seq, int(tok))
             if reason:
                 seq.t_finish = now
-                self.sched.finish(seq, reason)
-                self.counters["finished"] += 1
+                self._finish(seq, reason)
                 done.append(seq)
         return done
 
-    def _stop_reason(self, seq: Sequence, tok: int) -> Optional[str]:
+    def _stop_reason(self, seq: Sequence, tok: int, n_out: Optional[int] = None) -> Optional[str]:
         p = seq.params
+        n = len(seq.output_ids) if n_out is None else n_out
         if not p.ignore_eos and (tok in self.eos or tok in p.stop_token_ids):
             return "stop"
-        if len(seq.output_ids) >= p.max_tokens:
+        if n >= p.max_tokens:
             return "length"
-        if seq.num_tokens >= self.runner.max_len:
+        if len(seq.prompt_ids) + n >= self.runner.max_len:
             return "length"
         return None
 
@@ -159,6 +250,9 @@ class LLMEngine:
         while any(s.status not in (SeqStatus.FINISHED, SeqStatus.ABORTED) for s in seqs):
             self.step()
         return seqs
+
+    def has_inflight(self) -> bool:
+        return self._inflight is not None
 
     def decode_text(self, seq: Sequence) -> str:
         return self.tokenizer.decode(seq.output_ids)
@@ -179,19 +273,29 @@ class LLMEngine:
 
     def worker_loop(self) -> None:
         """Non-leader TP ranks: mirror the leader's steps until it broadcasts ``None``."""
+        pending = None
         while True:
             msg = tp_broadcast_object(None, ps=self.ps)
             if msg is None:
                 return
-            is_prefill, items = msg
+            is_prefill, items = msg[0], msg[1]
             if is_prefill:
+                if pending is not None:
+                    self.runner.decode_collect(pending)
+                    pending = None
                 views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p)) for ids, bt, p in items]
                 self.runner.prefill(views)
             else:
+                src = msg[2] if len(msg) > 2 else None
                 views = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in items]
-                self.runner.decode(views)
+                h = self.runner.decode_launch(views, src)
+                if pending is not None:  # keep at most two steps enqueued (staging is double-buffered)
+                    self.runner.decode_collect(pending)
+                pending = h
 
     def stop_workers(self) -> None:
+        if self._inflight is not None:
+            self._resolve()
         if self.ps.tp_size > 1 and self.is_leader:
             tp_broadcast_object(None, ps=self.ps)
 

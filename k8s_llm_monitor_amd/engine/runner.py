@@ -70,21 +70,13 @@ class ModelRunner:
         self.d_out = torch.zeros(B, dtype=torch.int32, device=dev)
         self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev, model.hkv) \
             if self.is_gpu else None
-        # pinned host staging
-        pin = self.is_gpu
-        self.h_ids = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        self.h_pos = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        self.h_slots = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        self.h_lens = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        self.h_bt = torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
-        self.h_temp = torch.zeros(B, dtype=torch.float32, pin_memory=pin)
-        self.h_topk = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        self.h_topp = torch.ones(B, dtype=torch.float32, pin_memory=pin)
-        self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
-        # numpy views of the pinned buffers: cheap per-element host writes
-        self.n_ids, self.n_pos, self.n_slots = self.h_ids.numpy(), self.h_pos.numpy(), self.h_slots.numpy()
-        self.n_lens, self.n_bt = self.h_lens.numpy(), self.h_bt.numpy()
-        self.n_temp, self.n_topk, self.n_topp = self.h_temp.numpy(), self.h_topk.numpy(), self.h_topp.numpy()
+        self.d_src = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        # pinned host staging, double-buffered: with pipelined decode the host fills step N+1's
+        # inputs while step N's host-to-device copies may still be queued
+        self.stage = [_Staging(B, self.max_blocks_per_seq, self.is_gpu) for _ in range(2)]
+        self._stage_i = 0
+        self.h_out = [torch.zeros(B, dtype=torch.int32, pin_memory=self.is_gpu) for _ in range(2)]
+        self._out_i = 0
         self.buckets = [b for b in DEFAULT_BUCKETS if b < B] + [B]
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -137,7 +129,12 @@ class ModelRunner:
     def _decode_body(self, b: int) -> None:
         meta = AttnMeta(is_prefill=False, positions=self.d_pos[:b], slot_mapping=self.d_slots[:b],
                         block_tables=self.d_bt[:b], seq_lens=self.d_lens[:b], decode_ws=self.decode_ws)
-        logits = self.model.forward(self.d_ids[:b], meta, self.kv)
+        # pipelined decode: a row whose input is the token sampled by the previous step (still in
+        # flight when this step was enqueued) takes it from d_out on the device (d_src = its row
+        # there); other rows take the host-provided id
+        src = self.d_src[:b]
+        ids = torch.where(src >= 0, self.d_out.index_select(0, src.clamp(min=0).long()), self.d_ids[:b])
+        logits = self.model.forward(ids, meta, self.kv)
         self._sample(logits, self.d_temp[:b], self.d_topk[:b], self.d_topp[:b], out=self.d_out[:b])
 
     def capture_graphs(self, buckets: Optional[list[int]] = None) -> None:
@@ -164,16 +161,28 @@ class ModelRunner:
         torch.cuda.synchronize()
         self.rng.copy_(rng_state)
 
-    def decode(self, seqs: list[Sequence]) -> list[int]:
+    def decode(self, seqs: list, src_rows: Optional[list] = None) -> list[int]:
+        """One decode step, synchronous: the sampled token per sequence."""
+        return self.decode_collect(self.decode_launch(seqs, src_rows))
+
+    def decode_launch(self, seqs: list, src_rows: Optional[list] = None) -> "DecodeHandle":
+        """Enqueue one decode step without waiting for it.  ``src_rows[i] >= 0``: sequence i's input
+        token is the one the previous (possibly still running) step sampled in that row; else its
+        ``last_token``.  Positions come from ``num_tokens``, so a sequence carrying a not yet
+        resolved token from the in-flight step is already one position further."""
         n = len(seqs)
         b = self.bucket_for(n) if self.graphs else n
-        ids, pos_a, slots, lens = self.n_ids, self.n_pos, self.n_slots, self.n_lens
-        temp, topk, topp, bt_a = self.n_temp, self.n_topk, self.n_topp, self.n_bt
+        st = self.stage[self._stage_i]
+        self._stage_i ^= 1
+        ids, pos_a, slots, lens, src = st.n_ids, st.n_pos, st.n_slots, st.n_lens, st.n_src
+        temp, topk, topp, bt_a = st.n_temp, st.n_topk, st.n_topp, st.n_bt
         bt_a[:b] = 0
         for i, s in enumerate(seqs):
             pos = s.num_tokens - 1  # position of the token being fed (the last generated one)
             bt = s.block_table
-            ids[i] = s.last_token
+            r = src_rows[i] if src_rows is not None else -1
+            src[i] = r
+            ids[i] = s.last_token if r < 0 else 0
             pos_a[i] = pos
             slots[i] = bt[pos // BLOCK_SIZE] * BLOCK_SIZE + pos % BLOCK_SIZE
             lens[i] = pos + 1
@@ -184,38 +193,69 @@ class ModelRunner:
             topp[i] = p.top_p
         if b > n:
             ids[n:b] = 0
+            src[n:b] = -1
             pos_a[n:b] = 0
             slots[n:b] = -1
             lens[n:b] = 0
             temp[n:b] = 0
             topk[n:b] = 0
             topp[n:b] = 1
-        hb = self.h_bt[:b]
         nb = True
-        self.d_ids[:b].copy_(self.h_ids[:b], non_blocking=nb)
-        self.d_pos[:b].copy_(self.h_pos[:b], non_blocking=nb)
-        self.d_slots[:b].copy_(self.h_slots[:b], non_blocking=nb)
-        self.d_lens[:b].copy_(self.h_lens[:b], non_blocking=nb)
-        self.d_bt[:b].copy_(hb, non_blocking=nb)
-        self.d_temp[:b].copy_(self.h_temp[:b], non_blocking=nb)
-        self.d_topk[:b].copy_(self.h_topk[:b], non_blocking=nb)
-        self.d_topp[:b].copy_(self.h_topp[:b], non_blocking=nb)
+        self.d_ids[:b].copy_(st.h_ids[:b], non_blocking=nb)
+        self.d_src[:b].copy_(st.h_src[:b], non_blocking=nb)
+        self.d_pos[:b].copy_(st.h_pos[:b], non_blocking=nb)
+        self.d_slots[:b].copy_(st.h_slots[:b], non_blocking=nb)
+        self.d_lens[:b].copy_(st.h_lens[:b], non_blocking=nb)
+        self.d_bt[:b].copy_(st.h_bt[:b], non_blocking=nb)
+        self.d_temp[:b].copy_(st.h_temp[:b], non_blocking=nb)
+        self.d_topk[:b].copy_(st.h_topk[:b], non_blocking=nb)
+        self.d_topp[:b].copy_(st.h_topp[:b], non_blocking=nb)
         g = self.graphs.get(b)
         if g is not None:
             g.replay()
         else:
             self._decode_body(b)
         self.n_steps["decode"] += 1
-        if self.is_gpu:
-            self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            return self.h_out[:n].tolist()
-        return self.d_out[:n].tolist()
+        if not self.is_gpu:
+            return DecodeHandle(n, None, self.d_out[:n].tolist())
+        h = self.h_out[self._out_i]
+        self._out_i ^= 1
+        h[:n].copy_(self.d_out[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return DecodeHandle(n, ev, h)
+
+    @staticmethod
+    def decode_collect(handle: "DecodeHandle") -> list[int]:
+        if handle.event is None:
+            return handle.out
+        handle.event.synchronize()
+        return handle.out[: handle.n].tolist()
 
     def memory_report(self) -> dict:
         kv = (self.k_cache.numel() + self.v_cache.numel()) * self.k_cache.element_size()
         return {"kv_cache_bytes": kv, "kv_blocks": self.num_blocks, "block_size": BLOCK_SIZE,
                 "max_model_len": self.max_len, "graph_buckets": sorted(self.graphs)}
+
+
+class _Staging:
+    """Pinned host buffers for one decode step's inputs, with numpy views for cheap writes."""
+
+    def __init__(self, B: int, max_blocks: int, pin: bool):
+        z = lambda *shape, dt=torch.int32: torch.zeros(*shape, dtype=dt, pin_memory=pin)  # noqa: E731
+        self.h_ids, self.h_pos, self.h_slots, self.h_lens, self.h_src = z(B), z(B), z(B), z(B), z(B)
+        self.h_bt = z(B, max_blocks)
+        self.h_temp, self.h_topk, self.h_topp = z(B, dt=torch.float32), z(B), z(B, dt=torch.float32)
+        self.n_ids, self.n_pos, self.n_slots = self.h_ids.numpy(), self.h_pos.numpy(), self.h_slots.numpy()
+        self.n_lens, self.n_src, self.n_bt = self.h_lens.numpy(), self.h_src.numpy(), self.h_bt.numpy()
+        self.n_temp, self.n_topk, self.n_topp = self.h_temp.numpy(), self.h_topk.numpy(), self.h_topp.numpy()
+
+
+@dataclass
+class DecodeHandle:
+    n: int
+    event: object  # torch.cuda.Event, None on the CPU
+    out: object  # pinned host tensor (GPU) or the token list (CPU)
 
 
 def kv_blocks_for(cfg_layers: int, hkv: int, D: int, gb: float) -> int:

@@ -209,7 +209,7 @@ class CausalLM:
         return tp_all_reduce(y, self.ps)
 
     def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None,
-                   rows: Optional[int] = None) -> torch.Tensor:
+                   rows: Optional[int] = None, rownorm: Optional[tuple] = None) -> torch.Tensor:
         """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
         ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM over ``x`` (row-major
         or fragment-packed with ``rows`` valid rows), reduced inside rope_and_cache; the attention
@@ -220,7 +220,7 @@ class CausalLM:
         T = rows if rows is not None else x.shape[0]
         if slabs is not None:
             ws, splits = slabs
-            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T)
+            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T, rownorm=rownorm)
             partial = ws
             qkv = torch.empty(T, L["wqkv_p"].shape[0] * 16, dtype=self.dtype, device=self.device)
         else:
@@ -370,33 +370,49 @@ class CausalLM:
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list]) -> torch.Tensor:
-        """Activations between the skinny GEMMs travel fragment-packed (whole-line A loads):
-        x_norm (reduce_add_rms_norm), the attention output (paged_decode) and the MLP activation
-        (SwiGLU epilogue) are all written in the A-operand layout."""
+        """Activations between the skinny GEMMs travel fragment-packed (whole-line A loads): the
+        attention output (paged_decode) and the MLP activation (SwiGLU epilogue) are written in the
+        A-operand layout, and every RMSNorm is deferred: add_norm_partial writes residual * w plus
+        per-row partial sums of squares, and the consuming GEMM scales its outputs by 1/rms."""
         c, ws, n = self.cfg, self._skinny_ws, len(self.layers)
+        eps = c.norm_eps
         M = residual.shape[0]
-        xp = ops.reduce_add_rms_norm(ops.packed_empty(M, c.d_model, self.dtype, self.device), residual, None, 0,
-                                     self.layers[0]["attn_norm"], c.norm_eps)
+        xw, rn = self._norm_tail(residual, None, 0, self.layers[0]["attn_norm"])
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
-            op = self._attn_core(L, xp, meta, kv, slabs=(ws, self._split_qkv), rows=M)
-            xp = self._row_parallel_tail(op, L["wo_p"], residual, L["mlp_norm"], self._split_o, M, packed_out=True)
-            act = ops.skinny_swiglu(xp, L["w13_p"], rows=M, packed_out=True)
-            last = i + 1 == n
-            nw = self.final_norm if last else self.layers[i + 1]["attn_norm"]
-            xp = self._row_parallel_tail(act, L["w2_p"], residual, nw, self._split_d, M, packed_out=not last)
-        return self._logits(xp)
+            op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
+            ns = ops.skinny_slabs(op, L["wo_p"], ws, self._split_o, rows=M)
+            xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
+            act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
+            ns = ops.skinny_slabs(act, L["w2_p"], ws, self._split_d, rows=M)
+            if i + 1 < n:
+                xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
+        # final norm feeds the LM head (hipBLASLt): complete, row-major
+        x = self._row_parallel_sum(ws, ns, M, residual)
+        if x is None:
+            x = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, self.final_norm, eps)
+        else:
+            x = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
+        return self._logits(x)
 
-    def _row_parallel_tail(self, a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w,
-                           splits: int, rows: int, packed_out: bool) -> torch.Tensor:
-        eps, ws = self.cfg.norm_eps, self._skinny_ws
-        if self.tp == 1:
-            return ops.proj_add_rms_norm(a, wp, residual, norm_w, eps, workspace=ws, splits=splits, rows=rows,
-                                         packed_out=packed_out)
-        ns = ops.skinny_slabs(a, wp, ws, splits, rows=rows)
-        y = ops.reduce_slabs(ws, ns, rows, wp.shape[0] * 16, dtype=residual.dtype)
-        x = ops.fused_add_rms_norm(tp_all_reduce(y, self.ps), residual, norm_w, eps)
-        return ops.pack_activation(x) if packed_out else x
+    def _row_parallel_sum(self, ws, ns: int, M: int, residual: torch.Tensor) -> Optional[torch.Tensor]:
+        """TP>1: the row-parallel projection's slabs summed to bf16 and all-reduced; None at TP=1."""
+        if self.tp == 1 or ns == 0:
+            return None
+        y = ops.reduce_slabs(ws, ns, M, residual.shape[1], dtype=residual.dtype)
+        return tp_all_reduce(y, self.ps)
+
+    def _norm_tail(self, residual: torch.Tensor, ws, ns: int, norm_w, rows: Optional[int] = None) -> tuple:
+        """residual += the projection's slabs; returns (A operand for the next skinny GEMM, rownorm)."""
+        eps = self.cfg.norm_eps
+        y = self._row_parallel_sum(ws, ns, residual.shape[0], residual)
+        if y is not None:  # TP>1: all-reduced partial sums, complete norm, packed A
+            return ops.pack_activation(ops.fused_add_rms_norm(y, residual, norm_w, eps)), None
+        if residual.shape[1] % 512 == 0:
+            xw, ss = ops.add_norm_partial(residual, ws, ns, norm_w)
+            return xw, (ss, eps)
+        out = ops.packed_empty(residual.shape[0], residual.shape[1], residual.dtype, residual.device)
+        return ops.reduce_add_rms_norm(out, residual, ws, ns, norm_w, eps), None
 
 
 _DUMMY_CS: dict = {}

@@ -99,9 +99,11 @@ def interleave_gate_up(w13: torch.Tensor) -> torch.Tensor:
     return w13.reshape(2, F // 32, 32, K).permute(1, 0, 2, 3).reshape(F2, K)
 
 
-def skinny_splits(N: int, K: int, target_wgs: int = 512) -> int:
-    """Split-K factor for a slab-epilogue gemm_skinny: (N/64) x S workgroups ~ two per CU, each K
-    slice at least 512 deep.  ``K8SLLM_SKINNY_SPLITS`` overrides."""
+def skinny_splits(N: int, K: int, target_wgs: int = 256) -> int:
+    """Split-K factor for a slab-epilogue gemm_skinny: (N/64) x S workgroups ~ one per CU, each K
+    slice at least 512 deep (tools/bench_skinny.py on MI355X, decode batch 1-64: S = 4 beats 2, 6
+    and 8 for Llama-3-8B o/down - more slices add slab traffic to the reduce faster than they add
+    weight-streaming parallelism).  ``K8SLLM_SKINNY_SPLITS`` overrides."""
     env = os.environ.get("K8SLLM_SKINNY_SPLITS")
     if env:
         return max(1, int(env))
@@ -165,30 +167,51 @@ def pack_activation(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     return out.copy_(p) if out is not None else p
 
 
+def _rn_scale(rownorm, M: int, K: int) -> Optional[torch.Tensor]:
+    """CPU form of the deferred RMSNorm row scale: 1 / rms per row from partial sums of squares."""
+    if rownorm is None:
+        return None
+    ss, eps = rownorm
+    return torch.rsqrt(ss[:M].float().sum(1, keepdim=True) / K + eps)
+
+
+def _rn_args(rownorm) -> tuple:
+    return (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
+
+
 def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  nt_tiles: int = 4, rows: Optional[int] = None) -> torch.Tensor:
-    """``a @ W^T`` for <= 64 rows over the fragment-packed weight, one K slice."""
+                  nt_tiles: int = 4, rows: Optional[int] = None, rownorm: Optional[tuple] = None) -> torch.Tensor:
+    """``a @ W^T`` for <= 64 rows over the fragment-packed weight, one K slice.  ``rownorm =
+    (ss_part, eps)``: ``a`` holds x * norm_w (add_norm_partial) and the rows' 1/rms is applied to
+    the outputs (the deferred RMSNorm)."""
     M = _rows(a, rows)
     if not _gpu(a):
         x = _cpu_a(a, rows)
-        y = (x.float() @ _cpu_w(wp).t()).to(x.dtype)
+        y = x.float() @ _cpu_w(wp).t()
+        sc = _rn_scale(rownorm, M, x.shape[1])
+        y = (y * sc if sc is not None else y).to(x.dtype)
         return out.copy_(y) if out is not None else y
     N = wp.shape[0] * 16
     if out is None:
         out = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, M)
+    native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, M, *_rn_args(rownorm))
     return out
 
 
 def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  rows: Optional[int] = None, packed_out: bool = False) -> torch.Tensor:
+                  rows: Optional[int] = None, packed_out: bool = False,
+                  rownorm: Optional[tuple] = None) -> torch.Tensor:
     """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F], or with
     ``packed_out`` the fragment-packed [ceil(M/16), F/32, 64, 8] (the down projection's A)."""
     M = _rows(a, rows)
     F = wp13.shape[0] * 8
     if not _gpu(a):
         x = _cpu_a(a, rows)
-        g, u = _cpu_deinterleave((x.float() @ _cpu_w(wp13).t()).to(x.dtype).float())
+        gu = x.float() @ _cpu_w(wp13).t()
+        sc = _rn_scale(rownorm, M, x.shape[1])
+        if sc is not None:
+            gu = gu * sc
+        g, u = _cpu_deinterleave(gu.to(x.dtype).float())
         y = (torch.nn.functional.silu(g) * u).to(x.dtype)
         if packed_out:
             y = pack_activation(y)
@@ -196,12 +219,12 @@ def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tenso
     if out is None:
         shape = (-(-M // 16), F // 32, 64, 8) if packed_out else (M, F)
         out = torch.empty(shape, dtype=a.dtype, device=a.device)
-    native().gemm_skinny(a, wp13, None, out, 1, 3 if packed_out else 2, 4, M)
+    native().gemm_skinny(a, wp13, None, out, 1, 3 if packed_out else 2, 4, M, *_rn_args(rownorm))
     return out
 
 
 def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, splits: int,
-                 nt_tiles: int = 4, rows: Optional[int] = None) -> int:
+                 nt_tiles: int = 4, rows: Optional[int] = None, rownorm: Optional[tuple] = None) -> int:
     """Split-K ``a @ W^T`` into fp32 slabs [S', M, N] in ``workspace``; returns S'."""
     M = _rows(a, rows)
     if not _gpu(a):
@@ -209,11 +232,38 @@ def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, spl
         N, K = wp.shape[0] * 16, wp.shape[1] * 32
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
         w = _cpu_w(wp)
+        sc = _rn_scale(rownorm, M, K)
         slabs = workspace[: ns * M * N].view(ns, M, N)
         for s in range(ns):
-            slabs[s] = x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].t()
+            y = x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].t()
+            slabs[s] = y * sc if sc is not None else y
         return ns
-    return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, M)
+    return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, M, *_rn_args(rownorm))
+
+
+def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int, norm_w: torch.Tensor,
+                     out: Optional[torch.Tensor] = None, ss_part: Optional[torch.Tensor] = None,
+                     packed: bool = True) -> tuple:
+    """Residual update with a deferred RMSNorm: ``residual <- residual + sum of slabs``;
+    returns ``(residual * norm_w`` (fragment-packed by default), ``ss_part [M, d/512])`` for a
+    consumer skinny GEMM called with ``rownorm=(ss_part, eps)``.  One wave per 512 columns: the
+    norm's row reduction is left to the consumer's epilogue."""
+    M, d = residual.shape
+    if ss_part is None:
+        ss_part = torch.empty(M, d // 512, dtype=torch.float32, device=residual.device)
+    if out is None:
+        out = packed_empty(M, d, residual.dtype, residual.device) if packed else torch.empty_like(residual)
+    if not _gpu(residual):
+        if nslabs:
+            s = workspace[: nslabs * M * d].view(nslabs, M, d).sum(0)
+            residual.copy_((residual.float() + s).to(residual.dtype))
+        v = residual.float()
+        ss_part.copy_((v * v).view(M, d // 512, 512).sum(-1))
+        y = (v * norm_w.float()).to(residual.dtype)
+        out.copy_(pack_activation(y) if out.dim() == 4 else y)
+        return out, ss_part
+    native().add_norm_partial(out, residual, workspace, nslabs, norm_w, ss_part)
+    return out, ss_part
 
 
 def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=torch.bfloat16,

@@ -34,7 +34,10 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
-                       int S, int epi, int nt_tiles, int a_packed, hipStream_t s);
+                       int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
+                       float rn_eps, hipStream_t s);
+int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
+                            const void* w, int d, float* ss_part, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
 int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
@@ -249,7 +252,8 @@ void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t 
 // written fragment-packed.  Returns the
 // number of slabs written (1 for epi 1/2).
 int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
-                    c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows) {
+                    c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows,
+                    c10::optional<torch::Tensor> rn_ss, double rn_eps) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
               "gemm_skinny: wp must be fragment-packed [N/16, K/32, 64, 8]");
@@ -294,10 +298,50 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
     }
     yp = y->data_ptr();
   }
+  const float* rp = nullptr;
+  int rn_nc = 0;
+  if (rn_ss.has_value()) {  // deferred RMSNorm: per-row partial sums of squares [M, K/512]
+    TORCH_CHECK(rn_ss->is_cuda() && rn_ss->scalar_type() == torch::kFloat32 && rn_ss->is_contiguous() &&
+                    rn_ss->dim() == 2 && rn_ss->size(0) >= M && rn_ss->size(1) * 512 == K,
+                "gemm_skinny: rn_ss must be [M, K/512] fp32");
+    rp = rn_ss->data_ptr<float>();
+    rn_nc = (int)rn_ss->size(1);
+  }
   check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
-                           epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, cur()),
+                           epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, rp, rn_nc, K,
+                           (float)rn_eps, cur()),
         "gemm_skinny");
   return S;
+}
+
+// residual += sum of S slabs; out = residual * w (row-major or fragment-packed); ss_part[m][c] =
+// sum of residual^2 over columns [512 c, 512 c + 512) - the deferred-RMSNorm producer.
+void add_norm_partial(torch::Tensor out, torch::Tensor residual, c10::optional<torch::Tensor> partial, int64_t S,
+                      torch::Tensor w, torch::Tensor ss_part) {
+  dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
+  TORCH_CHECK(residual.is_contiguous() && out.is_contiguous() && w.is_contiguous() && residual.dim() == 2,
+              "add_norm_partial layout");
+  const int M = (int)residual.size(0), d = (int)residual.size(1);
+  TORCH_CHECK(d % 512 == 0, "add_norm_partial: d % 512 != 0");
+  TORCH_CHECK(ss_part.is_cuda() && ss_part.scalar_type() == torch::kFloat32 && ss_part.is_contiguous() &&
+                  ss_part.numel() >= (int64_t)M * (d / 512), "ss_part");
+  const float* pp = nullptr;
+  if (S > 0) {
+    TORCH_CHECK(partial.has_value() && partial->scalar_type() == torch::kFloat32 && partial->is_contiguous() &&
+                    partial->numel() >= S * M * d, "partial");
+    pp = partial->data_ptr<float>();
+  }
+  long ostride = d;
+  if (out.dim() == 4) {
+    TORCH_CHECK(out.size(0) == (M + 15) / 16 && out.size(1) * 32 == d && out.size(2) == 64 && out.size(3) == 8,
+                "packed out must be [ceil(M/16), d/32, 64, 8]");
+    ostride = -(long)(d / 32);
+  } else {
+    TORCH_CHECK(out.numel() == (int64_t)M * d, "out shape");
+  }
+  check(k8sllm_add_norm_partial(out.data_ptr(), ostride, residual.data_ptr(), pp, (int)S, M, w.data_ptr(), d,
+                                ss_part.data_ptr<float>(), cur()),
+        "add_norm_partial");
 }
 
 void reduce_slabs(torch::Tensor out, torch::Tensor partial, int64_t S) {
@@ -354,4 +398,5 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gemm_skinny", &gemm_skinny);
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
+  m.def("add_norm_partial", &add_norm_partial);
 }

@@ -45,7 +45,8 @@ template <int MT, int NT, int EPI, bool APK>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
-                                                          int kchunk) {
+                                                          int kchunk, const float* __restrict__ rn_ss, int rn_nc,
+                                                          float rn_inv_d, float rn_eps) {
   // U k-steps per wave group; two groups in flight per wave (register double buffer)
   constexpr int U = MT <= 2 ? 4 : 2;
   __shared__ __attribute__((aligned(16))) float red[4][NT][64][4];  // one m-tile at a time: 16 KiB at NT 4
@@ -138,10 +139,24 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
       f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][nt][l][0]);
 #pragma unroll
       for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
+      // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms is
+      // applied here, once per output - linear, so it is exact for split-K slabs too
+      f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
+      if (rn_ss != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = min(mt * 16 + (l >> 4) * 4 + r, M - 1);
+          float ss = 0.f;
+          for (int c = 0; c < rn_nc; ++c) ss += rn_ss[row * rn_nc + c];
+          rs[r] = rsqrtf(ss * rn_inv_d + rn_eps);
+        }
+      }
+      v *= rs;
       if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
         f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][nt + NT / 2][l][0]);
 #pragma unroll
         for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
+        u *= rs;
         const int f = blockIdx.x * (NT * 8) + nt * 16 + (l & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -196,6 +211,7 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
     if (idx < d) {
       float acc[8];
       unpack8(*reinterpret_cast<const uint4*>(rr + idx), acc);
+#pragma unroll 4
       for (int s = 0; s < S; ++s) {
         const float* p = partial + ((long)s * M + row) * d + idx;
         const float4 a = *reinterpret_cast<const float4*>(p);
@@ -224,6 +240,45 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
   }
 }
 
+// Residual update with a deferred RMSNorm, fully parallel (grid (M, d/512), one wave per 512
+// columns): residual <- bf16(residual + sum_s partial[s]); out <- bf16(residual * w) (packed via
+// act_index); ss_part[m][chunk] <- sum of residual^2 over the chunk.  The consumer skinny GEMM
+// applies 1/rms per row (rn_ss).  Replaces a one-workgroup-per-row norm pass, which is latency-
+// bound at decode batch sizes (64 workgroups on 256 CUs).
+__global__ __launch_bounds__(64) void add_norm_partial_kernel(bf16_t* __restrict__ out, long out_stride,
+                                                              bf16_t* __restrict__ residual,
+                                                              const float* __restrict__ partial, int S, int M,
+                                                              const bf16_t* __restrict__ w, int d,
+                                                              float* __restrict__ ss_part) {
+  const int row = blockIdx.x, chunk = blockIdx.y;
+  const int col = chunk * 512 + threadIdx.x * 8;
+  bf16_t* rr = residual + (long)row * d + col;
+  float acc[8];
+  unpack8(*reinterpret_cast<const uint4*>(rr), acc);
+#pragma unroll 4
+  for (int s = 0; s < S; ++s) {
+    const float* p = partial + ((long)s * M + row) * d + col;
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  }
+  const uint4 q = pack8(acc);
+  if (S > 0) *reinterpret_cast<uint4*>(rr) = q;
+  float v[8], wf[8], o[8];
+  unpack8(q, v);
+  unpack8(*reinterpret_cast<const uint4*>(w + col), wf);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss += v[j] * v[j];
+    o[j] = v[j] * wf[j];
+  }
+  *reinterpret_cast<uint4*>(out + act_index(row, col, out_stride)) = pack8(o);
+  ss = wave_sum(ss);
+  if (threadIdx.x == 0) ss_part[row * (d / 512) + chunk] = ss;
+}
+
 // out[i] = bf16(sum_s partial[s][i]) over n elements (n % 8 == 0): the TP>1 decode tails sum
 // the split-K slabs before the RCCL all-reduce.
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(bf16_t* __restrict__ out,
@@ -243,6 +298,15 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(bf16_t* __restrict__ 
 }  // namespace k8sllm
 
 using namespace k8sllm;
+
+extern "C" int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S,
+                                       int M, const void* w, int d, float* ss_part, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (d % 512 != 0) return -1;
+  hipLaunchKernelGGL(add_norm_partial_kernel, dim3(M, d / 512), dim3(64), 0, s, (bf16_t*)out, out_stride,
+                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, ss_part);
+  return (int)hipGetLastError();
+}
 
 extern "C" int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s) {
   if (n <= 0) return 0;
@@ -268,8 +332,11 @@ extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
 
 // epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; a_packed: A in the
 // fragment-packed layout (lda ignored)
+// rn_ss (optional): per-row partial sums of squares [M][rn_nc] of the un-normalised A rows
+// (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
-                                  int N, int K, int S, int epi, int nt_tiles, int a_packed, hipStream_t s) {
+                                  int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
+                                  int rn_nc, int rn_d, float rn_eps, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > 64 || K % 32 != 0 || S < 1 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   const int kc = skinny_kchunk(K, S);
@@ -280,7 +347,8 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
   const int MT = (M + 15) / 16;
 #define K8S_SK(MTV, NTV, EPV, APKV)                                                                            \
   hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc)
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc,                  \
+                     rn_d > 0 ? 1.f / (float)rn_d : 0.f, rn_eps)
 #define K8S_SK_M(NTV, EPV, NTLV)             \
   switch (MT) {                              \
     case 1: K8S_SK(1, NTV, EPV, NTLV); break; \

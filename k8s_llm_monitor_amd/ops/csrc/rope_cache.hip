@@ -16,6 +16,7 @@ template <int N>
 __device__ __forceinline__ void slab_sum(const float* __restrict__ p, long slab_stride, int S, float* out) {
 #pragma unroll
   for (int j = 0; j < N; ++j) out[j] = 0.f;
+#pragma unroll 4
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int j = 0; j < N; j += 4) {

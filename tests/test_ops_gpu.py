@@ -326,3 +326,25 @@ def test_skinny_swiglu_packed_out_feeds_down(M):
     y = ops.skinny_linear(actp, ops.pack_skinny(w2), rows=M)
     _close(y.cpu(), torch.nn.functional.linear(act_ref.float(), w2.cpu().float()), atol=5e-2, rtol=3e-2,
            what="down from packed act")
+
+
+@pytest.mark.parametrize("M", [1, 21, 64])
+def test_deferred_rmsnorm_chain(M):
+    """add_norm_partial (residual += slabs; residual * w; partial sums of squares) followed by a
+    skinny GEMM with rownorm == rms_norm(residual) @ W^T."""
+    d, N, S = 4096, 512, 3
+    r = torch.randn(M, d, device=DEV, dtype=torch.bfloat16)
+    slabs = torch.randn(S, M, d, device=DEV, dtype=torch.float32) * 0.1
+    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, d, device=DEV, dtype=torch.bfloat16) * 0.02).to(torch.bfloat16)
+    r_ref = (r.cpu().float() + slabs.cpu().sum(0)).to(torch.bfloat16)
+    x_ref = ref.rms_norm(r_ref, nw.cpu(), 1e-5)
+    y_ref = torch.nn.functional.linear(x_ref.float(), w.cpu().float())
+    xw, ss = ops.add_norm_partial(r, slabs.reshape(-1), S, nw)
+    _close(r.cpu(), r_ref, atol=1e-2, rtol=1e-2, what="residual")
+    _close(ss.sum(1).cpu(), (r_ref.float() ** 2).sum(1), atol=1.0, rtol=1e-3, what="sum of squares")
+    y = ops.skinny_linear(xw, ops.pack_skinny(w), rows=M, rownorm=(ss, 1e-5))
+    _close(y.cpu(), y_ref, atol=3e-2, rtol=3e-2, what="deferred-norm GEMM")
+    ws = ops.skinny_workspace(M, N, 4, DEV)
+    ns = ops.skinny_slabs(xw, ops.pack_skinny(w), ws, 4, rows=M, rownorm=(ss, 1e-5))
+    _close(ops.reduce_slabs(ws, ns, M, N).cpu(), y_ref, atol=3e-2, rtol=3e-2, what="deferred-norm slabs")

@@ -29,9 +29,9 @@ def test_interleave_gate_up():
 
 def test_skinny_splits_bounds(monkeypatch):
     monkeypatch.delenv("K8SLLM_SKINNY_SPLITS", raising=False)
-    assert ops.skinny_splits(4096, 4096) == 8
-    assert ops.skinny_splits(4096, 14336) == 8
-    assert ops.skinny_splits(6144, 4096) == 5
+    assert ops.skinny_splits(4096, 4096) == 4
+    assert ops.skinny_splits(4096, 14336) == 4
+    assert ops.skinny_splits(6144, 4096) == 3
     assert ops.skinny_splits(64, 256) == 1
     monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")
     assert ops.skinny_splits(4096, 4096) == 3
