@@ -34,7 +34,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import reference as ref
-from ..parallel.comm import shard_range, tp_all_gather_last, tp_all_reduce
+from ..parallel.comm import shard_range, tp_all_gather_last, tp_all_gather_rows, tp_all_reduce, tp_all_to_all
 from ..parallel.state import ParallelState, get_state
 from .config import ModelConfig
 
@@ -86,6 +86,7 @@ class CausalLM:
             if cfg.n_experts % tp:
                 raise ValueError("n_experts must be divisible by tp for expert parallelism")
             self.e_lo, self.e_hi = shard_range(cfg.n_experts, tp, r)
+        self.moe_comm = os.environ.get("K8SLLM_MOE_COMM", "a2a")  # "a2a" (prefill all-to-all EP) | "allreduce"
         self.layers: list[dict] = []
         self._build()
         self._init_skinny()
@@ -247,6 +248,8 @@ class CausalLM:
                 y += L["b2"]
             return tp_all_reduce(y, self.ps)
         if c.is_moe:
+            if meta.is_prefill and self.tp > 1 and self.moe_comm == "a2a":
+                return self._moe_a2a(L, x)
             return tp_all_reduce(self._moe(L, x, meta), self.ps)
         h = ops.silu_mul(F.linear(x, L["w13"]))
         return tp_all_reduce(F.linear(h, L["w2"]), self.ps)
@@ -280,6 +283,51 @@ class CausalLM:
                 h = ops.silu_mul(F.linear(xs[a:b], L["w13"][j]))
                 ys[a:b] = F.linear(h, L["w2"][j])
         return ops.moe_combine(ys, inv_idx, w, T)
+
+    def _moe_a2a(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+        """Expert-parallel MoE with all-to-all dispatch / combine, for prefill
+        at TP>1.  Activations arrive replicated (tensor-parallel attention); rank r routes its
+        1/tp slice of the tokens, sends every (token, expert) row to the rank owning the expert,
+        the owners run their experts on what they received (one GEMM pair per local expert over
+        contiguous rows), the results travel back by the reverse all-to-all, are combined with the
+        routing weights, and the slices are all-gathered to the replicated layout the next layer's
+        attention expects.  Decode keeps the graph-capturable replicated form (_moe + all-reduce):
+        all-to-all splits are data-dependent and need a host sync."""
+        c = self.cfg
+        T, K, P, r = x.shape[0], c.top_k_experts, self.tp, self.rank
+        epr = c.n_experts // P
+        chunk = -(-T // P)
+        t0, t1 = min(T, r * chunk), min(T, (r + 1) * chunk)
+        n = t1 - t0
+        xs = x[t0:t1]
+        logits = F.linear(xs, L["router"]).float()
+        ids, w = ops.moe_route(logits, K, True)
+        offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
+        send = ops.gather_rows(xs, sorted_idx, K) if n else xs.new_zeros(0, c.d_model)
+        send_exp = ids.reshape(-1)[sorted_idx.long()].to(torch.int64)
+        off = offsets.tolist()  # host sync: all-to-all split sizes
+        send_counts = [off[(p + 1) * epr] - off[p * epr] for p in range(P)]
+        cnt = torch.tensor(send_counts, dtype=torch.int64, device=x.device)
+        rcnt = torch.empty_like(cnt)
+        tp_all_to_all(rcnt, cnt, [1] * P, [1] * P, self.ps)
+        recv_counts = rcnt.tolist()
+        nrecv = sum(recv_counts)
+        recv = x.new_empty(nrecv, c.d_model)
+        tp_all_to_all(recv, send, recv_counts, send_counts, self.ps)
+        recv_exp = torch.empty(nrecv, dtype=torch.int64, device=x.device)
+        tp_all_to_all(recv_exp, send_exp, recv_counts, send_counts, self.ps)
+        y = torch.zeros_like(recv)
+        for j, e in enumerate(range(self.e_lo, self.e_hi)):
+            rows = (recv_exp == e).nonzero().flatten()
+            if rows.numel():
+                h = ops.silu_mul(F.linear(recv[rows], L["w13"][j]))
+                y[rows] = F.linear(h, L["w2"][j])
+        back = x.new_empty(n * K, c.d_model)
+        tp_all_to_all(back, y, send_counts, recv_counts, self.ps)
+        out = ops.moe_combine(back, inv_idx, w, n) if n else back[:0]
+        if n < chunk:  # equal-size blocks for the all-gather
+            out = torch.cat([out, out.new_zeros(chunk - n, c.d_model)])
+        return tp_all_gather_rows(out, self.ps)[:T]
 
     def _norm(self, x: torch.Tensor, w) -> torch.Tensor:
         if isinstance(w, tuple):

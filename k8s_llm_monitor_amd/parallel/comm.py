@@ -38,6 +38,30 @@ def tp_all_gather_last(x: torch.Tensor, ps=None) -> torch.Tensor:
     return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
 
 
+def tp_all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits: list, in_splits: list, ps=None) -> torch.Tensor:
+    """Uneven all-to-all of rows over the TP group (C-5: MoE expert dispatch / combine)."""
+    st = ps or get_state()
+    if st.tp_size == 1:
+        out.copy_(inp)
+        return out
+    dist.all_to_all_single(out, inp.contiguous(), out_splits, in_splits, group=st.tp_group)
+    return out
+
+
+def tp_all_gather_rows(x: torch.Tensor, ps=None) -> torch.Tensor:
+    """Concatenate equal-shaped [n, ...] row blocks of every TP rank in rank order."""
+    st = ps or get_state()
+    if st.tp_size == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        dist.all_gather_into_tensor(out, x, group=st.tp_group)
+    else:
+        dist.all_gather(list(out.chunk(st.tp_size)), x, group=st.tp_group)
+    return out
+
+
 def tp_broadcast_object(obj, src_tp_rank: int = 0, ps=None):
     """Broadcast a picklable control message (the step schedule, C-6) from the TP leader over the
     CPU gloo group."""

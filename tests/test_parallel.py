@@ -78,3 +78,51 @@ def test_tp2_matches_tp1(model):
         assert err < 2e-3, f"rank {rank}: max |tp - ref| = {err}"
         if rank == 0:
             assert toks == ref
+
+
+def _a2a_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
+    from k8s_llm_monitor_amd.parallel.state import ParallelState, destroy, init_parallel
+
+    try:
+        ps = init_parallel(tp_size=world, device="cpu")
+        cfg = get_config("mixtral-tiny")
+        res = []
+        for n in (7, 1, 2, 9):  # uneven token slices, including empty ones
+            ids = torch.arange(5, 5 + n, dtype=torch.int32)
+            cu = torch.tensor([0, n], dtype=torch.int32)
+            meta = AttnMeta(is_prefill=True, positions=torch.arange(n, dtype=torch.int32),
+                            slot_mapping=torch.full((n,), -1, dtype=torch.int32), cu_seqlens=cu,
+                            logits_idx=torch.arange(n))
+            outs = {}
+            for mode in ("a2a", "allreduce"):
+                os.environ["K8SLLM_MOE_COMM"] = mode
+                m = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=4, pstate=ps)
+                outs[mode] = m.forward(ids, meta, None)
+            ref = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=4, pstate=ParallelState()).forward(
+                ids, meta, None)
+            res.append(max((outs["a2a"] - ref).abs().max().item(), (outs["allreduce"] - ref).abs().max().item()))
+        q.put((rank, res))
+        destroy()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_moe_all_to_all_matches_allreduce_and_tp1():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(60)
+    for rank, errs in res:
+        assert not isinstance(errs, str), errs
+        assert max(errs) < 2e-3, f"rank {rank}: {errs}"
