@@ -121,6 +121,8 @@ def main() -> None:
     p50_local = statistics.median(lats)
     p50 = comm.all_reduce_max_scalar(p50_local)
     stats = svc.stats()
+    if eng.trace is not None and rank == 0:
+        _print_trace(eng.trace, t0)
     svc.close()
     if server is not None:
         server.shutdown()
@@ -156,6 +158,24 @@ def main() -> None:
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+
+
+def _print_trace(trace: list, t0: float) -> None:
+    """K8SLLM_TRACE=1: per timed wave, when requests arrived, the prefill batches and the decode
+    span (stderr)."""
+    ev = [e for e in trace if e[0] >= t0]
+    adds = [e for e in ev if e[1] == "add"]
+    pre = [e for e in ev if e[1] == "prefill"]
+    dec = [e for e in ev if e[1] == "decode"]
+    if not adds:
+        return
+    print(f"[trace] adds {len(adds)} first +{(adds[0][0] - t0) * 1e3:.1f} ms last +{(adds[-1][0] - t0) * 1e3:.1f} ms",
+          file=sys.stderr)
+    for e in pre:
+        print(f"[trace] prefill +{(e[0] - t0) * 1e3:.1f} ms seqs {e[2]} tokens {e[3]}", file=sys.stderr)
+    if dec:
+        print(f"[trace] decode steps {len(dec)} first +{(dec[0][0] - t0) * 1e3:.1f} last +{(dec[-1][0] - t0) * 1e3:.1f} ms",
+              file=sys.stderr)
 
 
 if __name__ == "__main__":

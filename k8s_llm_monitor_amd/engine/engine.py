@@ -14,6 +14,7 @@ replicated (same logits, same RNG counter) so no token broadcast is needed.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -90,6 +91,7 @@ class LLMEngine:
                          "prefill_steps": 0, "decode_steps": 0, "preemptions": 0}
         self.is_leader = self.ps.tp_rank == 0
         self._inflight = None  # (seqs, DecodeHandle) of the enqueued, not yet read back decode step
+        self.trace: Optional[list] = [] if os.environ.get("K8SLLM_TRACE") else None  # (t, kind, n, tokens)
         self._inflight_rows: dict = {}
 
     # ----------------------------------------------------------------- public API
@@ -109,6 +111,8 @@ class LLMEngine:
         seq = Sequence(prompt_ids=ids, params=params or SamplingParams(),
                        request_id=request_id or uuid.uuid4().hex[:16], user=user)
         self.sched.add(seq)
+        if self.trace is not None:
+            self.trace.append((time.perf_counter(), "add", 1, len(ids)))
         self.counters["requests"] += 1
         self.counters["prompt_tokens"] += len(ids)
         return seq
@@ -153,6 +157,8 @@ class LLMEngine:
                                          for q in seqs], src), ps=self.ps)
         handle = self.runner.decode_launch(seqs, src)
         self.counters["decode_steps"] += 1
+        if self.trace is not None:
+            self.trace.append((time.perf_counter(), "decode", len(seqs), 0))
         for q in seqs:
             q.output_ids.append(self.PENDING)
         prev = self._inflight
@@ -214,6 +220,9 @@ class LLMEngine:
         if plan.is_prefill:
             toks = self.runner.prefill(plan.seqs)
             self.counters["prefill_steps"] += 1
+            if self.trace is not None:
+                self.trace.append((time.perf_counter(), "prefill", len(plan.seqs),
+                                   sum(q.num_tokens for q in plan.seqs)))
         else:
             toks = self.runner.decode(plan.seqs)
             self.counters["decode_steps"] += 1

@@ -456,7 +456,7 @@ class CausalLM:
         y = self._row_parallel_sum(ws, ns, residual.shape[0], residual)
         if y is not None:  # TP>1: all-reduced partial sums, complete norm, packed A
             return ops.pack_activation(ops.fused_add_rms_norm(y, residual, norm_w, eps)), None
-        if residual.shape[1] % 512 == 0:
+        if residual.shape[1] % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0":
             xw, ss = ops.add_norm_partial(residual, ws, ns, norm_w)
             return xw, (ss, eps)
         out = ops.packed_empty(residual.shape[0], residual.shape[1], residual.dtype, residual.device)

@@ -38,6 +38,21 @@ WEB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.a
 VERSION = "1.0.0"
 
 
+_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def _bounded_pool():
+    global _POOL
+    if _POOL is None:
+        with _POOL_LOCK:
+            if _POOL is None:
+                import concurrent.futures as cf
+
+                _POOL = cf.ThreadPoolExecutor(max_workers=512, thread_name_prefix="bounded")
+    return _POOL
+
+
 class Reply(Exception):
     def __init__(self, code: int, body: bytes, ctype: str, headers: Optional[dict] = None):
         self.code, self.body, self.ctype, self.headers = code, body, ctype, headers or {}
@@ -280,12 +295,10 @@ class MonitorApp:
         return self.analysis is not None and not isinstance(self.analysis.backend, RuleBackend)
 
     def _bounded(self, fn):
-        """Run fn within the write timeout (leave 0.5 s to write the answer)."""
-        import concurrent.futures as cf
-
+        """Run fn within the write timeout (leave 0.5 s to write the answer).  One shared pool (no
+        thread spawned per request); a timed-out call keeps its worker until the engine answers."""
         limit = max(0.5, min(self.llm_timeout_s, self.write_timeout_s) - 0.5)
-        with cf.ThreadPoolExecutor(max_workers=1) as ex:
-            return ex.submit(fn).result(timeout=limit)
+        return _bounded_pool().submit(fn).result(timeout=limit)
 
     def query(self, method, body, q) -> Reply:
         _only(method, "POST")

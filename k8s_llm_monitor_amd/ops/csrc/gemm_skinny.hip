@@ -79,6 +79,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // deferred RMSNorm: 1/rms of each A row from its partial sums of squares, once per workgroup
+  // (its loads overlap the first weight loads; read back in the epilogue after the barriers)
+  __shared__ float s_inv[MT * 16];
+  if (rn_ss != nullptr && threadIdx.x < MT * 16) {
+    const int row = min((int)threadIdx.x, M - 1);
+    float ss = 0.f;
+    for (int c = 0; c < rn_nc; ++c) ss += rn_ss[row * rn_nc + c];
+    s_inv[threadIdx.x] = rsqrtf(ss * rn_inv_d + rn_eps);
+  }
+
   auto load = [&](SkinnyBatch<U, MT, NT>& bt, int i0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -139,17 +149,12 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
       f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][nt][l][0]);
 #pragma unroll
       for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
-      // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms is
-      // applied here, once per output - linear, so it is exact for split-K slabs too
+      // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms
+      // (s_inv, computed at kernel start) is applied here - linear, so exact for split-K slabs too
       f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
       if (rn_ss != nullptr) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = min(mt * 16 + (l >> 4) * 4 + r, M - 1);
-          float ss = 0.f;
-          for (int c = 0; c < rn_nc; ++c) ss += rn_ss[row * rn_nc + c];
-          rs[r] = rsqrtf(ss * rn_inv_d + rn_eps);
-        }
+        for (int r = 0; r < 4; ++r) rs[r] = s_inv[mt * 16 + (l >> 4) * 4 + r];
       }
       v *= rs;
       if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
