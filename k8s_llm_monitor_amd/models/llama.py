@@ -410,10 +410,14 @@ class CausalLM:
             L["wo_p"] = ops.pack_skinny(L["wo"])
             L["w13_p"] = ops.pack_skinny(ops.interleave_gate_up(L["w13"]))
             L["w2_p"] = ops.pack_skinny(L["w2"])
-        self._split_qkv = ops.skinny_splits(nq, d)
-        self._split_o = ops.skinny_splits(d, self.hq * self.D)
-        self._split_d = ops.skinny_splits(d, self.f_local)
-        n = max(self._split_qkv * nq, self._split_o * d, self._split_d * d)
+        env = os.environ.get("K8SLLM_SKINNY_SPLITS")
+        split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
+        self._split_qkv = self._split_o = self._split_d = split
+
+        def most(N: int, K: int) -> int:
+            return split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
+
+        n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d, most(d, self.f_local) * d)
         self._skinny_ws = torch.empty(n * ops.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,

@@ -91,12 +91,13 @@ def unpack_skinny(wp: torch.Tensor) -> torch.Tensor:
 
 
 def interleave_gate_up(w13: torch.Tensor) -> torch.Tensor:
-    """[gate (F rows); up (F rows)] -> per 64-row tile [32 gate | 32 up] rows (the SWIGLU epilogue)."""
+    """[gate (F rows); up (F rows)] -> per 128-row tile [64 gate | 64 up] rows (the SWIGLU
+    epilogues: gate and up of an output column land in the same workgroup)."""
     F2, K = w13.shape
     F = F2 // 2
-    if F % 32:
-        raise ValueError("interleave_gate_up: F must be a multiple of 32")
-    return w13.reshape(2, F // 32, 32, K).permute(1, 0, 2, 3).reshape(F2, K)
+    if F % 64:
+        raise ValueError("interleave_gate_up: F must be a multiple of 64")
+    return w13.reshape(2, F // 64, 64, K).permute(1, 0, 2, 3).reshape(F2, K)
 
 
 def skinny_splits(N: int, K: int, target_wgs: int = 256) -> int:
@@ -138,7 +139,7 @@ def _cpu_w(wp: torch.Tensor) -> torch.Tensor:
 
 def _cpu_deinterleave(gu: torch.Tensor) -> tuple:
     M, F2 = gu.shape
-    t = gu.reshape(M, F2 // 64, 2, 32)
+    t = gu.reshape(M, F2 // 128, 2, 64)
     return t[:, :, 0].reshape(M, F2 // 2), t[:, :, 1].reshape(M, F2 // 2)
 
 
@@ -176,7 +177,16 @@ def _rn_scale(rownorm, M: int, K: int) -> Optional[torch.Tensor]:
 
 
 def _rn_args(rownorm) -> tuple:
-    return (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
+    wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1"  # opt-in: measured slower (gemm_skinny.hip)
+    return (None, 0.0, wide) if rownorm is None else (rownorm[0], float(rownorm[1]), wide)
+
+
+def skinny_auto_splits(M: int, N: int, K: int, packed: bool = True) -> int:
+    """Mirror of k8sllm_gemm_skinny_auto_splits: ~one workgroup per CU for the kernel the launcher
+    picks (wide: 128 columns per workgroup for packed A with 32 < M <= 64; narrow: 64)."""
+    wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1" and packed and M > 32 and N % 128 == 0
+    tiles = max(1, N // (128 if wide else 64))
+    return max(1, min(max(1, K // 512), (256 + tiles // 2) // tiles))
 
 
 def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -230,6 +240,8 @@ def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, spl
     if not _gpu(a):
         x = _cpu_a(a, rows)
         N, K = wp.shape[0] * 16, wp.shape[1] * 32
+        if splits <= 0:
+            splits = skinny_auto_splits(M, N, K, a.dim() == 4)
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
         w = _cpu_w(wp)
         sc = _rn_scale(rownorm, M, K)
@@ -310,9 +322,9 @@ def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor,
     then reduce_add_rms_norm."""
     M, N, K = _rows(a, rows), wp.shape[0] * 16, wp.shape[1] * 32
     if splits is None:
-        splits = skinny_splits(N, K)
+        splits = 0  # automatic (launcher)
     if workspace is None:
-        workspace = skinny_workspace(M, N, splits, a.device)
+        workspace = skinny_workspace(M, N, splits or skinny_auto_splits(M, N, K, a.dim() == 4), a.device)
     s = skinny_slabs(a, wp, workspace, splits, rows=M)
     if out is None:
         out = (packed_empty(M, N, residual.dtype, a.device) if packed_out

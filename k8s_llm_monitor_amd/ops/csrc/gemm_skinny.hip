@@ -34,6 +34,19 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2, EPI_SWIGLU_PACKED = 3 };
 
+// n-tile read for the workgroup's nt-th tile.  SwiGLU weights are interleaved per 128 rows as
+// [64 gate | 64 up] (interleave_gate_up): a 4-tile workgroup takes two gate tiles and the two
+// matching up tiles, so every output column has its gate and up value in the same workgroup.
+template <int EPI, int NT>
+__device__ __forceinline__ int swiglu_tile(int ntile0, int nt) {
+  if constexpr (EPI == 2 || EPI == 3) {
+    const int bx = ntile0 / NT;
+    return (bx >> 1) * 8 + (bx & 1) * 2 + (nt & 1) + (nt >> 1) * 4;
+  } else {
+    return ntile0 + nt;
+  }
+}
+
 // Loads of one wave group: U consecutive k-steps, NT weight and MT activation fragments each.
 template <int U, int MT, int NT>
 struct SkinnyBatch {
@@ -60,7 +73,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
   const u32x4* wp[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    wp[nt] = reinterpret_cast<const u32x4*>(Wp) + ((long)(ntile0 + nt) * ksteps + (kbeg >> 5)) * 64 + lane;
+    wp[nt] = reinterpret_cast<const u32x4*>(Wp) + ((long)swiglu_tile<EPI, NT>(ntile0, nt) * ksteps + (kbeg >> 5)) * 64 +
+             lane;
   // A: row-major [M][lda] (fragment-shaped loads, padding rows clamped) or, APK, fragment-packed
   // like W ([ceil(M/16)][K/32][64][8], padding rows present) so A loads are 1 KiB contiguous too
   const bf16_t* ap[MT];
@@ -162,7 +176,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
         for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
         u *= rs;
-        const int f = blockIdx.x * (NT * 8) + nt * 16 + (l & 15);
+        // gate n-tiles 8q + 2h + {0,1} pair with up n-tiles 8q + 4 + 2h + {0,1} (swiglu_tile)
+        const int f = (blockIdx.x >> 1) * 64 + (blockIdx.x & 1) * 32 + nt * 16 + (l & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = mt * 16 + (l >> 4) * 4 + r;
@@ -241,6 +256,135 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
       *reinterpret_cast<uint4*>(out + act_index(row, idx, out_stride)) = pack8(o);
+    }
+  }
+}
+
+// Wide variant for 32 < M <= 64 (A fragment-packed): the 4 waves own the 4 m-tiles, a workgroup
+// covers 128 output columns (8 n-tiles) of one K slice, and the weight tile is staged through LDS
+// once and shared by the waves.  Compared with the narrow kernel (waves split K, 64 columns), the
+// activation bytes read per weight byte halve (64 rows / 128 columns), every A fragment is read by
+// exactly one wave, and the epilogue needs no cross-wave reduction.  Register-staged double
+// buffer: group g+1's weight and activation loads are in flight while group g is multiplied.
+// Measured on MI355X (tools/bench_skinny.py, M 33-64, Llama-3-8B shapes): 10-25 % SLOWER than the
+// narrow kernel - one 16 KiB group in flight per workgroup plus a barrier per group cost more than
+// the halved activation traffic saves - so it is opt-in (K8SLLM_SKINNY_WIDE=1), kept as the
+// starting point for an LDS-DMA ring version.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_skinny_wide_kernel(const bf16_t* __restrict__ A,
+                                                               const bf16_t* __restrict__ Wp,
+                                                               float* __restrict__ partial, bf16_t* __restrict__ Y,
+                                                               long ldy, int M, int N, int K, int kchunk,
+                                                               const float* __restrict__ rn_ss, int rn_nc,
+                                                               float rn_inv_d, float rn_eps) {
+  constexpr int NT = 8, U = 2;
+  constexpr int WPW = U * NT / 4;  // 1 KiB weight blocks staged per wave per group
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][U * NT][64];
+  __shared__ float s_inv[64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile0 = blockIdx.x * NT;
+  const int s = blockIdx.y;
+  const int kbeg = s * kchunk;
+  const int nsteps = (min(K, kbeg + kchunk) - kbeg) >> 5;
+  const int ksteps = K >> 5;
+  const int MT = (M + 15) >> 4;
+  const bool active = wave < MT;
+
+  if (rn_ss != nullptr && threadIdx.x < 64) {
+    const int row = min((int)threadIdx.x, M - 1);
+    float ss = 0.f;
+    for (int c = 0; c < rn_nc; ++c) ss += rn_ss[row * rn_nc + c];
+    s_inv[threadIdx.x] = rsqrtf(ss * rn_inv_d + rn_eps);
+  }
+
+  const u32x4* wbase = reinterpret_cast<const u32x4*>(Wp) + (long)(kbeg >> 5) * 64 + lane;
+  const bf16x8* abase = reinterpret_cast<const bf16x8*>(A) + ((long)min(wave, MT - 1) * ksteps + (kbeg >> 5)) * 64 +
+                        lane;
+  auto load_w = [&](u32x4* r, int g) {
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int idx = wave * WPW + j, u = idx / NT, nt = idx % NT;
+      const int st = min(g * U + u, nsteps - 1);
+      r[j] = __builtin_nontemporal_load(wbase + ((long)(tile0 + nt) * ksteps + st) * 64);
+    }
+  };
+  auto load_a = [&](bf16x8* r, int g) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = abase[(long)min(g * U + u, nsteps - 1) * 64];
+  };
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ngroups = (nsteps + U - 1) / U;
+  u32x4 wr[WPW];
+  bf16x8 ar[U], ac[U];
+  load_w(wr, 0);
+  load_a(ar, 0);
+  for (int g = 0; g < ngroups; ++g) {
+    const int buf = g & 1;
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) sW[buf][wave * WPW + j][lane] = wr[j];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ac[u] = ar[u];
+    if (g + 1 < ngroups) {
+      load_w(wr, g + 1);
+      load_a(ar, g + 1);
+    }
+    __syncthreads();  // group g staged by every wave (and group g-1's reads of this buffer done)
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (g * U + u < nsteps) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[u], __builtin_bit_cast(bf16x8, sW[buf][u * NT + nt][lane]),
+                                                              acc[nt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (!active) return;
+  f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
+  if (rn_ss != nullptr) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rs[r] = s_inv[wave * 16 + (lane >> 4) * 4 + r];
+  }
+  if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
+#pragma unroll
+    for (int nt = 0; nt < NT / 2; ++nt) {
+      const f32x4 gv = acc[nt] * rs, uv = acc[nt + NT / 2] * rs;
+      const int f = blockIdx.x * 64 + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 16 + (lane >> 4) * 4 + r;
+        const float g = bf2f(f2bf(gv[r]));
+        const float uu = bf2f(f2bf(uv[r]));
+        const bf16_t o = f2bf(g * uu / (1.f + __expf(-g)));
+        if constexpr (EPI == EPI_SWIGLU_PACKED) {
+          const int F = N >> 1;
+          Y[(((long)wave * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 + (row & 15)) * 8 + (f & 7)] = o;
+        } else if (row < M) {
+          Y[(long)row * ldy + f] = o;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const f32x4 v = acc[nt] * rs;
+      const int col = (tile0 + nt) * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 16 + (lane >> 4) * 4 + r;
+        if (row < M) {
+          if constexpr (EPI == EPI_BF16)
+            Y[(long)row * ldy + col] = f2bf(v[r]);
+          else
+            partial[((long)s * M + row) * N + col] = v[r];
+        }
+      }
     }
   }
 }
@@ -337,23 +481,53 @@ extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
 
 // epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; a_packed: A in the
 // fragment-packed layout (lda ignored)
+// Kernel choice: the wide kernel for fragment-packed A with 32 < M <= 64 and N % 128 == 0
+// (unless disabled), else the narrow one.  splits <= 0: automatic split-K, about one workgroup per
+// CU (tools/bench_skinny.py), at least 512-deep K slices.
+static bool skinny_use_wide(int M, int N, int a_packed, int wide) {
+  return wide && a_packed && M > 32 && N % 128 == 0;
+}
+
+extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide) {
+  const int tiles = N / (skinny_use_wide(M, N, a_packed, wide) ? 128 : 64);
+  int sp = (256 + tiles / 2) / (tiles > 0 ? tiles : 1);
+  sp = sp < 1 ? 1 : sp;
+  const int cap = K / 512 > 1 ? K / 512 : 1;
+  return sp < cap ? sp : cap;
+}
+
 // rn_ss (optional): per-row partial sums of squares [M][rn_nc] of the un-normalised A rows
 // (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
-                                  int rn_nc, int rn_d, float rn_eps, hipStream_t s) {
+                                  int rn_nc, int rn_d, float rn_eps, int wide, hipStream_t s) {
   if (M <= 0) return 0;
-  if (M > 64 || K % 32 != 0 || S < 1 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
+  if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
+  if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed, wide) : 1;
   const int kc = skinny_kchunk(K, S);
   const int slabs = (K + kc - 1) / kc;
   if (epi != EPI_SLAB && slabs != 1) return -3;
   if ((epi == EPI_SWIGLU || epi == EPI_SWIGLU_PACKED) && nt_tiles != 4) return -4;
+  const float inv_d = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
+  if (skinny_use_wide(M, N, a_packed, wide)) {
+    dim3 grid(N / 128, slabs), blk(256);
+#define K8S_WIDE(EPV)                                                                                      \
+  hipLaunchKernelGGL((gemm_skinny_wide_kernel<EPV>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+                     partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps)
+    switch (epi) {
+      case EPI_SLAB: K8S_WIDE(EPI_SLAB); break;
+      case EPI_BF16: K8S_WIDE(EPI_BF16); break;
+      case EPI_SWIGLU: K8S_WIDE(EPI_SWIGLU); break;
+      default: K8S_WIDE(EPI_SWIGLU_PACKED); break;
+    }
+#undef K8S_WIDE
+    return (int)hipGetLastError();
+  }
   dim3 grid(N / (16 * nt_tiles), slabs), blk(256);
   const int MT = (M + 15) / 16;
 #define K8S_SK(MTV, NTV, EPV, APKV)                                                                            \
   hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc,                  \
-                     rn_d > 0 ? 1.f / (float)rn_d : 0.f, rn_eps)
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps)
 #define K8S_SK_M(NTV, EPV, NTLV)             \
   switch (MT) {                              \
     case 1: K8S_SK(1, NTV, EPV, NTLV); break; \

@@ -16,15 +16,15 @@ def test_pack_roundtrip_and_fragment_order():
 
 
 def test_interleave_gate_up():
-    F, K = 64, 32
+    F, K = 128, 32
     g = torch.full((F, K), 1.0)
     u = torch.full((F, K), 2.0)
     g[:, 0] = torch.arange(F)
     u[:, 0] = torch.arange(F)
     w = ops.interleave_gate_up(torch.cat([g, u]))
-    # tile t (64 rows) = gate rows 32t..32t+31 then up rows 32t..32t+31
-    assert torch.equal(w[:32, 1], torch.ones(32)) and torch.equal(w[32:64, 1], torch.full((32,), 2.0))
-    assert torch.equal(w[64:96, 0], torch.arange(32, 64, dtype=torch.float32))
+    # tile t (128 rows) = gate rows 64t..64t+63 then up rows 64t..64t+63
+    assert torch.equal(w[:64, 1], torch.ones(64)) and torch.equal(w[64:128, 1], torch.full((64,), 2.0))
+    assert torch.equal(w[128:192, 0], torch.arange(64, 128, dtype=torch.float32))
 
 
 def test_skinny_splits_bounds(monkeypatch):
@@ -46,6 +46,9 @@ def test_decode_skinny_path_matches_generic_cpu(monkeypatch):
     cfg = get_config("llama-tiny-d128")
     m = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
     assert m._skinny_ws is not None and m._split_d == 3
+    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "0")
+    m0 = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
+    assert m0._split_d == 0  # automatic split-K per call
     B, bs, nb = 3, 16, 8
     g = torch.Generator().manual_seed(0)
     kv = [(torch.randn(nb, m.hkv, m.D // 8, bs, 8, generator=g), torch.randn(nb, m.hkv, m.D, bs, generator=g))
