@@ -348,3 +348,21 @@ def test_deferred_rmsnorm_chain(M):
     ws = ops.skinny_workspace(M, N, 4, DEV)
     ns = ops.skinny_slabs(xw, ops.pack_skinny(w), ws, 4, rows=M, rownorm=(ss, 1e-5))
     _close(ops.reduce_slabs(ws, ns, M, N).cpu(), y_ref, atol=3e-2, rtol=3e-2, what="deferred-norm slabs")
+
+
+@pytest.mark.parametrize("M", [33, 64])
+def test_gemm_skinny_wide_variant(M, monkeypatch):
+    """The opt-in wide kernel (waves split M, LDS-staged weights): slabs and packed SwiGLU."""
+    monkeypatch.setenv("K8SLLM_SKINNY_WIDE", "1")
+    K, N, F = 1024, 384, 320
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    ap = ops.pack_activation(a)
+    ws = ops.skinny_workspace(M, N, 8, DEV)
+    ns = ops.skinny_slabs(ap, ops.pack_skinny(w), ws, 0, rows=M)
+    _close(ops.reduce_slabs(ws, ns, M, N).cpu(), torch.nn.functional.linear(a.cpu().float(), w.cpu().float()),
+           atol=3e-2, rtol=2e-2, what="wide slabs")
+    w13 = (torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
+    actp = ops.skinny_swiglu(ap, ops.pack_skinny(ops.interleave_gate_up(w13)), rows=M, packed_out=True)
+    gu = torch.nn.functional.linear(a.cpu().float(), w13.cpu().float()).to(torch.bfloat16)
+    _close(ops.unpack_skinny(actp)[:M].cpu(), ref.silu_mul(gu), atol=3e-2, rtol=2e-2, what="wide swiglu")
