@@ -469,8 +469,14 @@ def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128) -> tuple[list[i
 
 def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
                   qblocks: Optional[tuple[torch.Tensor, torch.Tensor]] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, paged: Optional[tuple] = None) -> torch.Tensor:
+    """Causal varlen attention of the prefill rows.  ``paged = (ctx_start, k_cache, v_cache,
+    block_tables)``: each sequence's rows are its NEW tokens at positions ctx_start.. and the
+    keys/values (cached prefix + new) are read from the paged cache."""
     if not _gpu(qkv):
+        if paged is not None:
+            cs, kc, vc, bt = paged
+            return ref.paged_prefill(qkv, cu_seqlens, cs, kc, vc, bt, Hq, Hkv, D, scale)
         return ref.flash_prefill(qkv, cu_seqlens, Hq, Hkv, D, scale)
     if qblocks is None:
         qs, st = prefill_qblocks(cu_seqlens.tolist())
@@ -478,7 +484,12 @@ def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int
                    torch.tensor(st, dtype=torch.int32, device=qkv.device))
     if out is None:
         out = torch.empty(qkv.shape[0], Hq * D, dtype=qkv.dtype, device=qkv.device)
-    native().flash_prefill(out, qkv, cu_seqlens, qblocks[0], qblocks[1], Hq, Hkv, D, scale)
+    if paged is not None:
+        cs, kc, vc, bt = paged
+        native().flash_prefill(out, qkv, cu_seqlens, qblocks[0], qblocks[1], Hq, Hkv, D, scale, cs, kc, vc, bt)
+    else:
+        native().flash_prefill(out, qkv, cu_seqlens, qblocks[0], qblocks[1], Hq, Hkv, D, scale, None, None, None,
+                               None)
     return out
 
 

@@ -22,7 +22,8 @@ int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
 int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride, const int* cu_seqlens,
                          const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
-                         hipStream_t s);
+                         const int* ctx_start, const void* k_cache, const void* v_cache, const int* block_tables,
+                         int bt_stride, hipStream_t s);
 int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V, const float* temps,
                   const int* top_k, const float* top_p, const int64_t* rng, float* pv, int* pi, hipStream_t s);
 int k8sllm_sample_parts(long B, int V);
@@ -173,15 +174,39 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
         "paged_decode");
 }
 
+// paged (optional, all or none): ctx_start [S] (cached tokens before each sequence's new rows),
+// k_cache / v_cache (already holding the new tokens), block_tables [S, W] -> attention over the
+// whole context from the paged cache (prefix caching / chunked prefill).
 void flash_prefill(torch::Tensor out, torch::Tensor qkv, torch::Tensor cu_seqlens, torch::Tensor qb_seq,
-                   torch::Tensor qb_start, int64_t Hq, int64_t Hkv, int64_t D, double scale) {
+                   torch::Tensor qb_start, int64_t Hq, int64_t Hkv, int64_t D, double scale,
+                   c10::optional<torch::Tensor> ctx_start, c10::optional<torch::Tensor> k_cache,
+                   c10::optional<torch::Tensor> v_cache, c10::optional<torch::Tensor> block_tables) {
   dev_bf16(out, "out"); dev_bf16(qkv, "qkv");
   dev_i32(cu_seqlens, "cu_seqlens"); dev_i32(qb_seq, "qb_seq"); dev_i32(qb_start, "qb_start");
   TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv rows");
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [T, Hq*D]");
+  const int* cs = nullptr;
+  const void *kc = nullptr, *vc = nullptr;
+  const int* bt = nullptr;
+  int bts = 0;
+  if (ctx_start.has_value()) {
+    TORCH_CHECK(k_cache.has_value() && v_cache.has_value() && block_tables.has_value(), "paged prefill needs caches");
+    dev_i32(*ctx_start, "ctx_start"); dev_i32(*block_tables, "block_tables");
+    dev_bf16(*k_cache, "k_cache"); dev_bf16(*v_cache, "v_cache");
+    TORCH_CHECK(k_cache->dim() == 5 && k_cache->size(1) == Hkv && k_cache->size(3) == 16 && k_cache->size(4) == 8,
+                "k_cache layout [NB, Hkv, D/8, 16, 8]");
+    TORCH_CHECK(v_cache->dim() == 4 && v_cache->size(1) == Hkv && v_cache->size(2) == D && v_cache->size(3) == 16,
+                "v_cache layout [NB, Hkv, D, 16]");
+    TORCH_CHECK(block_tables->dim() == 2 && block_tables->size(0) == cu_seqlens.numel() - 1, "block_tables [S, W]");
+    cs = ctx_start->data_ptr<int>();
+    kc = k_cache->data_ptr();
+    vc = v_cache->data_ptr();
+    bt = block_tables->data_ptr<int>();
+    bts = (int)block_tables->stride(0);
+  }
   check(k8sllm_flash_prefill(out.data_ptr(), out.stride(0), qkv.data_ptr(), qkv.stride(0), cu_seqlens.data_ptr<int>(),
                              qb_seq.data_ptr<int>(), qb_start.data_ptr<int>(), (int)qb_seq.numel(), (int)Hq, (int)Hkv,
-                             (int)D, (float)scale, cur()),
+                             (int)D, (float)scale, cs, kc, vc, bt, bts, cur()),
         "flash_prefill");
 }
 

@@ -9,19 +9,30 @@
 // With the query on the MFMA column (= lane), the online-softmax statistics (m, l) and the
 // rescale of O are lane-local: no cross-lane traffic except one xor-32 per reduction.
 // The score accumulator is converted to bf16 and consumed as the PV B operand in place.
+//
+// PAGED variant (prefix caching / chunked prefill): the queries are the NEW tokens of each
+// sequence (rows of the qkv buffer), but keys and values come from the paged KV cache (which
+// rope_and_cache has already extended with the new tokens), covering positions [0, ctx_start +
+// new): the cached prefix is attended without being recomputed.  Only the tile staging and the
+// causal offsets differ: K pieces are 16-byte [D/8][16][8] cache rows; V is stored d-major
+// ([D][16] per block), so each 16-byte load (8 tokens of one dim) is scattered into the
+// token-major LDS tile with 2-byte writes.
 #include "common.h"
 
 namespace k8sllm {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-template <int D>
+template <int D, bool PAGED>
 __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restrict__ out, long out_stride,
                                                                const bf16_t* __restrict__ qkv, long qkv_stride,
                                                                const int* __restrict__ cu_seqlens,
                                                                const int* __restrict__ qb_seq,
                                                                const int* __restrict__ qb_start, int Hq, int Hkv,
-                                                               float scale_log2) {
+                                                               float scale_log2, const int* __restrict__ ctx_start,
+                                                               const bf16_t* __restrict__ k_cache,
+                                                               const bf16_t* __restrict__ v_cache,
+                                                               const int* __restrict__ block_tables, int bt_stride) {
   static_assert(D == 128, "prefill kernel is specialised for head_dim 128");
   constexpr int KS = D / 16;  // 8 k-steps over the head dim
   constexpr int DT = D / 32;  // 4 output tiles of 32 dims
@@ -36,7 +47,10 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
   const int seq = qb_seq[qb];
   const int qs = qb_start[qb];
   const int s0 = cu_seqlens[seq];
-  const int L = cu_seqlens[seq + 1] - s0;
+  const int L = cu_seqlens[seq + 1] - s0;  // query rows (new tokens)
+  const int cst = PAGED ? ctx_start[seq] : 0;  // absolute position of query row 0
+  const int LK = cst + L;                      // keys: positions [0, LK)
+  const int* bt = PAGED ? block_tables + (long)seq * bt_stride : nullptr;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, hh = lane >> 5;
   const int myq = qs + wave * 32 + r32;
@@ -60,26 +74,60 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float m = -1e30f, l = 0.f;
 
-  const int wave_q0 = qs + wave * 32;
-  const int kv_end = min(L, qs + 128);
+  const int wave_q0 = cst + qs + wave * 32;  // absolute position of the wave's first query
+  const int kv_end = min(LK, cst + qs + 128);
   // per-lane constants of the transposed V read (see header): group g = lane>>4
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
   const int vcol_base = 16 * ((lane >> 4) & 1) + 4 * p4;
 
   for (int k0 = 0; k0 < kv_end; k0 += 64) {
     __syncthreads();
+    if constexpr (!PAGED) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c / CH, ch = c % CH;
-      const int kr = k0 + r;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (kr < L) {
-        kv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + koff + ch * 8);
-        vv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + voff + ch * 8);
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i;
+        const int r = c / CH, ch = c % CH;
+        const int kr = k0 + r;
+        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+        if (kr < L) {
+          kv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + koff + ch * 8);
+          vv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + voff + ch * 8);
+        }
+        *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
+        *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
       }
-      *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
-      *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
+    } else {
+      // K: key row r, 16-byte piece ch = cache row [blk][kvh][ch][off][0:8]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i;
+        const int r = c / CH, ch = c % CH;
+        const int kr = k0 + r;
+        uint4 kv = make_uint4(0, 0, 0, 0);
+        if (kr < LK) {
+          const long blk = bt[kr >> 4];
+          kv = *reinterpret_cast<const uint4*>(k_cache + (((blk * Hkv + kvh) * CH + ch) * 16 + (kr & 15)) * 8);
+        }
+        *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
+      }
+      // V: dim d, 8 consecutive keys (one 16-byte cache row piece) -> 8 rows of the LDS tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i;
+        const int d = c >> 3, tg = c & 7;
+        const int kr0 = k0 + tg * 8;
+        uint4 vv = make_uint4(0, 0, 0, 0);
+        if (kr0 < LK) {
+          const long blk = bt[kr0 >> 4];
+          vv = *reinterpret_cast<const uint4*>(v_cache + ((blk * Hkv + kvh) * D + d) * 16 + (kr0 & 15));
+        }
+        const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = tg * 8 + j;
+          Vs[(r * CH + ((d >> 3) ^ ((r & 3) << 2))) * 8 + (d & 7)] = (bf16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xffff));
+        }
+      }
     }
     __syncthreads();
     if (k0 > wave_q0 + 31) continue;  // every key of this tile is in the future of every row of this wave
@@ -98,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
       }
     }
 
-    const bool need_mask = (k0 + 63 > wave_q0) || (k0 + 64 > L);
+    const bool need_mask = (k0 + 63 > wave_q0) || (k0 + 64 > LK);
     float mx = -1e30f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -107,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
         float v = sacc[i][r] * scale_log2;
         if (need_mask) {
           const int kv = k0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (kv > myq || kv >= L) v = -1e30f;
+          if (kv > cst + myq || kv >= LK) v = -1e30f;
         }
         sacc[i][r] = v;
         mx = fmaxf(mx, v);
@@ -180,11 +228,19 @@ using namespace k8sllm;
 
 extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride,
                                     const int* cu_seqlens, const int* qb_seq, const int* qb_start, int n_qblocks,
-                                    int Hq, int Hkv, int D, float scale, hipStream_t s) {
+                                    int Hq, int Hkv, int D, float scale, const int* ctx_start, const void* k_cache,
+                                    const void* v_cache, const int* block_tables, int bt_stride, hipStream_t s) {
   if (n_qblocks <= 0) return 0;
   if (D != 128 || Hq % Hkv != 0) return -1;
-  hipLaunchKernelGGL((flash_prefill_kernel<128>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out, out_stride,
-                     (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv,
-                     scale * 1.4426950408889634f);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (ctx_start != nullptr) {
+    hipLaunchKernelGGL((flash_prefill_kernel<128, true>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out,
+                       out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,
+                       ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride);
+  } else {
+    hipLaunchKernelGGL((flash_prefill_kernel<128, false>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out,
+                       out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,
+                       nullptr, nullptr, nullptr, nullptr, 0);
+  }
   return (int)hipGetLastError();
 }

@@ -166,6 +166,22 @@ def flash_prefill(qkv, cu_seqlens, Hq, Hkv, D, scale):
     return out
 
 
+def paged_prefill(qkv, cu_seqlens, ctx_start, k_cache, v_cache, block_tables, Hq, Hkv, D, scale):
+    """Queries = each sequence's new rows of ``qkv``; keys/values = positions [0, ctx_start + new)
+    from the paged cache (which already holds the new tokens)."""
+    T = qkv.shape[0]
+    out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    cu, cs = cu_seqlens.tolist(), ctx_start.tolist()
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if b <= a:
+            continue
+        k, v = gather_kv(k_cache, v_cache, block_tables[i], cs[i] + b - a)
+        q = qkv[a:b, : Hq * D].view(b - a, Hq, D)
+        out[a:b] = attention(q, k, v, scale, causal=True).reshape(b - a, -1).to(qkv.dtype)
+    return out
+
+
 def greedy(logits: torch.Tensor) -> torch.Tensor:
     return logits.float().argmax(-1).to(torch.int32)
 

@@ -366,3 +366,29 @@ def test_gemm_skinny_wide_variant(M, monkeypatch):
     actp = ops.skinny_swiglu(ap, ops.pack_skinny(ops.interleave_gate_up(w13)), rows=M, packed_out=True)
     gu = torch.nn.functional.linear(a.cpu().float(), w13.cpu().float()).to(torch.bfloat16)
     _close(ops.unpack_skinny(actp)[:M].cpu(), ref.silu_mul(gu), atol=3e-2, rtol=2e-2, what="wide swiglu")
+
+
+@pytest.mark.parametrize("cached,new", [([0, 32], [40, 7]), ([48, 160, 16], [1, 130, 64]), ([1008], [300])])
+def test_flash_prefill_paged(cached, new):
+    """Prefill of new tokens attending a cached prefix in the paged cache == the fp32 reference."""
+    hq, hkv, D, bs = 32, 8, 128, 16
+    S = len(new)
+    tot = [c + n for c, n in zip(cached, new)]
+    nblk = [(t + bs - 1) // bs for t in tot]
+    NB = sum(nblk) + 3
+    kc = torch.randn(NB, hkv, D // 8, bs, 8, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(NB, hkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    perm = torch.randperm(NB, device=DEV).to(torch.int32)
+    W = max(nblk)
+    bt = torch.zeros(S, W, dtype=torch.int32, device=DEV)
+    o = 0
+    for i, n in enumerate(nblk):
+        bt[i, :n] = perm[o:o + n]
+        o += n
+    T = sum(new)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(new).cumsum(0).tolist()), dtype=torch.int32, device=DEV)
+    cs = torch.tensor(cached, dtype=torch.int32, device=DEV)
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
+    _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what="paged prefill")
