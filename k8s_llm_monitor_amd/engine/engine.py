@@ -48,6 +48,8 @@ class EngineConfig:
     seed: int = 0
     tp_size: int = 1
     pipeline: bool = True  # overlap the host's per-step work with the GPU's decode step
+    # reuse KV blocks of identical prompt prefixes (block_manager.py); K8SLLM_PREFIX_CACHE=0 disables
+    prefix_caching: bool = field(default_factory=lambda: os.environ.get("K8SLLM_PREFIX_CACHE", "1") != "0")
     dtype: str = "bfloat16"  # compute / weight dtype ("float32" for CPU parity tests)
     model_overrides: dict = field(default_factory=dict)
 
@@ -55,11 +57,11 @@ class EngineConfig:
 class _View:
     """What the runner needs of a sequence; built on non-leader TP ranks from the broadcast."""
 
-    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params")
+    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params", "num_cached")
 
-    def __init__(self, all_ids, num_tokens, block_table, last_token, params):
+    def __init__(self, all_ids, num_tokens, block_table, last_token, params, num_cached=0):
         self.all_ids, self.num_tokens, self.block_table = all_ids, num_tokens, block_table
-        self.last_token, self.params = last_token, params
+        self.last_token, self.params, self.num_cached = last_token, params, num_cached
 
 
 class LLMEngine:
@@ -80,7 +82,7 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, RunnerConfig(
             max_num_seqs=cfg.max_num_seqs, max_model_len=cfg.max_model_len, kv_cache_gb=cfg.kv_cache_gb,
             num_blocks=cfg.num_blocks, use_graphs=cfg.use_graphs, seed=cfg.seed))
-        self.blocks = BlockManager(self.runner.num_blocks)
+        self.blocks = BlockManager(self.runner.num_blocks, prefix_caching=cfg.prefix_caching)
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
                                                max_prefill_tokens=cfg.max_prefill_tokens,
                                                max_model_len=self.runner.max_len), self.blocks)
@@ -277,7 +279,7 @@ class LLMEngine:
     @staticmethod
     def _pack(plan) -> tuple:
         if plan.is_prefill:
-            return (True, [(s.all_ids, s.block_table, _params_t(s.params)) for s in plan.seqs])
+            return (True, [(s.all_ids, s.block_table, _params_t(s.params), s.num_cached) for s in plan.seqs])
         return (False, [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.seqs])
 
     def worker_loop(self) -> None:
@@ -292,7 +294,7 @@ class LLMEngine:
                 if pending is not None:
                     self.runner.decode_collect(pending)
                     pending = None
-                views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p)) for ids, bt, p in items]
+                views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p), nc) for ids, bt, p, nc in items]
                 self.runner.prefill(views)
             else:
                 src = msg[2] if len(msg) > 2 else None

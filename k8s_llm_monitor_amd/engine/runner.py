@@ -100,17 +100,20 @@ class ModelRunner:
 
     # --------------------------------------------------------------------- prefill
     def prefill(self, seqs: list[Sequence]) -> list[int]:
-        """Run whole prompts (prompt + any tokens generated before a preemption); returns the first
-        sampled token of each sequence."""
+        """Run whole prompts (prompt + any tokens generated before a preemption) minus their cached
+        prefix (``seq.num_cached`` tokens whose KV blocks came from the prefix cache); returns
+        the first sampled token of each sequence.  With any cached prefix the attention reads
+        keys/values from the paged cache (paged flash prefill)."""
         dev = self.device
-        lens = [s.num_tokens for s in seqs]
-        ids = np.concatenate([np.asarray(s.all_ids, dtype=np.int32) for s in seqs])
-        pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        starts = [getattr(s, "num_cached", 0) for s in seqs]
+        lens = [s.num_tokens - c for s, c in zip(seqs, starts)]
+        ids = np.concatenate([np.asarray(s.all_ids[c:], dtype=np.int32) for s, c in zip(seqs, starts)])
+        pos = np.concatenate([np.arange(c, c + n, dtype=np.int32) for c, n in zip(starts, lens)])
         slots = np.empty(ids.shape[0], dtype=np.int32)
         o = 0
-        for s, n in zip(seqs, lens):
+        for s, c, n in zip(seqs, starts, lens):
             bt = np.asarray(s.block_table, dtype=np.int64)
-            p = np.arange(n)
+            p = np.arange(c, c + n)
             slots[o:o + n] = bt[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
             o += n
         cu = np.zeros(len(seqs) + 1, dtype=np.int32)
@@ -120,6 +123,14 @@ class ModelRunner:
         meta = AttnMeta(is_prefill=True, positions=t(pos), slot_mapping=t(slots), cu_seqlens=t(cu),
                         qb_seq=t(np.asarray(qs, dtype=np.int32)), qb_start=t(np.asarray(st, dtype=np.int32)),
                         logits_idx=t(cu[1:] - 1, torch.int64))
+        if any(starts):
+            W = max(len(s.block_table) for s in seqs)
+            bt = np.zeros((len(seqs), W), dtype=np.int32)
+            for i, s in enumerate(seqs):
+                bt[i, : len(s.block_table)] = s.block_table
+            meta.ctx_start = t(np.asarray(starts, dtype=np.int32))
+            meta.block_tables = t(bt)
+        self.n_steps["prefill_cached_tokens"] = self.n_steps.get("prefill_cached_tokens", 0) + sum(starts)
         logits = self.model.forward(t(ids), meta, self.kv)
         S = len(seqs)
         temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32).to(dev)

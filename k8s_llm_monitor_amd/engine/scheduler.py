@@ -74,7 +74,7 @@ class Scheduler:
             budget = self.cfg.max_prefill_tokens
             while self.waiting and len(self.running) + len(plan.seqs) < self.cfg.max_num_seqs:
                 seq = self.waiting[0]
-                n = seq.num_tokens
+                n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens this step computes
                 if plan.seqs and n > budget:
                     break
                 if not self.blocks.can_allocate(seq):
@@ -118,13 +118,15 @@ class Scheduler:
         self.blocks.free(seq)
 
     def stats(self) -> dict:
-        return {
+        d = {
             "waiting": len(self.waiting),
             "running": len(self.running),
             "kv_blocks_total": self.blocks.num_blocks,
             "kv_blocks_free": self.blocks.num_free,
             "kv_usage": round(self.blocks.usage(), 4),
         }
+        d.update(self.blocks.stats())
+        return d
 
 
 def next_plan_or_none(s: Scheduler) -> Optional[StepPlan]:

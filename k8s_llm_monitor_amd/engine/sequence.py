@@ -46,6 +46,7 @@ class Sequence:
     t_first_token: Optional[float] = None
     t_finish: Optional[float] = None
     n_preemptions: int = 0
+    num_cached: int = 0  # leading prompt tokens whose KV came from the prefix cache (this admission)
     user: object = None  # opaque payload for the caller (future, callback, ...)
 
     @property

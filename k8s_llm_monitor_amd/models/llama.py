@@ -51,6 +51,7 @@ class AttnMeta:
     qb_seq: Optional[torch.Tensor] = None  # flash_prefill q-block schedule
     qb_start: Optional[torch.Tensor] = None
     logits_idx: Optional[torch.Tensor] = None  # [S] int64 rows that produce logits
+    ctx_start: Optional[torch.Tensor] = None  # [S] int32 cached prefix tokens (paged prefill) or None
     # decode (one token per sequence)
     block_tables: Optional[torch.Tensor] = None  # [B, W] int32
     seq_lens: Optional[torch.Tensor] = None  # [B] int32 (including the token being decoded)
@@ -232,7 +233,11 @@ class CausalLM:
                            apply_rope=c.arch == "llama", partial=partial, nslabs=ns)
         if meta.is_prefill:
             qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
-            o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb)
+            paged = None
+            if meta.ctx_start is not None:  # some prompts start with cached prefix blocks
+                paged = (meta.ctx_start, k_cache, v_cache, meta.block_tables)
+            o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb,
+                                  paged=paged)
         else:
             out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device) if slabs is not None else None
             o = ops.paged_decode(qkv, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.hq, self.hkv,

@@ -21,6 +21,7 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <list>
 
 namespace py = pybind11;
 
@@ -60,6 +61,150 @@ class BlockAllocator {
   int num_blocks_;
   std::vector<int> free_;
   std::vector<uint8_t> used_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// BlockPool - reference-counted KV blocks with a prefix cache.  A full block of prompt tokens is
+// identified by a chained hash (block_hashes: the hash of block i covers tokens [0, 16 (i+1))),
+// so a lookup of a prompt's hash chain finds the longest already-computed prefix.  Blocks whose
+// last reference is dropped stay cached (LRU) until a fresh allocation needs them.
+inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+std::vector<uint64_t> block_hashes(const std::vector<int>& tokens, int block_size, uint64_t seed) {
+  if (block_size <= 0) throw std::invalid_argument("block_size <= 0");
+  std::vector<uint64_t> out;
+  const size_t nfull = tokens.size() / (size_t)block_size;
+  out.reserve(nfull);
+  uint64_t h = splitmix64(seed ^ 0x6b38c1a7d2e5f091ull);
+  for (size_t b = 0; b < nfull; ++b) {
+    uint64_t x = h;
+    for (int i = 0; i < block_size; ++i) x = splitmix64(x ^ (uint64_t)(uint32_t)tokens[b * block_size + i]);
+    h = x ? x : 1;  // 0 is reserved for "no hash"
+    out.push_back(h);
+  }
+  return out;
+}
+
+class BlockPool {
+ public:
+  explicit BlockPool(int num_blocks)
+      : num_blocks_(num_blocks), ref_(num_blocks, 0), hash_(num_blocks, 0), in_lru_(num_blocks, 0),
+        lru_pos_(num_blocks) {
+    if (num_blocks < 0) throw std::invalid_argument("num_blocks < 0");
+    free_.reserve(num_blocks);
+    for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
+  }
+
+  // Number of leading hashes that are cached (no references taken).
+  int peek(const std::vector<uint64_t>& hashes) const {
+    int n = 0;
+    for (uint64_t h : hashes) {
+      if (map_.find(h) == map_.end()) break;
+      ++n;
+    }
+    return n;
+  }
+
+  // Longest cached prefix; takes one reference on every returned block.
+  std::vector<int> match(const std::vector<uint64_t>& hashes) {
+    std::vector<int> out;
+    ++queries_;
+    for (uint64_t h : hashes) {
+      auto it = map_.find(h);
+      if (it == map_.end()) break;
+      const int b = it->second;
+      if (ref_[b] == 0 && in_lru_[b]) {
+        lru_.erase(lru_pos_[b]);
+        in_lru_[b] = 0;
+      }
+      ++ref_[b];
+      out.push_back(b);
+    }
+    hit_blocks_ += out.size();
+    return out;
+  }
+
+  // n fresh blocks (free list first, then the least recently used cached blocks).
+  std::optional<std::vector<int>> allocate(int n) {
+    if (n < 0 || n > (int)(free_.size() + lru_.size())) return std::nullopt;
+    std::vector<int> out(n);
+    for (int i = 0; i < n; ++i) {
+      int b;
+      if (!free_.empty()) {
+        b = free_.back();
+        free_.pop_back();
+      } else {
+        b = lru_.front();
+        lru_.pop_front();
+        in_lru_[b] = 0;
+        map_.erase(hash_[b]);
+        hash_[b] = 0;
+        ++evictions_;
+      }
+      ref_[b] = 1;
+      out[i] = b;
+    }
+    return out;
+  }
+
+  // Register a block whose contents are the prefix with this chained hash.  If another block
+  // already holds it, this one stays anonymous.
+  void publish(int b, uint64_t h) {
+    check(b);
+    if (h == 0 || hash_[b] != 0 || map_.count(h)) return;
+    map_[h] = b;
+    hash_[b] = h;
+  }
+
+  void release(const std::vector<int>& blocks) {
+    for (auto it = blocks.rbegin(); it != blocks.rend(); ++it) {
+      const int b = *it;
+      check(b);
+      if (ref_[b] <= 0) throw std::runtime_error("double free of KV block " + std::to_string(b));
+      if (--ref_[b] == 0) {
+        if (hash_[b] != 0) {
+          lru_.push_back(b);
+          lru_pos_[b] = std::prev(lru_.end());
+          in_lru_[b] = 1;
+        } else {
+          free_.push_back(b);
+        }
+      }
+    }
+  }
+
+  int num_free() const { return (int)(free_.size() + lru_.size()); }
+  int num_blocks() const { return num_blocks_; }
+  int num_cached() const { return (int)map_.size(); }
+  int refcount(int b) const { check(b); return ref_[b]; }
+  py::dict stats() const {
+    py::dict d;
+    d["cached_blocks"] = (int)map_.size();
+    d["evictable_blocks"] = (int)lru_.size();
+    d["hit_blocks"] = hit_blocks_;
+    d["queries"] = queries_;
+    d["evictions"] = evictions_;
+    return d;
+  }
+
+ private:
+  void check(int b) const {
+    if (b < 0 || b >= num_blocks_) throw std::out_of_range("block id out of range");
+  }
+  int num_blocks_;
+  std::vector<int> free_;
+  std::vector<int> ref_;
+  std::vector<uint64_t> hash_;
+  std::vector<uint8_t> in_lru_;
+  std::list<int> lru_;
+  std::vector<std::list<int>::iterator> lru_pos_;
+  std::unordered_map<uint64_t, int> map_;
+  int64_t hit_blocks_ = 0, queries_ = 0, evictions_ = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -276,4 +421,17 @@ PYBIND11_MODULE(_k8sllm_runtime, m) {
       .def("pretokenize", &BPE::pretokenize)
       .def_property_readonly("num_merges", &BPE::num_merges);
   m.def("pack_decode", &pack_decode);
+  py::class_<BlockPool>(m, "BlockPool")
+      .def(py::init<int>())
+      .def("peek", &BlockPool::peek)
+      .def("match", &BlockPool::match)
+      .def("allocate", &BlockPool::allocate)
+      .def("publish", &BlockPool::publish)
+      .def("release", &BlockPool::release)
+      .def("refcount", &BlockPool::refcount)
+      .def("stats", &BlockPool::stats)
+      .def_property_readonly("num_free", &BlockPool::num_free)
+      .def_property_readonly("num_blocks", &BlockPool::num_blocks)
+      .def_property_readonly("num_cached", &BlockPool::num_cached);
+  m.def("block_hashes", &block_hashes, py::arg("tokens"), py::arg("block_size") = 16, py::arg("seed") = 0);
 }

@@ -70,3 +70,24 @@ def test_gpu_graph_replay_equals_eager():
     oa = [s.output_ids for s in a.generate(prompts, p)]
     ob = [s.output_ids for s in b.generate(prompts, p)]
     assert oa == ob
+
+
+def test_prefix_caching_reuses_blocks_and_matches_uncached():
+    """Prompts sharing a long prefix: the second wave maps the cached blocks (paged prefill of the
+    suffix only) and generates exactly what an engine without prefix caching generates."""
+    from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+
+    shared = "集群状态概览: node-000 NotReady, payments-api CrashLoopBackOff, " * 6
+    prompts = [shared + f"问题 {i}: 为什么?" for i in range(3)]
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for pc in (True, False):
+        eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=512, num_blocks=128,
+                                     use_graphs=False, seed=2, prefix_caching=pc, dtype="float32"), device="cpu")
+        first = eng.generate(prompts[:1], sp)  # populates the cache
+        rest = eng.generate(prompts[1:], sp)
+        outs[pc] = [s.output_ids for s in first + rest]
+        if pc:
+            assert eng.blocks.stats()["prefix_cached_tokens"] >= 2 * 16
+            assert all(s.num_cached == 0 for s in rest)  # released at finish
+    assert outs[True] == outs[False]

@@ -4,7 +4,7 @@ import random
 import numpy as np
 import pytest
 
-from k8s_llm_monitor_amd.engine.block_manager import BlockManager, PyBlockAllocator
+from k8s_llm_monitor_amd.engine.block_manager import BlockManager, PyBlockPool, py_block_hashes
 from k8s_llm_monitor_amd.engine.sequence import SamplingParams, Sequence
 from k8s_llm_monitor_amd.engine.tokenizer import ByteBPETokenizer, tokenizer_for, train_bpe
 from k8s_llm_monitor_amd.llm.synthetic import synthetic_cluster_prompt
@@ -17,13 +17,39 @@ needs_rt = pytest.mark.skipif(rt is None, reason="C++ runtime not built")
 
 @needs_rt
 def test_native_allocator_matches_python_and_catches_double_free():
-    a, b = rt.BlockAllocator(16), PyBlockAllocator(16)
+    a, b = rt.BlockAllocator(16), PyBlockPool(16)
     for n in (3, 5, 2):
         assert a.allocate(n) == b.allocate(n)
     assert a.allocate(100) is None and a.num_free == b.num_free == 6
     a.free([0, 1])
     with pytest.raises(RuntimeError, match="double free"):
         a.free([1])
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_block_pool_prefix_cache(native):
+    if native and rt is None:
+        pytest.skip("C++ runtime not built")
+    p = rt.BlockPool(6) if native else PyBlockPool(6)
+    hashes = rt.block_hashes if native else py_block_hashes
+    toks = list(range(40))
+    h = hashes(toks, 16, 0)
+    assert len(h) == 2 and h == py_block_hashes(toks, 16, 0)  # native and Python chains agree
+    assert hashes(toks[:16] + [99] * 16, 16, 0)[0] == h[0] != hashes(toks[:16] + [99] * 16, 16, 0)[1]
+    b = p.allocate(3)
+    for blk, hh in zip(b, h):
+        p.publish(blk, hh)
+    assert p.peek(h) == 2 and p.num_cached == 2
+    m = p.match(h)  # second reference on the two prefix blocks
+    assert m == b[:2] and p.refcount(b[0]) == 2
+    p.release(b)
+    assert p.num_free == 4 and p.refcount(b[0]) == 1
+    p.release(m)  # last references: the prefix blocks stay cached but are evictable
+    assert p.num_free == 6 and p.num_cached == 2
+    got = p.allocate(5)  # 4 plain free + 1 eviction (least recently used cached block)
+    assert len(got) == 5 and p.num_cached == 1 and p.stats()["evictions"] == 1
+    with pytest.raises(RuntimeError, match="double free"):
+        p.release([b[2]]) if b[2] not in got else p.release([got[0], got[0]])
 
 
 def test_block_manager_slots():
@@ -34,6 +60,26 @@ def test_block_manager_slots():
     assert bm.ensure_slot(s) and len(s.block_table) == 3
     bm.free(s)
     assert bm.num_free == 8
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_block_manager_prefix_sharing(native):
+    if native and rt is None:
+        pytest.skip("C++ runtime not built")
+    bm = BlockManager(32, use_native=native)
+    a = Sequence(prompt_ids=list(range(50)), params=SamplingParams())
+    b = Sequence(prompt_ids=list(range(40)) + [7] * 5, params=SamplingParams())
+    c = Sequence(prompt_ids=list(range(32)), params=SamplingParams())  # exactly 2 full blocks
+    assert bm.allocate(a) and a.num_cached == 0
+    assert bm.cached_prefix_tokens(b) == 32 and bm.allocate(b) and b.num_cached == 32
+    assert b.block_table[:2] == a.block_table[:2] and b.block_table[2] != a.block_table[2]
+    # a fully cached prompt still runs its last token: only the first block is reused
+    assert bm.allocate(c) and c.num_cached == 16
+    bm.free(a)
+    bm.free(b)
+    bm.free(c)
+    assert bm.num_free == 32
+    assert bm.stats()["prefix_cached_tokens"] == 48
 
 
 @needs_rt
