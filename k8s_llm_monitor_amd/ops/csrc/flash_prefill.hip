@@ -14,9 +14,8 @@
 // sequence (rows of the qkv buffer), but keys and values come from the paged KV cache (which
 // rope_and_cache has already extended with the new tokens), covering positions [0, ctx_start +
 // new): the cached prefix is attended without being recomputed.  Only the tile staging and the
-// causal offsets differ: K pieces are 16-byte [D/8][16][8] cache rows; V is stored d-major
-// ([D][16] per block), so each 16-byte load (8 tokens of one dim) is scattered into the
-// token-major LDS tile with 2-byte writes.
+// causal offsets differ: keys of the new tokens stage from the qkv rows exactly as in the plain
+// kernel; only cached keys (position < ctx_start) are read from the paged cache.
 #include "common.h"
 
 namespace k8sllm {
@@ -97,36 +96,30 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
         *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
       }
     } else {
-      // K: key row r, 16-byte piece ch = cache row [blk][kvh][ch][off][0:8]
+      // keys of the new tokens come from this step's qkv rows (16-byte loads, as above); only the
+      // cached prefix [0, cst) is read from the paged cache: K as 16-byte [D/8][16][8] pieces, V
+      // (d-major [D][16] per block) gathered 8 dims x 2 bytes - a handful of tiles per sequence
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = tid + 256 * i;
         const int r = c / CH, ch = c % CH;
         const int kr = k0 + r;
-        uint4 kv = make_uint4(0, 0, 0, 0);
-        if (kr < LK) {
+        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+        if (kr >= cst && kr < LK) {
+          const bf16_t* row = base + (long)(kr - cst) * qkv_stride;
+          kv = *reinterpret_cast<const uint4*>(row + koff + ch * 8);
+          vv = *reinterpret_cast<const uint4*>(row + voff + ch * 8);
+        } else if (kr < cst) {
           const long blk = bt[kr >> 4];
           kv = *reinterpret_cast<const uint4*>(k_cache + (((blk * Hkv + kvh) * CH + ch) * 16 + (kr & 15)) * 8);
+          const bf16_t* vp = v_cache + ((blk * Hkv + kvh) * D + ch * 8) * 16 + (kr & 15);
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = (uint32_t)vp[(2 * j) * 16] | ((uint32_t)vp[(2 * j + 1) * 16] << 16);
+          vv = make_uint4(w[0], w[1], w[2], w[3]);
         }
         *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
-      }
-      // V: dim d, 8 consecutive keys (one 16-byte cache row piece) -> 8 rows of the LDS tile
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + 256 * i;
-        const int d = c >> 3, tg = c & 7;
-        const int kr0 = k0 + tg * 8;
-        uint4 vv = make_uint4(0, 0, 0, 0);
-        if (kr0 < LK) {
-          const long blk = bt[kr0 >> 4];
-          vv = *reinterpret_cast<const uint4*>(v_cache + ((blk * Hkv + kvh) * D + d) * 16 + (kr0 & 15));
-        }
-        const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = tg * 8 + j;
-          Vs[(r * CH + ((d >> 3) ^ ((r & 3) << 2))) * 8 + (d & 7)] = (bf16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xffff));
-        }
+        *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
       }
     }
     __syncthreads();

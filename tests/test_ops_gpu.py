@@ -389,6 +389,11 @@ def test_flash_prefill_paged(cached, new):
     qkv = torch.randn(T, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16)
     cu = torch.tensor([0] + list(torch.tensor(new).cumsum(0).tolist()), dtype=torch.int32, device=DEV)
     cs = torch.tensor(cached, dtype=torch.int32, device=DEV)
+    # as in the engine, the new tokens' K/V are in the cache too (rope_and_cache ran first)
+    pos = torch.cat([torch.arange(c, c + n) for c, n in zip(cached, new)]).to(DEV, torch.int32)
+    seq_of = torch.cat([torch.full((n,), i) for i, n in enumerate(new)]).to(DEV)
+    slots = (bt[seq_of, (pos // bs).long()] * bs + pos % bs).to(torch.int32)
+    ops.rope_and_cache(qkv, pos, torch.zeros(1, D, device=DEV), kc, vc, slots, hq, hkv, D, apply_rope=False)
     out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
     exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
     _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what="paged prefill")
