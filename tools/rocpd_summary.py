@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""Summarise a rocprofv3 ``--kernel-trace`` SQLite database (``*_results.db``) as a markdown
+table: per-kernel total / calls / average, sorted by total time.
+
+    python tools/rocpd_summary.py gpurun_out/prof1/run_results.db [--top 30] [--title "..."]
+"""
+from __future__ import annotations
+
+import argparse
+import sqlite3
+
+
+def summarise(db: str, top: int = 30) -> tuple[list[tuple], float]:
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select name, count(*), sum(duration), avg(duration), max(grid_x*grid_y*grid_z/"
+        "(workgroup_x*workgroup_y*workgroup_z)), max(lds_size), max(vgpr_count), max(accum_vgpr_count) "
+        "from kernels group by name order by sum(duration) desc").fetchall()
+    total = sum(r[2] for r in rows)
+    return rows[:top], total
+
+
+def short(name: str, n: int = 90) -> str:
+    name = name.replace("|", "/")
+    return name if len(name) <= n else name[: n - 3] + "..."
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    rows, total = summarise(a.db, a.top)
+    if a.title:
+        print(f"# {a.title}\n")
+    print(f"GPU kernel time total: {total / 1e6:.1f} ms\n")
+    print("| total ms | % | calls | avg us | WGs | LDS B | VGPR | AGPR | kernel |")
+    print("|---|---|---|---|---|---|---|---|---|")
+    for name, calls, tot, avg, wgs, lds, vgpr, agpr in rows:
+        print(f"| {tot / 1e6:.1f} | {100 * tot / total:.2f} | {calls} | {avg / 1e3:.1f} | {wgs} | {lds} | {vgpr} | "
+              f"{agpr} | `{short(name)}` |")
+
+
+if __name__ == "__main__":
+    main()
