@@ -176,17 +176,27 @@ def _rn_scale(rownorm, M: int, K: int) -> Optional[torch.Tensor]:
     return torch.rsqrt(ss[:M].float().sum(1, keepdim=True) / K + eps)
 
 
+def skinny_waves() -> int:
+    """Waves per gemm_skinny workgroup: 0 = the launcher's choice (8 for split-K slabs, 4 for the
+    single-slice epilogues); ``K8SLLM_SKINNY_WAVES`` = 4 or 8 forces one."""
+    return int(os.environ.get("K8SLLM_SKINNY_WAVES", "0"))
+
+
 def _rn_args(rownorm) -> tuple:
     wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1"  # opt-in: measured slower (gemm_skinny.hip)
-    return (None, 0.0, wide) if rownorm is None else (rownorm[0], float(rownorm[1]), wide)
+    return ((None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))) + (wide, skinny_waves())
 
 
 def skinny_auto_splits(M: int, N: int, K: int, packed: bool = True) -> int:
-    """Mirror of k8sllm_gemm_skinny_auto_splits: ~one workgroup per CU for the kernel the launcher
-    picks (wide: 128 columns per workgroup for packed A with 32 < M <= 64; narrow: 64)."""
+    """Mirror of k8sllm_gemm_skinny_auto_splits: the largest power-of-two split that keeps the grid
+    within one workgroup per CU (wide kernel: 128 columns per workgroup for packed A with
+    32 < M <= 64; narrow: 64), K slices >= 512 deep and whole 256-deep rounds of the waves."""
     wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1" and packed and M > 32 and N % 128 == 0
     tiles = max(1, N // (128 if wide else 64))
-    return max(1, min(max(1, K // 512), (256 + tiles // 2) // tiles))
+    sp = 1
+    while sp < 16 and tiles * sp * 2 <= 256 and K // (sp * 2) >= 512 and K % (sp * 2 * 256) == 0:
+        sp *= 2
+    return sp
 
 
 def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -36,7 +36,7 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
-                       float rn_eps, int wide, hipStream_t s);
+                       float rn_eps, int wide, int waves, hipStream_t s);
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
@@ -279,7 +279,7 @@ void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t 
 // number of slabs written (1 for epi 1/2).
 int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
                     c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows,
-                    c10::optional<torch::Tensor> rn_ss, double rn_eps, bool wide) {
+                    c10::optional<torch::Tensor> rn_ss, double rn_eps, bool wide, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
               "gemm_skinny: wp must be fragment-packed [N/16, K/32, 64, 8]");
@@ -336,7 +336,7 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   }
   check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
                            epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, rp, rn_nc, K,
-                           (float)rn_eps, wide ? 1 : 0, cur()),
+                           (float)rn_eps, wide ? 1 : 0, (int)waves, cur()),
         "gemm_skinny");
   return S;
 }

@@ -54,15 +54,15 @@ struct SkinnyBatch {
   bf16x8 a[U][MT];
 };
 
-template <int MT, int NT, int EPI, bool APK>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
+template <int MT, int NT, int EPI, bool APK, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
                                                           int kchunk, const float* __restrict__ rn_ss, int rn_nc,
                                                           float rn_inv_d, float rn_eps) {
   // U k-steps per wave group; two groups in flight per wave (register double buffer)
   constexpr int U = MT <= 2 ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) float red[4][NT][64][4];  // one m-tile at a time: 16 KiB at NT 4
+  __shared__ __attribute__((aligned(16))) float red[WAVES][NT][64][4];  // one m-tile at a time: 16 KiB per 4 waves
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ntile0 = blockIdx.x * NT;
   const int s = blockIdx.y;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 
   // software pipeline: the next group's loads are issued before this group's MFMAs, so every
   // wave keeps two groups of weight lines in flight instead of stalling once per group
-  constexpr int STRIDE = 4 * U;
+  constexpr int STRIDE = WAVES * U;
   int i0 = wave * U;
   if (i0 < nsteps) {
     SkinnyBatch<U, MT, NT> b0, b1;
@@ -158,11 +158,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(&red[wave][nt][lane][0]) = acc[mt][nt];
     __syncthreads();
-    for (int idx = threadIdx.x; idx < NOUT * 64; idx += 256) {
+    for (int idx = threadIdx.x; idx < NOUT * 64; idx += 64 * WAVES) {
       const int nt = idx >> 6, l = idx & 63;
       f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][nt][l][0]);
 #pragma unroll
-      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
+      for (int w = 1; w < WAVES; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
       // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms
       // (s_inv, computed at kernel start) is applied here - linear, so exact for split-K slabs too
       f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
       if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
         f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][nt + NT / 2][l][0]);
 #pragma unroll
-        for (int w = 1; w < 4; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
+        for (int w = 1; w < WAVES; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
         u *= rs;
         // gate n-tiles 8q + 2h + {0,1} pair with up n-tiles 8q + 4 + 2h + {0,1} (swiglu_tile)
         const int f = (blockIdx.x >> 1) * 64 + (blockIdx.x & 1) * 32 + nt * 16 + (l & 15);
@@ -482,25 +482,27 @@ extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
 // epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; a_packed: A in the
 // fragment-packed layout (lda ignored)
 // Kernel choice: the wide kernel for fragment-packed A with 32 < M <= 64 and N % 128 == 0
-// (unless disabled), else the narrow one.  splits <= 0: automatic split-K, about one workgroup per
-// CU (tools/bench_skinny.py), at least 512-deep K slices.
+// (unless disabled), else the narrow one.  splits <= 0: automatic split-K - the largest power of
+// two that keeps the grid within one workgroup per CU, K slices >= 512 deep and whole 256-deep
+// rounds of the 4 waves (uneven rounds leave waves idle at the tail).  Measured at M = 64
+// (tools/bench_skinny_waves.py, profiles/r01_s3_skinny_waves.jsonl): qkv S 2 14.9 us vs S 3
+// 18.1 us; o / down S 4 beat 2, 3, 6 and 8.
 static bool skinny_use_wide(int M, int N, int a_packed, int wide) {
   return wide && a_packed && M > 32 && N % 128 == 0;
 }
 
 extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide) {
   const int tiles = N / (skinny_use_wide(M, N, a_packed, wide) ? 128 : 64);
-  int sp = (256 + tiles / 2) / (tiles > 0 ? tiles : 1);
-  sp = sp < 1 ? 1 : sp;
-  const int cap = K / 512 > 1 ? K / 512 : 1;
-  return sp < cap ? sp : cap;
+  int sp = 1;
+  while (sp < 16 && (long)tiles * sp * 2 <= 256 && K / (sp * 2) >= 512 && K % (sp * 2 * 256) == 0) sp *= 2;
+  return sp;
 }
 
 // rn_ss (optional): per-row partial sums of squares [M][rn_nc] of the un-normalised A rows
 // (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
-                                  int rn_nc, int rn_d, float rn_eps, int wide, hipStream_t s) {
+                                  int rn_nc, int rn_d, float rn_eps, int wide, int waves, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed, wide) : 1;
@@ -523,17 +525,24 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
 #undef K8S_WIDE
     return (int)hipGetLastError();
   }
-  dim3 grid(N / (16 * nt_tiles), slabs), blk(256);
+  // 8-wave workgroups: twice the weight lines in flight per CU for the same K slice.  waves <= 0
+  // (auto): 8 for the split-K slab projections (o 11.1 vs 11.8 us, down 24.3 vs 25.9 at M = 64),
+  // 4 for the single-slice SwiGLU / bf16 epilogues (gate_up 47.5 vs 50.5 us).
+  const int nwaves = waves == 8 || (waves <= 0 && epi == EPI_SLAB) ? 8 : 4;
+  dim3 grid(N / (16 * nt_tiles), slabs), blk(64 * nwaves);
   const int MT = (M + 15) / 16;
-#define K8S_SK(MTV, NTV, EPV, APKV)                                                                            \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV>), grid, blk, 0, s, (const bf16_t*)A, lda,       \
+#define K8S_SK(MTV, NTV, EPV, APKV, WV)                                                                        \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV, WV>), grid, blk, 0, s, (const bf16_t*)A, lda,   \
                      (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps)
-#define K8S_SK_M(NTV, EPV, NTLV)             \
-  switch (MT) {                              \
-    case 1: K8S_SK(1, NTV, EPV, NTLV); break; \
-    case 2: K8S_SK(2, NTV, EPV, NTLV); break; \
-    case 3: K8S_SK(3, NTV, EPV, NTLV); break; \
-    default: K8S_SK(4, NTV, EPV, NTLV); break; \
+#define K8S_SK_W(MTV, NTV, EPV, NTLV)                                       \
+  if (nwaves == 8) { K8S_SK(MTV, NTV, EPV, NTLV, 8); }                      \
+  else { K8S_SK(MTV, NTV, EPV, NTLV, 4); }
+#define K8S_SK_M(NTV, EPV, NTLV)                   \
+  switch (MT) {                                    \
+    case 1: K8S_SK_W(1, NTV, EPV, NTLV); break;     \
+    case 2: K8S_SK_W(2, NTV, EPV, NTLV); break;     \
+    case 3: K8S_SK_W(3, NTV, EPV, NTLV); break;     \
+    default: K8S_SK_W(4, NTV, EPV, NTLV); break;    \
   }
 #define K8S_SK_NTL(NTV, EPV)  \
   if (a_packed) {             \
@@ -552,6 +561,7 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
   }
 #undef K8S_SK_NTL
 #undef K8S_SK_M
+#undef K8S_SK_W
 #undef K8S_SK
   return (int)hipGetLastError();
 }

@@ -37,6 +37,20 @@ def test_skinny_splits_bounds(monkeypatch):
     assert ops.skinny_splits(4096, 4096) == 3
 
 
+def test_skinny_auto_splits_whole_rounds(monkeypatch):
+    """Automatic split-K (mirror of the HIP launcher): power of two, grid <= one workgroup per CU,
+    slices >= 512 deep and a multiple of the 4 waves' 256-deep round."""
+    monkeypatch.delenv("K8SLLM_SKINNY_WIDE", raising=False)
+    assert ops.skinny_auto_splits(64, 6144, 4096) == 2   # Llama-3-8B qkv: 96 tiles x 2
+    assert ops.skinny_auto_splits(64, 4096, 4096) == 4   # o
+    assert ops.skinny_auto_splits(64, 4096, 14336) == 4  # down
+    assert ops.skinny_auto_splits(64, 1280, 8192) == 8   # Llama-3-70B qkv at TP=8
+    assert ops.skinny_auto_splits(64, 256, 128) == 1     # tiny model: no split
+    for N, K in ((6144, 4096), (4096, 14336), (1280, 8192), (28672, 4096)):
+        s = ops.skinny_auto_splits(64, N, K)
+        assert s == 1 or ((N // 64) * s <= 256 and K % (s * 256) == 0)
+
+
 def test_decode_skinny_path_matches_generic_cpu(monkeypatch):
     """The decode control flow over packed weights (split-K slabs reduced in rope / the norm tail,
     SwiGLU epilogue) equals the generic path, on the CPU forms of the ops (fp32)."""
