@@ -39,8 +39,12 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
   __shared__ __attribute__((aligned(16))) bf16_t Ks[64 * D];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[64 * D];
 
-  const int qb = blockIdx.x;
-  const int hq = blockIdx.y;
+  // grid (Hq, q-blocks): the host orders q-blocks heaviest first (most keys), and x = head runs
+  // fastest so the whole grid drains heavy-first.  Blocks x and x + 8 share an XCD (round-robin
+  // dispatch), so heads are remapped to give each XCD a contiguous head range - the query heads
+  // of one GQA group then share their K/V tiles through that XCD's L2.
+  const int qb = blockIdx.y;
+  const int hq = (Hq & 7) == 0 ? (blockIdx.x & 7) * (Hq >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const int G = Hq / Hkv;
   const int kvh = hq / G;
   const int seq = qb_seq[qb];
@@ -79,32 +83,26 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
   const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
   const int vcol_base = 16 * ((lane >> 4) & 1) + 4 * p4;
 
-  for (int k0 = 0; k0 < kv_end; k0 += 64) {
-    __syncthreads();
-    if constexpr (!PAGED) {
+  // K/V tile staging, software-pipelined (cdna_hip_programming.md T14, issue-early / write-late):
+  // tile t+1's global loads are issued into registers right after tile t is staged, so they are in
+  // flight during tile t's MFMAs, and land in LDS at the top of the next iteration.
+  uint4 kreg[4], vreg[4];
+  auto fetch = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + 256 * i;
-        const int r = c / CH, ch = c % CH;
-        const int kr = k0 + r;
-        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CH, ch = c % CH;
+      const int kr = k0 + r;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if constexpr (!PAGED) {
         if (kr < L) {
           kv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + koff + ch * 8);
           vv = *reinterpret_cast<const uint4*>(base + (long)kr * qkv_stride + voff + ch * 8);
         }
-        *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
-        *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
-      }
-    } else {
-      // keys of the new tokens come from this step's qkv rows (16-byte loads, as above); only the
-      // cached prefix [0, cst) is read from the paged cache: K as 16-byte [D/8][16][8] pieces, V
-      // (d-major [D][16] per block) gathered 8 dims x 2 bytes - a handful of tiles per sequence
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + 256 * i;
-        const int r = c / CH, ch = c % CH;
-        const int kr = k0 + r;
-        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      } else {
+        // keys of the new tokens come from this step's qkv rows (16-byte loads, as above); only
+        // the cached prefix [0, cst) is read from the paged cache: K as 16-byte [D/8][16][8]
+        // pieces, V (d-major [D][16] per block) gathered 8 dims x 2 bytes
         if (kr >= cst && kr < LK) {
           const bf16_t* row = base + (long)(kr - cst) * qkv_stride;
           kv = *reinterpret_cast<const uint4*>(row + koff + ch * 8);
@@ -118,11 +116,23 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
           for (int j = 0; j < 4; ++j) w[j] = (uint32_t)vp[(2 * j) * 16] | ((uint32_t)vp[(2 * j + 1) * 16] << 16);
           vv = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kv;
-        *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vv;
       }
+      kreg[i] = kv;
+      vreg[i] = vv;
+    }
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < kv_end; k0 += 64) {
+    __syncthreads();  // every wave is done reading the previous tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CH, ch = c % CH;
+      *reinterpret_cast<uint4*>(Ks + (r * CH + (ch ^ (r & 15))) * 8) = kreg[i];
+      *reinterpret_cast<uint4*>(Vs + (r * CH + (ch ^ ((r & 3) << 2))) * 8) = vreg[i];
     }
     __syncthreads();
+    if (k0 + 64 < kv_end) fetch(k0 + 64);
     if (k0 > wave_q0 + 31) continue;  // every key of this tile is in the future of every row of this wave
 
     f32x16 sacc[2];
@@ -227,11 +237,11 @@ extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv,
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   if (ctx_start != nullptr) {
-    hipLaunchKernelGGL((flash_prefill_kernel<128, true>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out,
+    hipLaunchKernelGGL((flash_prefill_kernel<128, true>), dim3(Hq, n_qblocks), dim3(256), 0, s, (bf16_t*)out,
                        out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,
                        ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride);
   } else {
-    hipLaunchKernelGGL((flash_prefill_kernel<128, false>), dim3(n_qblocks, Hq), dim3(256), 0, s, (bf16_t*)out,
+    hipLaunchKernelGGL((flash_prefill_kernel<128, false>), dim3(Hq, n_qblocks), dim3(256), 0, s, (bf16_t*)out,
                        out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,
                        nullptr, nullptr, nullptr, nullptr, 0);
   }
