@@ -195,12 +195,19 @@ class BlockManager:
             return False
         seq.block_table = list(matched) + list(got)
         seq.num_cached = len(matched) * self.block_size
+        seq.num_computed = seq.num_cached
+        seq.prefilled = False
         self.cached_tokens += seq.num_cached
-        # the blocks this prefill computes become reusable prefixes (stream order makes any later
-        # reader - even another sequence of the same prefill step - see them computed)
-        for i in range(len(matched), len(hs)):
-            self.pool.publish(seq.block_table[i], hs[i])
         return True
+
+    def publish_computed(self, seq: Sequence, n_tokens: int) -> None:
+        """Publish the full prompt blocks below position ``n_tokens`` as reusable prefixes - called
+        for the tokens a prefill step is about to compute (stream order makes any later reader,
+        even another sequence of the same prefill step, see them computed).  With chunked
+        prefill, blocks of later chunks are published only when their chunk is scheduled."""
+        hs = self._prefix_hashes(seq)
+        for i in range(seq.num_cached // self.block_size, min(len(hs), n_tokens // self.block_size)):
+            self.pool.publish(seq.block_table[i], hs[i])
 
     def ensure_slot(self, seq: Sequence) -> bool:
         """Make room for the token at position seq.num_tokens (the next decode write)."""
@@ -217,6 +224,9 @@ class BlockManager:
             self.pool.release(list(seq.block_table))
             seq.block_table = []
         seq.num_cached = 0
+        seq.num_computed = 0
+        seq.chunk = 0
+        seq.prefilled = False
 
     def usage(self) -> float:
         return 1.0 - self.pool.num_free / max(1, self.num_blocks)

@@ -42,6 +42,7 @@ class EngineConfig:
     max_num_seqs: int = 64
     max_model_len: int = 8192
     max_prefill_tokens: int = 16384
+    chunked_prefill: bool = True  # prompts beyond a step's token budget prefill in chunks (scheduler.py)
     kv_cache_gb: float = 32.0
     num_blocks: Optional[int] = None
     use_graphs: bool = True
@@ -57,11 +58,12 @@ class EngineConfig:
 class _View:
     """What the runner needs of a sequence; built on non-leader TP ranks from the broadcast."""
 
-    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params", "num_cached")
+    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params", "num_computed", "chunk")
 
-    def __init__(self, all_ids, num_tokens, block_table, last_token, params, num_cached=0):
+    def __init__(self, all_ids, num_tokens, block_table, last_token, params, num_computed=0, chunk=0):
         self.all_ids, self.num_tokens, self.block_table = all_ids, num_tokens, block_table
-        self.last_token, self.params, self.num_cached = last_token, params, num_cached
+        self.last_token, self.params = last_token, params
+        self.num_computed, self.chunk = num_computed, chunk
 
 
 class LLMEngine:
@@ -85,7 +87,8 @@ class LLMEngine:
         self.blocks = BlockManager(self.runner.num_blocks, prefix_caching=cfg.prefix_caching)
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
                                                max_prefill_tokens=cfg.max_prefill_tokens,
-                                               max_model_len=self.runner.max_len), self.blocks)
+                                               max_model_len=self.runner.max_len,
+                                               chunked_prefill=cfg.chunked_prefill), self.blocks)
         self.tokenizer = tokenizer_for(mc)
         self.eos = set(mc.eos_ids)
         self.init_s = time.perf_counter() - t0
@@ -138,7 +141,7 @@ class LLMEngine:
             return self._step_sync()
         done: list[Sequence] = []
         s = self.sched
-        if self._inflight is not None and (not s.running or (s.waiting and len(s.running) < self.cfg.max_num_seqs)):
+        if self._inflight is not None and (not s.running or s.prefill_pending()):
             done += self._resolve()
         plan = s.schedule()
         self.counters["preemptions"] += len(plan.preempted)
@@ -224,13 +227,15 @@ class LLMEngine:
             self.counters["prefill_steps"] += 1
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), "prefill", len(plan.seqs),
-                                   sum(q.num_tokens for q in plan.seqs)))
+                                   sum(q.chunk for q in plan.seqs)))
         else:
             toks = self.runner.decode(plan.seqs)
             self.counters["decode_steps"] += 1
         now = time.perf_counter()
         done = []
         for seq, tok in zip(plan.seqs, toks):
+            if plan.is_prefill and not self.sched.chunk_done(seq):
+                continue  # a chunk short of the prompt's end: no token yet
             seq.output_ids.append(int(tok))
             self.counters["generated_tokens"] += 1
             if seq.t_first_token is None:
@@ -279,7 +284,8 @@ class LLMEngine:
     @staticmethod
     def _pack(plan) -> tuple:
         if plan.is_prefill:
-            return (True, [(s.all_ids, s.block_table, _params_t(s.params), s.num_cached) for s in plan.seqs])
+            return (True, [(s.all_ids, s.block_table, _params_t(s.params), s.num_computed, s.chunk)
+                           for s in plan.seqs])
         return (False, [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.seqs])
 
     def worker_loop(self) -> None:
@@ -294,7 +300,8 @@ class LLMEngine:
                 if pending is not None:
                     self.runner.decode_collect(pending)
                     pending = None
-                views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p), nc) for ids, bt, p, nc in items]
+                views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p), nc, ch)
+                         for ids, bt, p, nc, ch in items]
                 self.runner.prefill(views)
             else:
                 src = msg[2] if len(msg) > 2 else None

@@ -100,14 +100,15 @@ class ModelRunner:
 
     # --------------------------------------------------------------------- prefill
     def prefill(self, seqs: list[Sequence]) -> list[int]:
-        """Run whole prompts (prompt + any tokens generated before a preemption) minus their cached
-        prefix (``seq.num_cached`` tokens whose KV blocks came from the prefix cache); returns
-        the first sampled token of each sequence.  With any cached prefix the attention reads
-        keys/values from the paged cache (paged flash prefill)."""
+        """Run each sequence's scheduled prefill chunk: tokens [num_computed, num_computed + chunk)
+        of its prompt (+ any tokens generated before a preemption); the first num_computed tokens
+        already have their KV in the cache (prefix-cache hits, earlier chunks) and are attended
+        through the paged flash prefill.  Returns the token sampled after each chunk (the first
+        output token of sequences whose prompt this step completes)."""
         dev = self.device
-        starts = [getattr(s, "num_cached", 0) for s in seqs]
-        lens = [s.num_tokens - c for s, c in zip(seqs, starts)]
-        ids = np.concatenate([np.asarray(s.all_ids[c:], dtype=np.int32) for s, c in zip(seqs, starts)])
+        starts = [s.num_computed for s in seqs]
+        lens = [s.chunk or (s.num_tokens - c) for s, c in zip(seqs, starts)]
+        ids = np.concatenate([np.asarray(s.all_ids[c:c + n], dtype=np.int32) for s, c, n in zip(seqs, starts, lens)])
         pos = np.concatenate([np.arange(c, c + n, dtype=np.int32) for c, n in zip(starts, lens)])
         slots = np.empty(ids.shape[0], dtype=np.int32)
         o = 0
@@ -130,7 +131,8 @@ class ModelRunner:
                 bt[i, : len(s.block_table)] = s.block_table
             meta.ctx_start = t(np.asarray(starts, dtype=np.int32))
             meta.block_tables = t(bt)
-        self.n_steps["prefill_cached_tokens"] = self.n_steps.get("prefill_cached_tokens", 0) + sum(starts)
+        # tokens attended from the paged cache instead of recomputed (prefix hits + earlier chunks)
+        self.n_steps["prefill_context_tokens"] = self.n_steps.get("prefill_context_tokens", 0) + sum(starts)
         logits = self.model.forward(t(ids), meta, self.kv)
         S = len(seqs)
         temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32).to(dev)

@@ -1,7 +1,8 @@
 """Continuous-batching scheduler.
 
-Each engine step is either a *prefill* step (admit waiting requests whose whole prompts fit the
-token budget and the free KV blocks) or a *decode* step (one token for every running sequence).
+Each engine step is either a *prefill* step (admit waiting requests while the token budget and
+the free KV blocks last; a prompt larger than the remaining budget is prefilled in chunks over
+several steps) or a *decode* step (one token for every fully prefilled running sequence).
 Prefill has priority so newly arrived diagnostic queries join the running batch at the next
 step; decode steps are captured hipGraphs, so keeping them homogeneous keeps them replayable.
 When the cache runs out during decode the most recently admitted sequence is preempted
@@ -24,6 +25,11 @@ class SchedulerConfig:
     max_num_seqs: int = 64
     max_prefill_tokens: int = 16384
     max_model_len: int = 8192
+    # chunked prefill: a prompt that does not fit the step's remaining token budget is prefilled
+    # in chunks over several steps (later chunks attend the earlier ones through the paged flash
+    # prefill), so every prefill step computes at most max_prefill_tokens tokens - a bound on the
+    # step's activation memory and on how long running decodes wait behind a long prompt
+    chunked_prefill: bool = True
 
 
 @dataclass
@@ -67,27 +73,37 @@ class Scheduler:
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
 
+    def prefill_pending(self) -> bool:
+        """Would the next schedule() be a prefill step?"""
+        return bool(self.waiting and len(self.running) < self.cfg.max_num_seqs) or any(
+            not q.prefilled for q in self.running)
+
     def schedule(self) -> StepPlan:
-        # 1. prefill newly arrived (or preempted) requests
-        if self.waiting and len(self.running) < self.cfg.max_num_seqs:
+        # 1. prefill: first the next chunks of partially prefilled sequences, then newly arrived
+        #    (or preempted) requests, within the step's token budget
+        partial = [q for q in self.running if not q.prefilled]
+        if partial or (self.waiting and len(self.running) < self.cfg.max_num_seqs):
             plan = StepPlan(is_prefill=True)
             budget = self.cfg.max_prefill_tokens
-            while self.waiting and len(self.running) + len(plan.seqs) < self.cfg.max_num_seqs:
+            for seq in partial:
+                if budget <= 0:
+                    break
+                self._take_chunk(seq, budget, plan)
+                budget -= seq.chunk
+            while budget > 0 and self.waiting and len(self.running) + len(plan.seqs) < self.cfg.max_num_seqs:
                 seq = self.waiting[0]
-                n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens this step computes
-                if plan.seqs and n > budget:
+                n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens left to compute
+                if n > budget and not self.cfg.chunked_prefill and plan.seqs:
                     break
                 if not self.blocks.can_allocate(seq):
                     break
                 self.waiting.popleft()
                 self.blocks.allocate(seq)
                 seq.status = SeqStatus.RUNNING
-                plan.seqs.append(seq)
-                budget -= n
-                if budget <= 0:
-                    break
+                self.running.append(seq)
+                self._take_chunk(seq, budget if self.cfg.chunked_prefill else n, plan)
+                budget -= seq.chunk
             if plan.seqs:
-                self.running.extend(plan.seqs)
                 return plan
         # 2. decode every running sequence
         plan = StepPlan(is_prefill=False)
@@ -103,6 +119,21 @@ class Scheduler:
             # retry the same index (the victim may have been this very sequence)
         plan.seqs = list(self.running)
         return plan
+
+    def _take_chunk(self, seq: Sequence, budget: int, plan: StepPlan) -> None:
+        """Schedule seq's next prefill chunk (at most ``budget`` tokens) into ``plan``."""
+        seq.chunk = min(seq.num_tokens - seq.num_computed, max(1, budget))
+        self.blocks.publish_computed(seq, seq.num_computed + seq.chunk)
+        plan.seqs.append(seq)
+
+    @staticmethod
+    def chunk_done(seq: Sequence) -> bool:
+        """Account a finished prefill step for seq; True when its whole prompt is now prefilled
+        (the step's sampled token is then its first output token)."""
+        seq.num_computed += seq.chunk
+        seq.chunk = 0
+        seq.prefilled = seq.num_computed >= seq.num_tokens
+        return seq.prefilled
 
     def _preempt(self, seq: Sequence) -> None:
         self.blocks.free(seq)

@@ -47,6 +47,11 @@ class Sequence:
     t_finish: Optional[float] = None
     n_preemptions: int = 0
     num_cached: int = 0  # leading prompt tokens whose KV came from the prefix cache (this admission)
+    # chunked prefill: tokens whose KV is in the cache (prefix cache + prefill chunks run so far),
+    # the chunk the current prefill step computes, and whether the whole prompt has been prefilled
+    num_computed: int = 0
+    chunk: int = 0
+    prefilled: bool = False
     user: object = None  # opaque payload for the caller (future, callback, ...)
 
     @property

@@ -72,7 +72,9 @@ def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):
 
         ecfg = EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch, max_model_len=cfg.llm.max_model_len,
                             kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
-                            tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype))
+                            tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype),
+                            max_prefill_tokens=cfg.llm.max_prefill_tokens, chunked_prefill=cfg.llm.chunked_prefill,
+                            prefix_caching=cfg.llm.prefix_caching)
         eng = LLMEngine(ecfg, device=device, pstate=pstate)
         eng.warmup()
         svc = EngineService(eng)

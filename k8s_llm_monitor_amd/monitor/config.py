@@ -56,6 +56,9 @@ class LLMConfig:
     use_graphs: bool = True
     top_p: float = 1.0
     top_k: int = 0
+    max_prefill_tokens: int = 16384  # token budget of one prefill step
+    chunked_prefill: bool = True  # longer prompts prefill in chunks of that budget
+    prefix_caching: bool = True  # reuse the KV blocks of shared prompt prefixes
 
 
 @dataclass

@@ -91,3 +91,73 @@ def test_prefix_caching_reuses_blocks_and_matches_uncached():
             assert eng.blocks.stats()["prefix_cached_tokens"] >= 2 * 16
             assert all(s.num_cached == 0 for s in rest)  # released at finish
     assert outs[True] == outs[False]
+
+
+def test_chunked_prefill_matches_whole_prompt_prefill():
+    """A prefill budget far below the prompt lengths: every prompt is prefilled in chunks over
+    several steps (later chunks attend the earlier ones from the paged cache); greedy outputs equal
+    those of whole-prompt prefill, and no step computes more than the budget."""
+    prompts = ["集群状态概览: node-000 NotReady, payments-api CrashLoopBackOff " * 3, "why is coredns failing? " * 4,
+               "短"]
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for budget in (4096, 40):
+        eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=512, num_blocks=128,
+                                     use_graphs=False, seed=5, dtype="float32", max_prefill_tokens=budget,
+                                     prefix_caching=False), device="cpu")
+        eng.trace = []
+        seqs = eng.generate(prompts, sp)
+        outs[budget] = [s.output_ids for s in seqs]
+        chunks = [e[3] for e in eng.trace if e[1] == "prefill"]
+        assert max(chunks) <= budget
+        if budget == 40:
+            assert len(chunks) >= sum(len(s.prompt_ids) for s in seqs) // 40
+            assert eng.runner.n_steps["prefill_context_tokens"] > 0
+    assert outs[4096] == outs[40]
+
+
+def test_scheduler_chunks_and_defers_decode():
+    from k8s_llm_monitor_amd.engine.block_manager import BlockManager
+    from k8s_llm_monitor_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from k8s_llm_monitor_amd.engine.sequence import Sequence
+
+    s = Scheduler(SchedulerConfig(max_num_seqs=4, max_prefill_tokens=32), BlockManager(64, use_native=False))
+    a = Sequence(prompt_ids=list(range(70)), params=SamplingParams())
+    b = Sequence(prompt_ids=list(range(10)), params=SamplingParams())
+    s.add(a)
+    s.add(b)
+    p1 = s.schedule()
+    assert p1.is_prefill and [q.chunk for q in p1.seqs] == [32]  # a's first chunk fills the budget
+    assert not s.chunk_done(a)
+    p2 = s.schedule()  # a's next chunk comes first and uses the whole budget
+    assert p2.is_prefill and p2.seqs == [a] and a.chunk == 32
+    s.chunk_done(a)
+    p3 = s.schedule()
+    assert p3.is_prefill and p3.seqs == [a, b] and (a.chunk, b.chunk) == (6, 10)
+    assert s.chunk_done(a) and s.chunk_done(b)
+    a.output_ids.append(1)
+    b.output_ids.append(1)
+    p4 = s.schedule()
+    assert not p4.is_prefill and p4.seqs == [a, b]
+    # without chunking a prompt larger than the budget still runs whole (alone)
+    s2 = Scheduler(SchedulerConfig(max_num_seqs=4, max_prefill_tokens=32, chunked_prefill=False),
+                   BlockManager(64, use_native=False))
+    c = Sequence(prompt_ids=list(range(70)), params=SamplingParams())
+    s2.add(c)
+    assert s2.schedule().seqs[0].chunk == 70
+
+
+@pytest.mark.gpu
+def test_gpu_chunked_prefill_matches_whole():
+    """Chunked prefill on the GPU path (paged flash prefill over earlier chunks, hipGraph decode)."""
+    prompts = ["集群状态概览: " + "node-001 CPU=93.1% [资源压力]\n" * 30, "kube-system coredns CrashLoopBackOff " * 8]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for budget in (16384, 100):
+        eng = LLMEngine(EngineConfig(model="llama-tiny-d128", max_num_seqs=8, max_model_len=1024, num_blocks=512,
+                                     seed=4, max_prefill_tokens=budget, prefix_caching=False), device="cuda")
+        eng.warmup()
+        outs[budget] = [s.output_ids for s in eng.generate(prompts, sp)]
+        if budget == 100:
+            assert eng.counters["prefill_steps"] >= 4
+    assert outs[16384] == outs[100]

@@ -71,7 +71,12 @@ def test_block_manager_prefix_sharing(native):
     b = Sequence(prompt_ids=list(range(40)) + [7] * 5, params=SamplingParams())
     c = Sequence(prompt_ids=list(range(32)), params=SamplingParams())  # exactly 2 full blocks
     assert bm.allocate(a) and a.num_cached == 0
+    assert bm.cached_prefix_tokens(b) == 0  # published only when a prefill step computes them
+    bm.publish_computed(a, 16)  # chunked prefill: a's first chunk covers one block
+    assert bm.cached_prefix_tokens(b) == 16
+    bm.publish_computed(a, a.num_tokens)
     assert bm.cached_prefix_tokens(b) == 32 and bm.allocate(b) and b.num_cached == 32
+    bm.publish_computed(b, b.num_tokens)
     assert b.block_table[:2] == a.block_table[:2] and b.block_table[2] != a.block_table[2]
     # a fully cached prompt still runs its last token: only the first block is reused
     assert bm.allocate(c) and c.num_cached == 16
