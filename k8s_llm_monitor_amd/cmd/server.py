@@ -6,6 +6,8 @@ Multi-GPU (one process per GPU, ``torchrun --nproc-per-node N``):
 * ``llm.tp_size = N``   - one tensor-parallel engine; rank 0 serves HTTP, ranks 1.. mirror its steps.
 * ``llm.tp_size = 1``   - N data-parallel replicas, replica r serves on ``server.port + r`` (put a
                           Kubernetes Service / load balancer in front, as for any replica set).
+Single process, ``llm.dp_replicas = N``: one HTTP server whose queries a least-loaded router spreads
+over N engine processes, one per GPU (engine/dp.py).
 """
 from __future__ import annotations
 
@@ -36,14 +38,10 @@ def main(argv=None) -> int:
         if ws > 1:
             pstate = init_parallel(tp_size=cfg.llm.tp_size)
             if pstate.tp_rank != 0:  # TP worker: no HTTP, mirror the leader's engine steps
-                from ..engine import EngineConfig, LLMEngine
-                from ..monitor.app import torch_dtype_name
+                from ..engine import LLMEngine
+                from ..monitor.app import engine_config
 
-                eng = LLMEngine(EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch,
-                                             max_model_len=cfg.llm.max_model_len, kv_cache_gb=cfg.llm.kv_cache_gb,
-                                             use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
-                                             tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype)),
-                                pstate=pstate)
+                eng = LLMEngine(engine_config(cfg), pstate=pstate)
                 eng.warmup()
                 log.info("TP worker rank %d ready", pstate.rank)
                 eng.worker_loop()

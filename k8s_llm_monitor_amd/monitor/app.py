@@ -62,22 +62,36 @@ def make_backend(cfg: Config, fake_seed: int = 0):
         return None
 
 
+def engine_config(cfg: Config):
+    """The in-process engine's EngineConfig from the ``llm:`` block."""
+    from ..engine import EngineConfig
+
+    return EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch, max_model_len=cfg.llm.max_model_len,
+                        kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
+                        tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype),
+                        max_prefill_tokens=cfg.llm.max_prefill_tokens, chunked_prefill=cfg.llm.chunked_prefill,
+                        prefix_caching=cfg.llm.prefix_caching)
+
+
 def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):
-    """Returns (backend, engine, engine_service)."""
+    """Returns (backend, engine, engine_service).  ``llm.dp_replicas > 1`` (single process,
+    TP = 1): the service is a ReplicaRouter over that many engine processes, one per GPU
+    (engine/dp.py), and ``engine`` is None (the engines live in the replica processes)."""
     from ..llm.service import LocalEngineBackend, OpenAIBackend, RuleBackend
 
     prov = (cfg.llm.provider or "").lower()
     if prov in ("local-rocm", "local", "rocm"):
-        from ..engine import EngineConfig, EngineService, LLMEngine
+        from ..engine import EngineService, LLMEngine
 
-        ecfg = EngineConfig(model=cfg.llm.model, max_num_seqs=cfg.llm.max_batch, max_model_len=cfg.llm.max_model_len,
-                            kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
-                            tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype),
-                            max_prefill_tokens=cfg.llm.max_prefill_tokens, chunked_prefill=cfg.llm.chunked_prefill,
-                            prefix_caching=cfg.llm.prefix_caching)
-        eng = LLMEngine(ecfg, device=device, pstate=pstate)
-        eng.warmup()
-        svc = EngineService(eng)
+        ecfg = engine_config(cfg)
+        if cfg.llm.dp_replicas > 1 and pstate is None:
+            from ..engine.dp import ReplicaRouter, replica_devices
+
+            eng, svc = None, ReplicaRouter(ecfg, replica_devices(cfg.llm.dp_replicas))
+        else:
+            eng = LLMEngine(ecfg, device=device, pstate=pstate)
+            eng.warmup()
+            svc = EngineService(eng)
         return (LocalEngineBackend(svc, cfg.llm.max_tokens, cfg.llm.temperature, cfg.llm.top_p, cfg.llm.top_k,
                                    timeout_s=float(cfg.llm.timeout)), eng, svc)
     if prov == "openai":
