@@ -44,6 +44,12 @@ int k8sllm_gemm_skinny_slabs(int K, int S);
 int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
                               float eps, long out_stride, hipStream_t s);
+void* k8sllm_car_create(int rank, int world, long max_elems, void* handles, int* err);
+int k8sllm_car_handle_size();
+int k8sllm_car_open(void* state, const void* all_handles);
+int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
+int k8sllm_car_error(void* state);
+void k8sllm_car_destroy(void* state);
 }
 
 namespace {
@@ -405,6 +411,31 @@ void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, c10::optiona
         "reduce_add_rms_norm");
 }
 
+// One-shot IPC all-reduce (custom_ar.hip).  The state is an opaque pointer held by Python.
+py::tuple car_create(int64_t rank, int64_t world, int64_t max_elems) {
+  std::string h(2 * k8sllm_car_handle_size(), '\0');
+  int err = 0;
+  void* st = k8sllm_car_create((int)rank, (int)world, (long)max_elems, h.data(), &err);
+  TORCH_CHECK(st != nullptr, "custom all-reduce: allocation / IPC handle failed, hip error ", err);
+  return py::make_tuple((int64_t)(intptr_t)st, py::bytes(h));
+}
+
+void car_open(int64_t state, py::bytes all_handles) {
+  std::string a = all_handles;
+  check(k8sllm_car_open((void*)(intptr_t)state, a.data()), "car_open (hipIpcOpenMemHandle)");
+}
+
+void car_all_reduce(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit) {
+  dev_bf16(in, "in"); dev_bf16(out, "out");
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "car_all_reduce layout");
+  check(k8sllm_car_all_reduce((void*)(intptr_t)state, in.data_ptr(), out.data_ptr(), (long)in.numel(),
+                              (long)spin_limit, cur()),
+        "car_all_reduce");
+}
+
+int64_t car_error(int64_t state) { return k8sllm_car_error((void*)(intptr_t)state); }
+
+void car_destroy(int64_t state) { k8sllm_car_destroy((void*)(intptr_t)state); }
 
 PYBIND11_MODULE(_k8sllm_ops, m) {
   m.doc() = "gfx950 HIP kernels for k8s-llm-monitor-amd";
@@ -426,4 +457,9 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);
+  m.def("car_create", &car_create);
+  m.def("car_open", &car_open);
+  m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_error", &car_error);
+  m.def("car_destroy", &car_destroy);
 }

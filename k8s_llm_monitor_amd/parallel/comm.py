@@ -15,11 +15,21 @@ import torch.distributed as dist
 from .state import get_state
 
 
+def _rccl(st, x: torch.Tensor) -> bool:
+    """Device tensor on an RCCL group (gloo groups - CPU runs, or several ranks sharing one GPU in
+    tests - lack the *_into_tensor collectives)."""
+    return x.is_cuda and dist.get_backend(st.tp_group) == "nccl"
+
+
 def tp_all_reduce(x: torch.Tensor, ps=None) -> torch.Tensor:
-    """In-place sum over the TP group (C-1 / C-2 / C-3)."""
+    """In-place sum over the TP group (C-1 / C-2 / C-3): the one-shot IPC all-reduce for messages
+    that fit its staging buffer (decode), RCCL for the rest (prefill)."""
     st = ps or get_state()
     if st.tp_size == 1:
         return x
+    car = st.custom_ar
+    if car is not None and car.fits(x):
+        return car.all_reduce_(x)
     dist.all_reduce(x, op=dist.ReduceOp.SUM, group=st.tp_group)
     return x
 
@@ -31,7 +41,7 @@ def tp_all_gather_last(x: torch.Tensor, ps=None) -> torch.Tensor:
         return x
     x = x.contiguous()
     out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    if x.is_cuda:
+    if _rccl(st, x):
         dist.all_gather_into_tensor(out, x, group=st.tp_group)
     else:  # gloo has no all_gather_into_tensor
         dist.all_gather(list(out.unbind(0)), x, group=st.tp_group)
@@ -55,7 +65,7 @@ def tp_all_gather_rows(x: torch.Tensor, ps=None) -> torch.Tensor:
         return x
     x = x.contiguous()
     out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    if x.is_cuda:
+    if _rccl(st, x):
         dist.all_gather_into_tensor(out, x, group=st.tp_group)
     else:
         dist.all_gather(list(out.chunk(st.tp_size)), x, group=st.tp_group)

@@ -1,0 +1,76 @@
+"""One-shot IPC all-reduce for latency-bound tensor-parallel decode messages (custom_ar.hip).
+
+Every TP rank registers a double-buffered staging buffer and a signal block, exchanges their IPC
+handles over the CPU gloo group, and maps every peer's (``hipIpcOpenMemHandle``, xGMI peer
+access).  ``all_reduce_(x)`` is then ONE kernel launch, hipGraph-capturable, that stages x, flags
+every peer and sums all ranks' slices in rank order - one xGMI hop reading all peers at once,
+instead of a ring's 2(W-1) latency-bound hops over one link.  Messages larger than the staging
+buffer (prefill activations) keep RCCL (``parallel/comm.tp_all_reduce`` picks per call).
+
+Enabled with ``K8SLLM_CUSTOM_AR=1`` (``init_parallel(custom_ar=True)``): validated on one MI355X
+with two processes sharing the GPU (tests/test_custom_ar.py); RCCL stays the default until an
+8-GPU node has exercised it.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_MAX_BYTES = 8 << 20  # >= 64 rows x 8192 x bf16 (Llama-3-70B decode at TP=8) with headroom
+DEFAULT_SPIN_LIMIT = 4_000_000  # polls before a missing peer is declared failed (seconds, not forever)
+
+
+class CustomAllReduce:
+    def __init__(self, rank: int, world: int, cpu_group=None, max_bytes: int = DEFAULT_MAX_BYTES,
+                 spin_limit: int = DEFAULT_SPIN_LIMIT):
+        from ..ops import native
+
+        if world < 2 or world > 8:
+            raise ValueError("custom all-reduce supports 2..8 ranks")
+        self.rank, self.world = rank, world
+        self.max_elems = (max_bytes // 2) // 8 * 8
+        self.spin_limit = int(spin_limit)
+        self._n = native()
+        self.state, handles = self._n.car_create(rank, world, self.max_elems)
+        gathered: list = [None] * world
+        dist.all_gather_object(gathered, handles, group=cpu_group)
+        self._n.car_open(self.state, b"".join(gathered))
+        if cpu_group is not None or dist.is_initialized():
+            dist.barrier(group=cpu_group)  # every rank mapped every peer before the first call
+
+    def fits(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
+                and 0 < x.numel() <= self.max_elems)
+
+    def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the group (x must satisfy ``fits``)."""
+        self._n.car_all_reduce(self.state, x, x, self.spin_limit)
+        return x
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        out = torch.empty_like(x)
+        self._n.car_all_reduce(self.state, x, out, self.spin_limit)
+        return out
+
+    def error(self) -> bool:
+        """True if a call gave up waiting for a peer (its output was invalid)."""
+        return self._n.car_error(self.state) != 0
+
+    def close(self) -> None:
+        if self.state:
+            self._n.car_destroy(self.state)
+            self.state = 0
+
+
+def enabled() -> bool:
+    return os.environ.get("K8SLLM_CUSTOM_AR", "0") == "1"
+
+
+def maybe_create(ps) -> Optional[CustomAllReduce]:
+    """Collective over the TP group: a CustomAllReduce when enabled, on GPU, TP 2..8."""
+    if not (enabled() and ps.tp_size > 1 and ps.tp_size <= 8 and ps.device.type == "cuda"):
+        return None
+    return CustomAllReduce(ps.tp_rank, ps.tp_size, cpu_group=ps.cpu_group)

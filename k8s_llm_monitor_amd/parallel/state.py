@@ -38,6 +38,7 @@ class ParallelState:
     tp_group: Optional[object] = None  # device collectives (RCCL on GPU, gloo on CPU)
     cpu_group: Optional[object] = None  # gloo group spanning the TP group, for control broadcast
     device: torch.device = torch.device("cpu")
+    custom_ar: Optional[object] = None  # one-shot IPC all-reduce for small TP messages (custom_ar.py)
 
     @property
     def is_tp(self) -> bool:
@@ -104,6 +105,9 @@ def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optio
             cpu = dist.new_group(ranks, backend="gloo") if (tp_size > 1 and be != "gloo") else grp
             if rank in ranks:
                 st.tp_group, st.cpu_group = grp, cpu
+        from .custom_ar import maybe_create
+
+        st.custom_ar = maybe_create(st)  # K8SLLM_CUSTOM_AR=1, GPU, TP 2..8; else RCCL only
     set_state(st)
     return st
 
