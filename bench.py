@@ -128,8 +128,9 @@ def main() -> None:
         server.shutdown()
     if rank == 0:
         qps = total_q / t_max
-        metric = ("pod-communication analyses/sec (Llama-3-8B TP=1, /api/v1/analyze/pod-communication)"
-                  if a.path == "podcomm" else "diagnostic queries/sec (Llama-3-8B TP=1, /api/v1/query)")
+        name = _MODEL_NAMES.get(a.model, a.model)
+        metric = (f"pod-communication analyses/sec ({name} TP=1, /api/v1/analyze/pod-communication)"
+                  if a.path == "podcomm" else f"diagnostic queries/sec ({name} TP=1, /api/v1/query)")
         res = {
             "metric": metric,
             "value": round(qps, 4),
@@ -158,6 +159,10 @@ def main() -> None:
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+
+
+_MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "mixtral-8x7b": "Mixtral-8x7B",
+                "gpt2-small": "GPT-2-small"}
 
 
 def _print_trace(trace: list, t0: float) -> None:

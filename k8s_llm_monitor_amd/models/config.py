@@ -107,6 +107,11 @@ LLAMA_TINY128 = _reg(ModelConfig(
     name="llama-tiny-d128", arch="llama", vocab_size=1024, d_model=512, n_layers=2, n_heads=8, n_kv_heads=2,
     head_dim=128, ffn_dim=1024, max_position=2048, rope_theta=500000.0, bos_id=1, eos_ids=(2,)))
 
+MIXTRAL_TINY_D128 = _reg(ModelConfig(  # head_dim 128: the HIP attention kernels' shape, for GPU tests
+    name="mixtral-tiny-d128", arch="llama", vocab_size=1024, d_model=512, n_layers=2, n_heads=8, n_kv_heads=2,
+    head_dim=128, ffn_dim=1024, max_position=2048, rope_theta=1000000.0, n_experts=4, top_k_experts=2,
+    bos_id=1, eos_ids=(2,)))
+
 MIXTRAL_TINY = _reg(ModelConfig(
     name="mixtral-tiny", arch="llama", vocab_size=512, d_model=256, n_layers=2, n_heads=4, n_kv_heads=2,
     head_dim=64, ffn_dim=256, max_position=1024, rope_theta=10000.0, n_experts=4, top_k_experts=2,

@@ -405,16 +405,21 @@ class CausalLM:
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         c = self.cfg
-        if c.arch != "llama" or c.is_moe or os.environ.get("K8SLLM_SKINNY", "1") == "0":
+        if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0":
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
-        if d % 64 or nq % 64 or (self.hq * self.D) % 32 or self.f_local % 32:
+        ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
+        if d % 64 or nq % 64 or (self.hq * self.D) % 32 or ff % 64:
             return
         for L in self.layers:
             L["wqkv_p"] = ops.pack_skinny(L["wqkv"])
             L["wo_p"] = ops.pack_skinny(L["wo"])
-            L["w13_p"] = ops.pack_skinny(ops.interleave_gate_up(L["w13"]))
-            L["w2_p"] = ops.pack_skinny(L["w2"])
+            if c.is_moe:  # stacked per local expert for the grouped (grid.z = expert) launches
+                L["w13_pg"] = torch.stack([ops.pack_skinny(ops.interleave_gate_up(w)) for w in L["w13"]])
+                L["w2_pg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
+            else:
+                L["w13_p"] = ops.pack_skinny(ops.interleave_gate_up(L["w13"]))
+                L["w2_p"] = ops.pack_skinny(L["w2"])
         env = os.environ.get("K8SLLM_SKINNY_SPLITS")
         split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split
@@ -422,7 +427,8 @@ class CausalLM:
         def most(N: int, K: int) -> int:
             return split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
 
-        n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d, most(d, self.f_local) * d)
+        n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d,
+                (self.e_hi - self.e_lo) * ops.skinny_nslabs(ff, 1) * d if c.is_moe else most(d, ff) * d)
         self._skinny_ws = torch.empty(n * ops.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
@@ -439,9 +445,12 @@ class CausalLM:
             kv = kv_caches[i] if kv_caches is not None else None
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
             ns = ops.skinny_slabs(op, L["wo_p"], ws, self._split_o, rows=M)
-            xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
-            act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
-            ns = ops.skinny_slabs(act, L["w2_p"], ws, self._split_d, rows=M)
+            if c.is_moe:
+                ns = self._moe_skinny(L, residual, ws, ns, M)
+            else:
+                xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
+                act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
+                ns = ops.skinny_slabs(act, L["w2_p"], ws, self._split_d, rows=M)
             if i + 1 < n:
                 xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
         # final norm feeds the LM head (hipBLASLt): complete, row-major
@@ -451,6 +460,25 @@ class CausalLM:
         else:
             x = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return self._logits(x)
+
+    def _moe_skinny(self, L: dict, residual: torch.Tensor, ws, ns: int, M: int) -> int:
+        """MoE decode MLP on the grouped skinny kernels: residual += the o
+        projection; the router reads the complete RMSNorm; ONE launch runs gate/up + SwiGLU of every
+        local expert over every row (grid.z = expert; at decode batch sizes every expert is selected
+        by some row, so the step streams every expert's weights either way), ONE launch runs their
+        down projections into slabs scaled by the routing weights (0 where an expert was not
+        chosen) - the caller's residual-add kernel summing the slabs is the expert combine.  Host
+        sync free, so the step stays in the decode hipGraph."""
+        c = self.cfg
+        y = self._row_parallel_sum(ws, ns, M, residual)
+        if y is None:
+            xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps)
+        else:
+            xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
+        ids, w = ops.moe_route(F.linear(xn, L["router"]).float(), c.top_k_experts, True)
+        wd = torch.zeros(M, c.n_experts, dtype=torch.float32, device=xn.device).scatter_(1, ids.long(), w)
+        act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
+        return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 
     def _row_parallel_sum(self, ws, ns: int, M: int, residual: torch.Tensor) -> Optional[torch.Tensor]:
         """TP>1: the row-parallel projection's slabs summed to bf16 and all-reduced; None at TP=1."""

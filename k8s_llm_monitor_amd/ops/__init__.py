@@ -263,6 +263,44 @@ def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, spl
     return native().gemm_skinny(a, wp, workspace, None, splits, 0, nt_tiles, M, *_rn_args(rownorm))
 
 
+def skinny_grouped_swiglu(a: torch.Tensor, wp13: torch.Tensor, rows: int, out: Optional[torch.Tensor] = None
+                          ) -> torch.Tensor:
+    """MoE gate/up for every local expert in ONE launch (grid.z = experts): ``a`` is the shared
+    fragment-packed activation [MT, K/32, 64, 8], ``wp13`` the stacked packed, gate/up-interleaved
+    expert weights [E, 2F/16, K/32, 64, 8]; returns the per-expert packed SwiGLU activations
+    [E, MT, F/32, 64, 8] (the grouped down projection's A)."""
+    E, F = wp13.shape[0], wp13.shape[1] * 8
+    mt = -(-rows // 16)
+    if not _gpu(a):
+        y = torch.stack([skinny_swiglu(a, wp13[e], rows=rows, packed_out=True) for e in range(E)])
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(E, mt, F // 32, 64, 8, dtype=a.dtype, device=a.device)
+    native().gemm_skinny_grouped(a, wp13, None, out, 1, 3, rows, None, skinny_waves())
+    return out
+
+
+def skinny_grouped_slabs(act: torch.Tensor, wp2: torch.Tensor, workspace: torch.Tensor, rows: int,
+                         row_w: torch.Tensor, splits: int = 1) -> int:
+    """MoE down projection of every local expert in ONE launch: fp32 slabs [E * S', M, N] where
+    expert e's rows are scaled by its routing weights ``row_w[:, e]`` (0 where not selected), so
+    summing all slabs (add_norm_partial / reduce_slabs) IS the weighted expert combine.  Returns
+    the slab count E * S'."""
+    E, N, K = wp2.shape[0], wp2.shape[1] * 16, wp2.shape[2] * 32
+    M = rows
+    if not _gpu(act):
+        kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
+        slabs = workspace[: E * ns * M * N].view(E * ns, M, N)
+        for e in range(E):
+            x = unpack_skinny(act[e])[:M].float()
+            w = _cpu_w(wp2[e])
+            for s in range(ns):
+                slabs[e * ns + s] = (x[:, s * kc:(s + 1) * kc] @ w[:, s * kc:(s + 1) * kc].t()) * row_w[:M, e:e + 1]
+        return E * ns
+    return native().gemm_skinny_grouped(act, wp2, workspace, None, splits, 0, rows, row_w.contiguous(),
+                                        skinny_waves())
+
+
 def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int, norm_w: torch.Tensor,
                      out: Optional[torch.Tensor] = None, ss_part: Optional[torch.Tensor] = None,
                      packed: bool = True) -> tuple:

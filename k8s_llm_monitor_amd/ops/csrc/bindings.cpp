@@ -36,7 +36,8 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
-                       float rn_eps, int wide, int waves, hipStream_t s);
+                       float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
+                       const float* row_w, int row_w_ld, hipStream_t s);
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
@@ -342,9 +343,67 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   }
   check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
                            epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, rp, rn_nc, K,
-                           (float)rn_eps, wide ? 1 : 0, (int)waves, cur()),
+                           (float)rn_eps, wide ? 1 : 0, (int)waves, 1, 0, 0, 0, nullptr, 0, cur()),
         "gemm_skinny");
   return S;
+}
+
+// Grouped (MoE) skinny GEMM: wp [E, N/16, K/32, 64, 8] (one packed weight per local expert).
+// a: packed [MT, K/32, 64, 8] shared by every expert, or [E, MT, K/32, 64, 8] per expert.
+// epi 3: y = packed SwiGLU [E, MT, F/32, 64, 8]; epi 0: fp32 slabs partial[E * S'][M][N] with
+// row m of expert x's output scaled by row_w[m][x] (row_w [M, E] fp32, routing weights).
+// Returns E * S' (the slab count for the residual-add kernels) or 1.
+int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
+                            c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t rows,
+                            c10::optional<torch::Tensor> row_w, int64_t waves) {
+  dev_bf16(a, "a"); dev_bf16(wp, "wp");
+  TORCH_CHECK(wp.dim() == 5 && wp.size(3) == 64 && wp.size(4) == 8 && wp.is_contiguous(),
+              "gemm_skinny_grouped: wp must be [E, N/16, K/32, 64, 8]");
+  TORCH_CHECK(epi == 0 || epi == 3, "gemm_skinny_grouped: epi must be 0 (slabs) or 3 (packed SwiGLU)");
+  const int E = (int)wp.size(0), N = (int)wp.size(1) * 16, K = (int)wp.size(2) * 32, M = (int)rows;
+  const long w_es = wp[0].numel();
+  TORCH_CHECK(M > 0 && M <= 64, "gemm_skinny_grouped: 1..64 rows");
+  const int MT = (M + 15) / 16;
+  long a_es = 0;
+  TORCH_CHECK(a.is_contiguous() && a.size(-1) == 8 && a.size(-2) == 64 && a.size(-3) * 32 == K,
+              "gemm_skinny_grouped: a must be fragment-packed with K = ", K);
+  if (a.dim() == 5) {
+    TORCH_CHECK(a.size(0) == E && a.size(1) == MT, "gemm_skinny_grouped: per-expert a must be [E, MT, K/32, 64, 8]");
+    a_es = a[0].numel();
+  } else {
+    TORCH_CHECK(a.dim() == 4 && a.size(0) == MT, "gemm_skinny_grouped: shared a must be [MT, K/32, 64, 8]");
+  }
+  float* pp = nullptr;
+  void* yp = nullptr;
+  long y_es = 0;
+  const float* rw = nullptr;
+  int S = 1;
+  if (epi == 0) {
+    if (splits <= 0) splits = 1;
+    S = k8sllm_gemm_skinny_slabs(K, (int)splits);
+    TORCH_CHECK(partial.has_value() && partial->is_cuda() && partial->scalar_type() == torch::kFloat32 &&
+                    partial->is_contiguous() && partial->numel() >= (int64_t)E * S * M * N,
+                "gemm_skinny_grouped: partial must be fp32 with room for E * S * M * N");
+    pp = partial->data_ptr<float>();
+    if (row_w.has_value()) {
+      TORCH_CHECK(row_w->is_cuda() && row_w->scalar_type() == torch::kFloat32 && row_w->is_contiguous() &&
+                      row_w->dim() == 2 && row_w->size(0) >= M && row_w->size(1) == E,
+                  "gemm_skinny_grouped: row_w must be [M, E] fp32");
+      rw = row_w->data_ptr<float>();
+    }
+  } else {
+    TORCH_CHECK(y.has_value(), "gemm_skinny_grouped: output required");
+    dev_bf16(*y, "y");
+    TORCH_CHECK(y->dim() == 5 && y->is_contiguous() && y->size(0) == E && y->size(1) == MT &&
+                    y->size(2) * 64 == N && y->size(3) == 64 && y->size(4) == 8,
+                "gemm_skinny_grouped: y must be [E, MT, N/64, 64, 8]");
+    yp = y->data_ptr();
+    y_es = (*y)[0].numel();
+  }
+  check(k8sllm_gemm_skinny(a.data_ptr(), 0, wp.data_ptr(), pp, yp, 0, M, N, K, epi == 0 ? (int)splits : 1,
+                           (int)epi, 4, 1, nullptr, 0, K, 0.f, 0, (int)waves, E, w_es, a_es, y_es, rw, E, cur()),
+        "gemm_skinny_grouped");
+  return epi == 0 ? (int64_t)E * S : 1;
 }
 
 // residual += sum of S slabs; out = residual * w (row-major or fragment-packed); ss_part[m][c] =
@@ -454,6 +513,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("moe_combine", &moe_combine);
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
+  m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);

@@ -34,6 +34,17 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2, EPI_SWIGLU_PACKED = 3 };
 
+// Grouped (MoE expert) launches: grid.z = experts; expert x reads weights Wp + x * w_es, activations
+// A + x * a_es (0: every expert reads the same A), writes Y + x * y_es / slabs [x * S + s], and
+// (row_w) scales output row m by row_w[m * row_w_ld + x] - the routing weight, 0 for experts the
+// token did not select.  The down projection's slabs over (expert, split) are then summed by the
+// same residual-add kernels as a dense layer's split-K slabs.
+struct SkinnyGroup {
+  long w_es, a_es, y_es;
+  const float* row_w;
+  int row_w_ld;
+};
+
 // n-tile read for the workgroup's nt-th tile.  SwiGLU weights are interleaved per 128 rows as
 // [64 gate | 64 up] (interleave_gate_up): a 4-tile workgroup takes two gate tiles and the two
 // matching up tiles, so every output column has its gate and up value in the same workgroup.
@@ -59,13 +70,17 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const bf16_t* _
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
                                                           int kchunk, const float* __restrict__ rn_ss, int rn_nc,
-                                                          float rn_inv_d, float rn_eps) {
+                                                          float rn_inv_d, float rn_eps, SkinnyGroup grp) {
   // U k-steps per wave group; two groups in flight per wave (register double buffer)
   constexpr int U = MT <= 2 ? 4 : 2;
   __shared__ __attribute__((aligned(16))) float red[WAVES][NT][64][4];  // one m-tile at a time: 16 KiB per 4 waves
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ntile0 = blockIdx.x * NT;
   const int s = blockIdx.y;
+  const int ex = blockIdx.z;  // expert of a grouped launch (0 otherwise)
+  Wp += ex * grp.w_es;
+  A += ex * grp.a_es;
+  if (Y != nullptr) Y += ex * grp.y_es;
   const int kbeg = s * kchunk;
   const int nsteps = (min(K, kbeg + kchunk) - kbeg) >> 5;  // host guarantees 32 | K and 32 | kchunk
   const int ksteps = K >> 5;
@@ -199,10 +214,11 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const bf16_t* _
         for (int r = 0; r < 4; ++r) {
           const int row = mt * 16 + (l >> 4) * 4 + r;
           if (row < M) {
+            const float o = grp.row_w != nullptr ? v[r] * grp.row_w[(long)row * grp.row_w_ld + ex] : v[r];
             if constexpr (EPI == EPI_BF16)
-              Y[(long)row * ldy + col] = f2bf(v[r]);
+              Y[(long)row * ldy + col] = f2bf(o);
             else
-              partial[((long)s * M + row) * N + col] = v[r];
+              partial[((long)(ex * gridDim.y + s) * M + row) * N + col] = o;
           }
         }
       }
@@ -502,8 +518,12 @@ extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed,
 // (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
-                                  int rn_nc, int rn_d, float rn_eps, int wide, int waves, hipStream_t s) {
+                                  int rn_nc, int rn_d, float rn_eps, int wide, int waves, int experts, long w_es,
+                                  long a_es, long y_es, const float* row_w, int row_w_ld, hipStream_t s) {
   if (M <= 0) return 0;
+  if (experts < 1) return -5;
+  if (experts > 1) wide = 0;  // grouped launches use the narrow kernel
+  const SkinnyGroup grp{w_es, a_es, y_es, row_w, row_w_ld};
   if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed, wide) : 1;
   const int kc = skinny_kchunk(K, S);
@@ -529,11 +549,11 @@ extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float
   // (auto): 8 for the split-K slab projections (o 11.1 vs 11.8 us, down 24.3 vs 25.9 at M = 64),
   // 4 for the single-slice SwiGLU / bf16 epilogues (gate_up 47.5 vs 50.5 us).
   const int nwaves = waves == 8 || (waves <= 0 && epi == EPI_SLAB) ? 8 : 4;
-  dim3 grid(N / (16 * nt_tiles), slabs), blk(64 * nwaves);
+  dim3 grid(N / (16 * nt_tiles), slabs, experts), blk(64 * nwaves);
   const int MT = (M + 15) / 16;
 #define K8S_SK(MTV, NTV, EPV, APKV, WV)                                                                        \
   hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV, WV>), grid, blk, 0, s, (const bf16_t*)A, lda,   \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps)
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps, grp)
 #define K8S_SK_W(MTV, NTV, EPV, NTLV)                                       \
   if (nwaves == 8) { K8S_SK(MTV, NTV, EPV, NTLV, 8); }                      \
   else { K8S_SK(MTV, NTV, EPV, NTLV, 4); }

@@ -161,3 +161,14 @@ def test_gpu_chunked_prefill_matches_whole():
         if budget == 100:
             assert eng.counters["prefill_steps"] >= 4
     assert outs[16384] == outs[100]
+
+
+@pytest.mark.gpu
+def test_gpu_moe_decode_grouped_skinny_matches_recompute():
+    """Mixtral-shaped model on the GPU: grouped-skinny MoE decode in hipGraphs vs full recompute."""
+    eng = LLMEngine(EngineConfig(model="mixtral-tiny-d128", max_num_seqs=8, max_model_len=1024, num_blocks=256),
+                    device="cuda")
+    eng.warmup()
+    assert eng.runner.graphs and "w13_pg" in eng.model.layers[0]
+    _check_greedy_consistency(eng, ["why is pod default/api not ready?", "kube-system coredns " * 20, "x" * 100],
+                              8, "cuda")

@@ -397,3 +397,28 @@ def test_flash_prefill_paged(cached, new):
     out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
     exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
     _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what="paged prefill")
+
+
+@pytest.mark.parametrize("M,E", [(1, 4), (24, 8), (64, 2)])
+def test_skinny_grouped_moe(M, E):
+    """Grouped (grid.z = expert) SwiGLU + routing-weighted down slabs == per-expert fp32 references
+    combined with the routing weights (the MoE decode MLP)."""
+    K, F, d = 512, 448, 256
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(E, 2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(E, d, F, device=DEV) * 0.05).to(torch.bfloat16)
+    wd = torch.rand(M, E, device=DEV) * (torch.rand(M, E, device=DEV) > 0.5)
+    w13p = torch.stack([ops.pack_skinny(ops.interleave_gate_up(w)) for w in w13])
+    w2p = torch.stack([ops.pack_skinny(w) for w in w2])
+    act = ops.skinny_grouped_swiglu(ops.pack_activation(x), w13p, rows=M)
+    ws = torch.empty(E * M * d, device=DEV, dtype=torch.float32)
+    ns = ops.skinny_grouped_slabs(act, w2p, ws, M, wd, splits=1)
+    assert ns == E
+    out = ws[: E * M * d].view(E, M, d).sum(0)
+    ref_out = torch.zeros(M, d)
+    for e in range(E):
+        gu = torch.nn.functional.linear(x.cpu().float(), w13[e].cpu().float()).to(torch.bfloat16)
+        a = ref.silu_mul(gu)
+        _close(ops.unpack_skinny(act[e])[:M].cpu(), a, atol=3e-2, rtol=2e-2, what=f"expert {e} act")
+        ref_out += torch.nn.functional.linear(a.float(), w2[e].cpu().float()) * wd[:, e:e + 1].cpu()
+    _close(out.cpu(), ref_out, atol=6e-2, rtol=3e-2, what="weighted combine")

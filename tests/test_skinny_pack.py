@@ -1,4 +1,5 @@
 """Host-side layout helpers of the decode skinny GEMM (the GPU numerics are in test_ops_gpu.py)."""
+import pytest
 import torch
 
 from k8s_llm_monitor_amd import ops
@@ -51,13 +52,14 @@ def test_skinny_auto_splits_whole_rounds(monkeypatch):
         assert s == 1 or ((N // 64) * s <= 256 and K % (s * 256) == 0)
 
 
-def test_decode_skinny_path_matches_generic_cpu(monkeypatch):
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_decode_skinny_path_matches_generic_cpu(monkeypatch, model):
     """The decode control flow over packed weights (split-K slabs reduced in rope / the norm tail,
     SwiGLU epilogue) equals the generic path, on the CPU forms of the ops (fp32)."""
     from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
 
     monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")  # force real split-K slicing on tiny shapes
-    cfg = get_config("llama-tiny-d128")
+    cfg = get_config(model)
     m = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
     assert m._skinny_ws is not None and m._split_d == 3
     monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "0")
