@@ -1,6 +1,7 @@
 """REST contract tests: every route, dev mode and FakeCluster."""
 import http.client
 import json
+import os
 import threading
 
 import pytest
@@ -156,3 +157,19 @@ def test_real_http_roundtrip(mon):
         assert r.getheader("X-Content-Type-Options") == "nosniff"
     finally:
         srv.shutdown()
+
+
+def test_dev_mode_script_without_cluster():
+    """scripts/test_with_mock_k8s.sh: the server in development mode (no cluster, no model)."""
+    import shutil
+    import socket
+    import subprocess
+
+    if shutil.which("curl") is None:
+        pytest.skip("curl not installed")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run(["bash", "scripts/test_with_mock_k8s.sh", str(port)], capture_output=True, text=True,
+                       timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr
