@@ -1,6 +1,8 @@
 """The HTTP paths bench.py drives, end to end on the CPU with a tiny model: POST /api/v1/query
 and POST /api/v1/analyze/pod-communication (LLM explanation) through the in-process server, the
 engine thread and continuous batching."""
+import os
+
 import pytest
 
 from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine
@@ -36,3 +38,27 @@ def test_pod_communication_path(served):
     res = post_pod_communication(port, pairs, 5)
     assert len(res) == 3
     assert all(r["completion_tokens"] == 5 and r["type"] == "pod_communication" for r in res)
+
+
+def test_bench_two_ranks_under_torchrun_cpu():
+    """The driver's multi-GPU contract rehearsed on CPU: torchrun, 2 ranks (gloo), one JSON line
+    from rank 0 with the whole-job value, n_gpus 2 and dp2 parallelism."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch", "4",
+                        "--max-new-tokens", "4"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 8
+    assert d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0 and d["scaling"] == "weak"
