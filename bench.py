@@ -37,6 +37,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--kv-cache-gb", type=float, default=48.0)
+    ap.add_argument("--max-prefill-tokens", type=int, default=16384, help="token budget of one prefill step")
+    ap.add_argument("--chunked-prefill", type=int, default=1, choices=[0, 1])
     ap.add_argument("--path", choices=["http", "engine", "podcomm"], default="http",
                     help="http: POST /api/v1/query (headline); podcomm: POST /api/v1/analyze/pod-communication "
                          "with the LLM explanation (BASELINE config 3); engine: the engine queue directly")
@@ -62,6 +64,7 @@ def main() -> None:
         ops.native()  # fail loudly if the HIP kernels are missing
 
     eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, max_model_len=8192,
+                                 max_prefill_tokens=a.max_prefill_tokens, chunked_prefill=bool(a.chunked_prefill),
                                  kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
                                  seed=a.seed + rank), pstate=ps)
     eng.warmup()
