@@ -39,6 +39,8 @@ def main() -> None:
     ap.add_argument("--kv-cache-gb", type=float, default=48.0)
     ap.add_argument("--max-prefill-tokens", type=int, default=16384, help="token budget of one prefill step")
     ap.add_argument("--chunked-prefill", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--admit-gap-ms", type=float, default=None, help="engine admission coalescing gap (0 disables)")
+    ap.add_argument("--admit-window-ms", type=float, default=None)
     ap.add_argument("--path", choices=["http", "engine", "podcomm"], default="http",
                     help="http: POST /api/v1/query (headline); podcomm: POST /api/v1/analyze/pod-communication "
                          "with the LLM explanation (BASELINE config 3); engine: the engine queue directly")
@@ -63,7 +65,9 @@ def main() -> None:
         from k8s_llm_monitor_amd import ops
         ops.native()  # fail loudly if the HIP kernels are missing
 
-    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, max_model_len=8192,
+    admit = {k: v for k, v in (("admit_gap_ms", a.admit_gap_ms), ("admit_window_ms", a.admit_window_ms))
+             if v is not None}
+    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, max_model_len=8192, **admit,
                                  max_prefill_tokens=a.max_prefill_tokens, chunked_prefill=bool(a.chunked_prefill),
                                  kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
                                  seed=a.seed + rank), pstate=ps)
@@ -177,8 +181,18 @@ def _print_trace(trace: list, t0: float) -> None:
     dec = [e for e in ev if e[1] == "decode"]
     if not adds:
         return
-    print(f"[trace] adds {len(adds)} first +{(adds[0][0] - t0) * 1e3:.1f} ms last +{(adds[-1][0] - t0) * 1e3:.1f} ms",
-          file=sys.stderr)
+    waves, cur = [], [adds[0]]
+    for e in adds[1:]:  # a new wave starts after a > 0.5 s pause in arrivals
+        if e[0] - cur[-1][0] > 0.5:
+            waves.append(cur)
+            cur = []
+        cur.append(e)
+    waves.append(cur)
+    for w in waves:
+        gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
+        print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"
+              + (f" median gap {gaps[len(gaps) // 2] * 1e3:.2f} ms max gap {gaps[-1] * 1e3:.2f} ms" if gaps else ""),
+              file=sys.stderr)
     for e in pre:
         print(f"[trace] prefill +{(e[0] - t0) * 1e3:.1f} ms seqs {e[2]} tokens {e[3]}", file=sys.stderr)
     if dec:

@@ -52,6 +52,11 @@ class EngineConfig:
     # reuse KV blocks of identical prompt prefixes (block_manager.py); K8SLLM_PREFIX_CACHE=0 disables
     prefix_caching: bool = field(default_factory=lambda: os.environ.get("K8SLLM_PREFIX_CACHE", "1") != "0")
     dtype: str = "bfloat16"  # compute / weight dtype ("float32" for CPU parity tests)
+    # admission coalescing: when an idle engine receives a request, keep collecting arrivals until
+    # none comes for `admit_gap_ms` (at most `admit_window_ms`) before the first prefill, so a
+    # burst of queries starts as one full prefill batch instead of a lone first prompt
+    admit_gap_ms: float = 2.0
+    admit_window_ms: float = 20.0
     model_overrides: dict = field(default_factory=dict)
 
 
@@ -350,6 +355,9 @@ class EngineService:
             item = self._q.get(block=block, timeout=0.05 if block else None)
         except queue.Empty:
             return
+        cfg = self.engine.cfg
+        coalesce = block and cfg.admit_window_ms > 0  # the engine was idle: let a burst gather
+        t_end = time.perf_counter() + cfg.admit_window_ms * 1e-3
         while item is not None:
             prompt, params, rid, fut = item
             try:
@@ -360,6 +368,12 @@ class EngineService:
                 item = self._q.get_nowait()
             except queue.Empty:
                 item = None
+                wait = min(cfg.admit_gap_ms * 1e-3, t_end - time.perf_counter()) if coalesce else 0.0
+                if wait > 0:
+                    try:
+                        item = self._q.get(timeout=wait)
+                    except queue.Empty:
+                        item = None
 
     def _loop(self) -> None:
         eng = self.engine

@@ -90,7 +90,7 @@ class Scheduler:
                     break
                 self._take_chunk(seq, budget, plan)
                 budget -= seq.chunk
-            while budget > 0 and self.waiting and len(self.running) + len(plan.seqs) < self.cfg.max_num_seqs:
+            while budget > 0 and self.waiting and len(self.running) < self.cfg.max_num_seqs:  # admitted join running
                 seq = self.waiting[0]
                 n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens left to compute
                 if n > budget and not self.cfg.chunked_prefill and plan.seqs:

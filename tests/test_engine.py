@@ -172,3 +172,45 @@ def test_gpu_moe_decode_grouped_skinny_matches_recompute():
     assert eng.runner.graphs and "w13_pg" in eng.model.layers[0]
     _check_greedy_consistency(eng, ["why is pod default/api not ready?", "kube-system coredns " * 20, "x" * 100],
                               8, "cuda")
+
+
+def test_scheduler_admits_up_to_max_num_seqs_in_one_step():
+    """Regression: sequences admitted in this step count once against max_num_seqs."""
+    from k8s_llm_monitor_amd.engine.block_manager import BlockManager
+    from k8s_llm_monitor_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from k8s_llm_monitor_amd.engine.sequence import Sequence
+
+    s = Scheduler(SchedulerConfig(max_num_seqs=8, max_prefill_tokens=4096), BlockManager(256, use_native=False))
+    for _ in range(10):
+        s.add(Sequence(prompt_ids=list(range(20)), params=SamplingParams()))
+    p = s.schedule()
+    assert p.is_prefill and len(p.seqs) == 8 and len(s.running) == 8 and len(s.waiting) == 2
+
+
+def test_service_coalesces_a_burst_into_one_prefill():
+    """An idle engine receiving a burst (requests 1 ms apart) starts with one prefill of the
+    burst, not a lone first prompt (admission coalescing window)."""
+    import threading
+    import time
+
+    from k8s_llm_monitor_amd.engine import EngineService
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=16, max_model_len=256, num_blocks=128,
+                                 use_graphs=False, admit_gap_ms=5.0, admit_window_ms=200.0), device="cpu")
+    eng.trace = []
+    svc = EngineService(eng)
+    futs = []
+
+    def burst():
+        for i in range(8):
+            futs.append(svc.submit(f"pod-{i} OOMKilled", SamplingParams(max_tokens=2, ignore_eos=True)))
+            time.sleep(0.001)
+
+    t = threading.Thread(target=burst)
+    t.start()
+    t.join()
+    for f in futs:
+        f.result(timeout=60)
+    svc.close()
+    first = next(e for e in eng.trace if e[1] == "prefill")
+    assert first[2] == 8
