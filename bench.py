@@ -7,7 +7,9 @@ One process per GPU (torchrun launches N ranks); each rank is an independent TP=
 ``--batch`` concurrent diagnostic queries per GPU, each a synthetic cluster-state prompt in the
 reference's prompt format answered with up to ``--max-new-tokens`` tokens through the
 continuous-batching engine (prefill + hipGraph decode + sampling).  With ``--path http`` (default)
-every query is a real ``POST /api/v1/query`` to the in-process REST server; ``--path engine``
+every query is a real ``POST /api/v1/query`` to the in-process REST server, sent by a child
+load-generator process (``--client process``, default: remote clients do not share the serving
+process's interpreter lock; ``--client thread`` keeps them in-process); ``--path engine``
 submits to the engine queue directly (same engine, no HTTP).
 
 Timing: W untimed warmup waves, then a barrier + device sync, K timed waves, a device sync + barrier;
@@ -44,10 +46,20 @@ def main() -> None:
     ap.add_argument("--path", choices=["http", "engine", "podcomm"], default="http",
                     help="http: POST /api/v1/query (headline); podcomm: POST /api/v1/analyze/pod-communication "
                          "with the LLM explanation (BASELINE config 3); engine: the engine queue directly")
+    ap.add_argument("--client", choices=["process", "thread"], default="process",
+                    help="process: the HTTP clients run in a child load-generator process (remote clients; the "
+                         "serving process keeps its interpreter lock); thread: client threads in this process")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args()
+
+    loadgen = None
+    if a.path in ("http", "podcomm") and a.client == "process":
+        # started before this process initialises the GPU (the child never touches it)
+        from k8s_llm_monitor_amd.monitor.loadgen import LoadGen
+
+        loadgen = LoadGen(ROOT)
 
     import torch
 
@@ -86,7 +98,7 @@ def main() -> None:
             from k8s_llm_monitor_amd.monitor.app import post_queries
 
             items = [synthetic_context(s)[::-1] for s in seeds]  # (question, cluster context)
-            res = post_queries(port, items, a.max_new_tokens)
+            res = (loadgen.post_queries if loadgen else post_queries)(port, items, a.max_new_tokens)
             lat = [r["http_latency_ms"] for r in res]
             ptok = sum(r["prompt_tokens"] for r in res)
             gtok = sum(r["completion_tokens"] for r in res)
@@ -94,7 +106,8 @@ def main() -> None:
             from k8s_llm_monitor_amd.monitor.app import bench_pod_pairs, post_pod_communication
 
             pairs = bench_pod_pairs(a.batch * (w + 1))[a.batch * w:]
-            res = post_pod_communication(port, pairs, a.max_new_tokens)
+            res = (loadgen.post_pod_communication if loadgen else post_pod_communication)(port, pairs,
+                                                                                          a.max_new_tokens)
             lat = [r["http_latency_ms"] for r in res]
             ptok = sum(r["prompt_tokens"] for r in res)
             gtok = sum(r["completion_tokens"] for r in res)
@@ -133,6 +146,8 @@ def main() -> None:
     svc.close()
     if server is not None:
         server.shutdown()
+    if loadgen is not None:
+        loadgen.close()
     if rank == 0:
         qps = total_q / t_max
         name = _MODEL_NAMES.get(a.model, a.model)
@@ -154,7 +169,8 @@ def main() -> None:
             "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": 8192,
                        "parallelism": f"dp{world}" if world > 1 else "tp1",
                        "prompt_tokens_mean": round(ptoks / max(1, a.batch * a.steps), 1),
-                       "max_new_tokens": a.max_new_tokens, "path": a.path},
+                       "max_new_tokens": a.max_new_tokens, "path": a.path,
+                       "client": a.client if a.path != "engine" else None},
             "p50_latency_ms": round(p50, 2),
             "p99_latency_ms": round(sorted(lats)[min(len(lats) - 1, int(len(lats) * 0.99))], 2),
             "generated_tokens_per_s": round(total_gen / t_max, 1),

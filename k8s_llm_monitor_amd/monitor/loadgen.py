@@ -1,0 +1,86 @@
+"""Out-of-process HTTP load generator for the benchmarks.
+
+The serving process (REST server threads + engine loop) shares one interpreter lock; firing 64
+concurrent client requests from threads of that same process makes request arrival contend with
+the server for it (the arrival of a 64-query wave spread over ~90 ms in-process).  Real clients
+are remote, so ``bench.py`` runs them here, in a child process started before the parent touches
+the GPU (this module imports no torch and never initialises a device).
+
+Protocol: one JSON request per stdin line, one JSON reply per stdout line.
+
+    {"op": "query", "port": P, "items": [[question, context], ...], "max_new_tokens": N}
+    {"op": "podcomm", "port": P, "pairs": [[pod_a, pod_b], ...], "max_new_tokens": N}
+    -> {"ok": true, "results": [...]}   (post_queries / post_pod_communication result dicts)
+    -> {"ok": false, "error": "..."}
+"""
+from __future__ import annotations
+
+import json
+import subprocess
+import sys
+
+
+def serve(stdin=None, stdout=None) -> None:
+    from .app import post_pod_communication, post_queries
+
+    stdin = stdin or sys.stdin
+    stdout = stdout or sys.stdout
+    for line in stdin:
+        line = line.strip()
+        if not line:
+            continue
+        try:
+            req = json.loads(line)
+            if req["op"] == "query":
+                res = post_queries(req["port"], [tuple(x) for x in req["items"]], req["max_new_tokens"])
+            elif req["op"] == "podcomm":
+                res = post_pod_communication(req["port"], [tuple(x) for x in req["pairs"]], req["max_new_tokens"])
+            else:
+                raise ValueError(f"unknown op {req['op']!r}")
+            out = {"ok": True, "results": res}
+        except Exception as e:  # noqa: BLE001 - reported to the parent, which raises
+            out = {"ok": False, "error": f"{type(e).__name__}: {e}"}
+        stdout.write(json.dumps(out) + "\n")
+        stdout.flush()
+
+
+class LoadGen:
+    """Parent-side handle: a persistent child running :func:`serve`.  Start it before the parent
+    initialises the GPU."""
+
+    def __init__(self, root: str | None = None):
+        self.proc = subprocess.Popen([sys.executable, "-m", "k8s_llm_monitor_amd.monitor.loadgen"],
+                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1,
+                                     cwd=root)
+
+    def _call(self, req: dict) -> list:
+        self.proc.stdin.write(json.dumps(req) + "\n")
+        self.proc.stdin.flush()
+        line = self.proc.stdout.readline()
+        if not line:
+            raise RuntimeError(f"load generator exited (rc={self.proc.poll()})")
+        rep = json.loads(line)
+        if not rep["ok"]:
+            raise RuntimeError(f"load generator: {rep['error']}")
+        return rep["results"]
+
+    def post_queries(self, port: int, items: list, max_new_tokens: int) -> list:
+        return self._call({"op": "query", "port": port, "items": [list(x) for x in items],
+                           "max_new_tokens": max_new_tokens})
+
+    def post_pod_communication(self, port: int, pairs: list, max_new_tokens: int) -> list:
+        return self._call({"op": "podcomm", "port": port, "pairs": [list(x) for x in pairs],
+                           "max_new_tokens": max_new_tokens})
+
+    def close(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.stdin.close()
+            try:
+                self.proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+
+
+if __name__ == "__main__":
+    serve()

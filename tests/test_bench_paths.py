@@ -31,6 +31,26 @@ def test_query_path(served):
     assert all(r["completion_tokens"] == 6 and r["prompt_tokens"] > 100 for r in res)
 
 
+def test_query_path_from_loadgen_process(served):
+    """The bench's default client: a child load-generator process posting the wave."""
+    from k8s_llm_monitor_amd.monitor.loadgen import LoadGen
+
+    svc, port = served
+    lg = LoadGen(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        items = [(q, ctx[:400]) for ctx, q in (synthetic_context(s) for s in range(10, 13))]
+        res = lg.post_queries(port, items, 4)
+        assert len(res) == 3 and all(r["completion_tokens"] == 4 and r["http_latency_ms"] > 0 for r in res)
+        res = lg.post_pod_communication(port, bench_pod_pairs(2), 3)
+        assert len(res) == 2 and all(r["completion_tokens"] == 3 for r in res)
+        with pytest.raises(RuntimeError, match="unknown op"):
+            lg._call({"op": "bogus"})  # errors come back to the parent; the child keeps serving
+        assert len(lg.post_queries(port, items[:1], 2)) == 1
+    finally:
+        lg.close()
+    assert lg.proc.returncode == 0
+
+
 def test_pod_communication_path(served):
     svc, port = served
     pairs = bench_pod_pairs(3)
@@ -62,3 +82,4 @@ def test_bench_two_ranks_under_torchrun_cpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 8
     assert d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0 and d["scaling"] == "weak"
+    assert d["config"]["path"] == "http" and d["config"]["client"] == "process"
