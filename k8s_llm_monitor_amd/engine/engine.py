@@ -25,6 +25,7 @@ from typing import Optional, Union
 
 import torch
 
+from ..models.checkpoint import config_from_hf, load_checkpoint
 from ..models.config import ModelConfig, get_config
 from ..models.llama import CausalLM
 from ..parallel.comm import tp_broadcast_object
@@ -33,7 +34,7 @@ from .block_manager import BlockManager
 from .runner import ModelRunner, RunnerConfig
 from .scheduler import Scheduler, SchedulerConfig
 from .sequence import SamplingParams, Sequence, SeqStatus
-from .tokenizer import tokenizer_for
+from .tokenizer import tokenizer_for, tokenizer_from_dir
 
 
 @dataclass
@@ -58,6 +59,9 @@ class EngineConfig:
     admit_gap_ms: float = 2.0
     admit_window_ms: float = 20.0
     model_overrides: dict = field(default_factory=dict)
+    # a Hugging Face model directory (config.json, *.safetensors, optional tokenizer.json): real
+    # weights instead of the seeded random init (models/checkpoint.py); None = random init
+    weights: Optional[str] = None
 
 
 class _View:
@@ -80,12 +84,17 @@ class LLMEngine:
             device = self.ps.device if self.ps.device.type == "cuda" else (
                 "cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device)
+        if model_cfg is None and cfg.weights:
+            model_cfg = config_from_hf(cfg.weights)
         mc = model_cfg or get_config(cfg.model)
         if cfg.model_overrides:
             mc = mc.replace(**cfg.model_overrides)
         self.model_cfg = mc
         t0 = time.perf_counter()
-        self.model = CausalLM(mc, device=self.device, dtype=getattr(torch, cfg.dtype), seed=cfg.seed, pstate=self.ps)
+        self.model = CausalLM(mc, device=self.device, dtype=getattr(torch, cfg.dtype), seed=cfg.seed, pstate=self.ps,
+                              init="empty" if cfg.weights else "random")
+        if cfg.weights:
+            load_checkpoint(self.model, cfg.weights)
         self.runner = ModelRunner(self.model, RunnerConfig(
             max_num_seqs=cfg.max_num_seqs, max_model_len=cfg.max_model_len, kv_cache_gb=cfg.kv_cache_gb,
             num_blocks=cfg.num_blocks, use_graphs=cfg.use_graphs, seed=cfg.seed))
@@ -94,7 +103,7 @@ class LLMEngine:
                                                max_prefill_tokens=cfg.max_prefill_tokens,
                                                max_model_len=self.runner.max_len,
                                                chunked_prefill=cfg.chunked_prefill), self.blocks)
-        self.tokenizer = tokenizer_for(mc)
+        self.tokenizer = tokenizer_from_dir(cfg.weights, mc) if cfg.weights else tokenizer_for(mc)
         self.eos = set(mc.eos_ids)
         self.init_s = time.perf_counter() - t0
         self.counters = {"requests": 0, "finished": 0, "prompt_tokens": 0, "generated_tokens": 0,

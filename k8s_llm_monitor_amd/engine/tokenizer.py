@@ -167,3 +167,30 @@ def tokenizer_for(model_cfg, merges_path: Path = DEFAULT_MERGES) -> ByteBPEToken
     merges = merges[:max(0, room)]
     return ByteBPETokenizer(merges, bos_id=model_cfg.bos_id, eos_id=model_cfg.eos_ids[0],
                             vocab_size=model_cfg.vocab_size)
+
+
+class HFTokenizer:
+    """A Hugging Face ``tokenizer.json`` (the ``tokenizers`` library, Rust BPE) behind the same
+    encode / decode interface, for engines loading real checkpoints (EngineConfig.weights)."""
+
+    def __init__(self, path: Path, bos_id: Optional[int], eos_id: Optional[int]):
+        from tokenizers import Tokenizer
+
+        self.tok = Tokenizer.from_file(str(path))
+        self.bos_id, self.eos_id = bos_id, eos_id
+        self.vocab_size = self.tok.get_vocab_size()
+
+    def encode(self, text: str, bos: bool = True) -> list[int]:
+        ids = self.tok.encode(text, add_special_tokens=False).ids
+        return ([self.bos_id] if bos and self.bos_id is not None else []) + ids
+
+    def decode(self, ids: Iterable[int], skip_special: bool = True) -> str:
+        return self.tok.decode([int(t) for t in ids if t >= 0], skip_special_tokens=skip_special)
+
+
+def tokenizer_from_dir(path, model_cfg):
+    """``path/tokenizer.json`` as an :class:`HFTokenizer` when present, else the built-in BPE."""
+    f = Path(path) / "tokenizer.json"
+    if f.exists():
+        return HFTokenizer(f, model_cfg.bos_id, model_cfg.eos_ids[0])
+    return tokenizer_for(model_cfg)

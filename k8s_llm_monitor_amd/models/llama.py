@@ -65,7 +65,12 @@ def _seed_for(name: str, seed: int) -> int:
 
 class CausalLM:
     def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16, seed: int = 0,
-                 pstate: Optional[ParallelState] = None, init_std: float = 0.02):
+                 pstate: Optional[ParallelState] = None, init_std: float = 0.02, init: str = "random"):
+        """``init``: "random" (seeded per tensor name) or "empty" (uninitialised storage, for
+        models about to be filled by models/checkpoint.load_checkpoint)."""
+        if init not in ("random", "empty"):
+            raise ValueError(f"init must be 'random' or 'empty', not {init!r}")
+        self._empty_init = init == "empty"
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -98,6 +103,8 @@ class CausalLM:
 
     # ------------------------------------------------------------------ weights
     def _rand(self, name: str, shape, std: Optional[float] = None) -> torch.Tensor:
+        if self._empty_init:
+            return torch.empty(shape, dtype=self.dtype, device=self.device)
         g = torch.Generator(device=self.device)
         g.manual_seed(_seed_for(name, self.seed))
         t = torch.empty(shape, dtype=torch.float32 if self.device.type == "cpu" else self.dtype, device=self.device)

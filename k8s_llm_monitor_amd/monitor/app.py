@@ -70,7 +70,7 @@ def engine_config(cfg: Config):
                         kv_cache_gb=cfg.llm.kv_cache_gb, use_graphs=cfg.llm.use_graphs, seed=cfg.llm.seed,
                         tp_size=cfg.llm.tp_size, dtype=torch_dtype_name(cfg.llm.dtype),
                         max_prefill_tokens=cfg.llm.max_prefill_tokens, chunked_prefill=cfg.llm.chunked_prefill,
-                        prefix_caching=cfg.llm.prefix_caching)
+                        prefix_caching=cfg.llm.prefix_caching, weights=cfg.llm.weights or None)
 
 
 def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):

@@ -59,6 +59,7 @@ class LLMConfig:
     max_prefill_tokens: int = 16384  # token budget of one prefill step
     chunked_prefill: bool = True  # longer prompts prefill in chunks of that budget
     prefix_caching: bool = True  # reuse the KV blocks of shared prompt prefixes
+    weights: str = ""  # Hugging Face model dir (config.json + *.safetensors); "" = random init
 
 
 @dataclass
