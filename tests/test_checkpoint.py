@@ -157,3 +157,42 @@ def test_config_from_hf_transformers5_rope_parameters():
     with pytest.raises(ValueError):
         config_from_hf({"model_type": "falcon"})
     json.dumps(c.rope_scaling)
+
+
+@pytest.mark.gpu
+def test_gpu_engine_on_hf_checkpoint_matches_transformers(tmp_path):
+    """A transformers-written Llama checkpoint (head_dim 128, GQA) served by the engine on the GPU
+    in bf16 - flash prefill, hipGraph decode, skinny GEMMs, sampler - greedily generates what the
+    fp32 transformers model generates (allowing near-ties from bf16 rounding)."""
+    from k8s_llm_monitor_amd import ops
+    from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+
+    ops.native()
+    torch.manual_seed(0)
+    cfg = transformers.LlamaConfig(vocab_size=1024, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
+                                   num_attention_heads=8, num_key_value_heads=2, head_dim=128,
+                                   max_position_embeddings=1024, rope_theta=500000.0, tie_word_embeddings=False,
+                                   bos_token_id=1, eos_token_id=2)
+    hf = _randomize(transformers.LlamaForCausalLM(cfg)).float().eval()
+    with torch.no_grad():  # larger weights: decisive logits, so bf16 rounding rarely flips a choice
+        for p in hf.parameters():
+            if p.dim() == 2:
+                p.mul_(3.0)
+    hf.save_pretrained(tmp_path, safe_serialization=True)
+    eng = LLMEngine(EngineConfig(weights=str(tmp_path), max_num_seqs=4, max_model_len=512, num_blocks=64, seed=0),
+                    device="cuda:0")
+    eng.warmup()
+    prompts = [[1, 17, 33, 250, 5, 99, 140, 7, 61, 200, 3, 45] * 3, [1, 900, 12, 12, 4, 700, 31]]
+    n_new = 12
+    seqs = eng.generate(prompts, SamplingParams(max_tokens=n_new, temperature=0.0, ignore_eos=True))
+    agree = total = 0
+    for s, p in zip(seqs, prompts):
+        with torch.no_grad():
+            out = hf.generate(torch.tensor([p]), max_new_tokens=n_new, do_sample=False,
+                              attention_mask=torch.ones(1, len(p), dtype=torch.long))[0, len(p):].tolist()
+        for a, b in zip(s.output_ids, out):
+            total += 1
+            agree += int(a == b)
+            if a != b:
+                break  # the continuations diverge after the first differing token
+    assert agree >= 0.8 * total, (agree, total)
