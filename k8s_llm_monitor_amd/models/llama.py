@@ -238,6 +238,12 @@ class CausalLM:
         elif slabs is not None:
             ws, splits = slabs
             ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T, rownorm=rownorm)
+            if self._attn_rope and not meta.is_prefill and k_cache is not None and c.arch == "llama":
+                # the attention kernel reduces the slabs, applies RoPE and writes the new k / v
+                out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device)
+                return ops.paged_decode_fused(ws, ns, meta.positions, cs, meta.slot_mapping, k_cache, v_cache,
+                                              meta.block_tables, meta.seq_lens, self.hq, self.hkv, self.D, self.scale,
+                                              workspace=meta.decode_ws, out=out)
             partial = ws
             qkv = torch.empty(T, L["wqkv_p"].shape[0] * 16, dtype=self.dtype, device=self.device)
         else:
@@ -429,14 +435,17 @@ class CausalLM:
         # last arriver costs more than the launch boundary it saves, so the default keeps the pair.
         fuse = os.environ.get("K8SLLM_FUSED_EPI", "0") == "1"
         self._fuse_rope = fuse and self.D == 128
+        # decode RoPE + KV write inside the attention kernel (paged_decode_fused), reading the qkv
+        # GEMM's split-K slabs directly: one launch per layer fewer (K8SLLM_ATTN_ROPE=0 disables)
+        self._attn_rope = not self._fuse_rope and self.D == 128 and os.environ.get("K8SLLM_ATTN_ROPE", "1") != "0"
         self._fuse_resnorm = fuse and self.tp == 1 and not c.is_moe and c.d_model % 64 == 0
         if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0":
-            self._fuse_rope = self._fuse_resnorm = False
+            self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
         ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
         if d % 64 or nq % 64 or (self.hq * self.D) % 32 or ff % 64:
-            self._fuse_rope = self._fuse_resnorm = False
+            self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
             return
         for L in self.layers:
             L["wqkv_p"] = ops.pack_skinny(L["wqkv"])

@@ -573,6 +573,33 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
     return out
 
 
+def paged_decode_fused(slabs: torch.Tensor, nslabs: int, positions: torch.Tensor, cos_sin: torch.Tensor,
+                       slot_mapping: Optional[torch.Tensor], k_cache: torch.Tensor, v_cache: torch.Tensor,
+                       block_tables: torch.Tensor, seq_lens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
+                       workspace: Optional[tuple] = None, out: Optional[torch.Tensor] = None,
+                       splits: Optional[int] = None) -> torch.Tensor:
+    """paged_decode with rope_and_cache folded in: the new token's q / k / v are the sum of the qkv
+    projection's ``nslabs`` fp32 split-K slabs [nslabs, B, (Hq + 2 Hkv) * D] (skinny_slabs),
+    rounded to the cache dtype, q / k rotated at ``positions``, k / v written to the cache at
+    ``slot_mapping``; attention over the cached tokens plus the new one (D = 128 on the GPU)."""
+    B = seq_lens.shape[0]
+    if not _gpu(slabs):
+        n = (Hq + 2 * Hkv) * D
+        qkv = slabs[: nslabs * B * n].view(nslabs, B, n).sum(0).to(k_cache.dtype)
+        ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, Hq, Hkv, D, True)
+        return paged_decode(qkv, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, out=out)
+    if workspace is None:
+        workspace = decode_workspace(B, Hq, D, device=slabs.device)
+    if out is None:
+        out = torch.empty(B, Hq * D, dtype=k_cache.dtype, device=slabs.device)
+    S = splits or decode_splits(B, Hkv)
+    native().paged_decode_fused(out, slabs, nslabs, positions, cos_sin,
+                                slot_mapping if slot_mapping is not None else _empty_i32(slabs.device),
+                                k_cache, v_cache, block_tables, seq_lens, workspace[0], workspace[1], Hq, Hkv, D,
+                                scale, S)
+    return out
+
+
 def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128) -> tuple[list[int], list[int]]:
     """Q-block schedule for flash_prefill: (seq index, first q row) per 128-row block, heaviest
     (largest first row, i.e. longest causal span) first so the tail of the grid is short."""

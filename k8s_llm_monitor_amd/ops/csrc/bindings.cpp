@@ -20,6 +20,10 @@ int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const fl
 int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q, long q_stride,
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
+int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml, const float* slabs,
+                              int nslabs, const int* positions, const float* cos_sin, const int* slot_mapping,
+                              void* k_cache, void* v_cache, const int* block_tables, int bt_stride,
+                              const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
 int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride, const int* cu_seqlens,
                          const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
                          const int* ctx_start, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -184,6 +188,51 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                             block_tables.data_ptr<int>(), (int)block_tables.stride(0), seq_lens.data_ptr<int>(), B,
                             (int)Hq, (int)Hkv, (int)D, (int)splits, (float)scale, cur()),
         "paged_decode");
+}
+
+// paged_decode with the new token's q / k / v taken from the qkv projection's fp32 split-K slabs
+// [nslabs, B, (Hq + 2 Hkv) * D] (summed, rounded, RoPE at positions, k / v written to the cache at
+// slot_mapping inside the attention kernel: rope_and_cache folded in).  D = 128.
+void paged_decode_fused(torch::Tensor out, torch::Tensor slabs, int64_t nslabs, torch::Tensor positions,
+                        torch::Tensor cos_sin, torch::Tensor slot_mapping, torch::Tensor k_cache,
+                        torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor seq_lens,
+                        torch::Tensor part_out, torch::Tensor part_ml, int64_t Hq, int64_t Hkv, int64_t D,
+                        double scale, int64_t splits) {
+  dev_bf16(out, "out"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
+  dev_i32(block_tables, "block_tables"); dev_i32(seq_lens, "seq_lens"); dev_i32(positions, "positions");
+  TORCH_CHECK(D == 128, "paged_decode_fused: head_dim 128");
+  const int B = (int)seq_lens.size(0);
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == torch::kFloat32 && slabs.is_contiguous() &&
+                  slabs.numel() >= nslabs * B * (Hq + 2 * Hkv) * D && nslabs >= 1,
+              "paged_decode_fused: slabs must hold nslabs x [B, (Hq + 2 Hkv) * D] fp32");
+  TORCH_CHECK(positions.numel() >= B, "paged_decode_fused: positions [B]");
+  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == torch::kFloat32 && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == D, "paged_decode_fused: cos_sin [max_pos, D] fp32");
+  const bool has_slots = slot_mapping.numel() > 0;
+  if (has_slots) {
+    dev_i32(slot_mapping, "slot_mapping");
+    TORCH_CHECK(slot_mapping.numel() >= B, "paged_decode_fused: slot_mapping [B]");
+  }
+  const bool packed = out.dim() == 4;
+  if (packed) {
+    TORCH_CHECK(out.is_contiguous() && out.size(1) * 32 == Hq * D && out.size(2) == 64 && out.size(3) == 8 &&
+                    out.size(0) * 16 >= B, "packed out must be [ceil(B/16), Hq*D/32, 64, 8]");
+  } else {
+    TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == Hq * D, "out must be [B, Hq*D]");
+  }
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == Hkv && k_cache.size(3) == 16 && v_cache.size(3) == 16,
+              "paged_decode_fused: caches [NB, Hkv, D/8, 16, 8] / [NB, Hkv, D, 16]");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "splits must be in [1, 64]");
+  TORCH_CHECK(part_out.numel() >= (int64_t)B * Hq * splits * D && part_ml.numel() >= (int64_t)B * Hq * splits * 2,
+              "decode workspace too small for batch x splits");
+  check(k8sllm_paged_decode_fused(out.data_ptr(), packed ? -(long)(Hq * D / 32) : (long)out.stride(0),
+                                  part_out.data_ptr<float>(), part_ml.data_ptr<float>(), slabs.data_ptr<float>(),
+                                  (int)nslabs, positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                                  has_slots ? slot_mapping.data_ptr<int>() : nullptr, k_cache.data_ptr(),
+                                  v_cache.data_ptr(), block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                                  seq_lens.data_ptr<int>(), B, (int)Hq, (int)Hkv, (int)D, (int)splits, (float)scale,
+                                  cur()),
+        "paged_decode_fused");
 }
 
 // paged (optional, all or none): ctx_start [S] (cached tokens before each sequence's new rows),
@@ -605,6 +654,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("embedding", &embedding);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_decode", &paged_decode);
+  m.def("paged_decode_fused", &paged_decode_fused);
   m.def("flash_prefill", &flash_prefill);
   m.def("sample", &sample);
   m.def("moe_route", &moe_route);

@@ -39,7 +39,24 @@ __device__ __forceinline__ void split_range(int seq_len, int S, int split, int* 
   *nvalid = (nch + per - 1) / per;
 }
 
-template <int D, int G>
+// FQ (fused q/k/v, decode at TP>=1 behind the skinny qkv GEMM, D = 128): the kernel also does
+// what rope_and_cache did between the two launches - the new token's q / k / v are the sum of the
+// qkv projection's fp32 split-K slabs, rounded to bf16, q and k rotated (neox pairs) - so one
+// launch per layer disappears.  The new token is not read back from the cache: every split
+// attends to the cached tokens [0, seq_len - 1) and the split owning the last chunk folds the new
+// token into its online softmax from registers (and writes its k / v to the cache for the next
+// steps), so no workgroup waits for another's cache write.
+struct DecodeFuse {
+  const float* slabs;  // [nslabs][B][(Hq + 2 Hkv) * D] fp32
+  int nslabs;
+  const int* positions;    // [B]
+  const float* cos_sin;    // [max_pos][D]: cos | sin
+  const int* slot_mapping;  // [B], -1 = no cache write
+  bf16_t* k_cache;
+  bf16_t* v_cache;
+};
+
+template <int D, int G, bool FQ>
 __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ out, long out_stride,
                                                            float* __restrict__ part_out,  // [B][Hq][S][D]
                                                            float* __restrict__ part_ml,   // [B][Hq][S][2]
@@ -48,12 +65,14 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ seq_lens, int Hq, int Hkv, int S,
-                                                           float scale_log2) {
+                                                           float scale_log2, DecodeFuse fz) {
   constexpr int KS = D / 32;  // QK k-steps
   constexpr int DT = D / 16;  // PV output tiles (16 dims each)
   __shared__ float s_max[4][16];
   __shared__ float s_sum[4][16];
   __shared__ float s_o[4][G][D];
+  __shared__ __attribute__((aligned(16))) bf16_t s_q[FQ ? G : 1][D];  // FQ: rotated q of the group's heads
+  __shared__ __attribute__((aligned(16))) bf16_t s_kv[FQ ? 2 : 1][D];  // FQ: the new token's rotated k, v
 
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int seq_len = seq_lens[b];
@@ -71,9 +90,50 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   const long head_block = (long)D * kBS;  // elements of one (block, head) tile
   const int nblk = (seq_len + kBS - 1) / kBS;
   const int first_blk = bt[0];
+  // FQ: the cache holds tokens [0, seq_len - 1); the new token is folded in from registers
+  const int n_cached = FQ ? seq_len - 1 : seq_len;
+  const bool owns_new = FQ && c1 == (seq_len + kCH - 1) / kCH;
 
   bf16x8 qf[KS];
-  {
+  if constexpr (FQ) {
+    // q (G heads) + the new k (rotated) + v of kv head kvh from the qkv slabs: (G + 1) * D/2
+    // rotary pairs and D/2 value pairs, one item per thread
+    const int ncols = (Hq + 2 * Hkv) * D;
+    const long slab = (long)gridDim.z * ncols;
+    const float* row = fz.slabs + (long)b * ncols;
+    const float* cs = fz.cos_sin + (long)fz.positions[b] * D;
+    constexpr int HALF = D / 2;
+    for (int it = threadIdx.x; it < (G + 2) * HALF; it += 256) {
+      const int h = it / HALF, p = it - h * HALF;  // h < G: q head kvh*G+h; h == G: k; h == G+1: v
+      const int c = h < G ? (kvh * G + h) * D : (h == G ? (Hq + kvh) * D : (Hq + Hkv + kvh) * D);
+      float x1 = 0.f, x2 = 0.f;
+      for (int z = 0; z < fz.nslabs; ++z) {
+        x1 += row[z * slab + c + p];
+        x2 += row[z * slab + c + HALF + p];
+      }
+      x1 = bf2f(f2bf(x1));  // rounded as the unfused GEMM output -> rope_cache path is
+      x2 = bf2f(f2bf(x2));
+      if (h <= G) {
+        const float cc = cs[p], sn = cs[HALF + p];
+        const float o1 = x1 * cc - x2 * sn, o2 = x2 * cc + x1 * sn;
+        x1 = o1;
+        x2 = o2;
+      }
+      bf16_t* dst = h < G ? s_q[h] : s_kv[h - G];
+      dst[p] = f2bf(x1);
+      dst[HALF + p] = f2bf(x2);
+    }
+    __syncthreads();
+    const int hc = col < G ? col : 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(&s_q[hc][32 * s + 8 * kg]);
+    const int slot = fz.slot_mapping != nullptr ? fz.slot_mapping[b] : -1;
+    if (owns_new && slot >= 0 && threadIdx.x < D) {  // the new token's k / v for the next steps
+      const int blk = slot / kBS, off = slot - blk * kBS, d = threadIdx.x;
+      fz.k_cache[(((long)blk * Hkv + kvh) * (D / 8) + (d >> 3)) * (kBS * 8) + off * 8 + (d & 7)] = s_kv[0][d];
+      fz.v_cache[(((long)blk * Hkv + kvh) * D + d) * kBS + off] = s_kv[1][d];
+    }
+  } else {
     const int hc = col < G ? col : 0;
     const bf16_t* qp = q + (long)b * q_stride + (long)(kvh * G + hc) * D;
 #pragma unroll
@@ -129,7 +189,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = wtok0 + 16 * i + 4 * kg + r;
-        const float v = (t < seq_len) ? sacc[i][r] * scale_log2 : -INFINITY;
+        const float v = (t < n_cached) ? sacc[i][r] * scale_log2 : -INFINITY;
         sacc[i][r] = v;
         mx = fmaxf(mx, v);
       }
@@ -167,6 +227,32 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
             __builtin_bit_cast(bf16x8, make_uint4(vlo[s][dt].x, vlo[s][dt].y, vhi[s][dt].x, vhi[s][dt].y));
         oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[dt], 0, 0, 0);
       }
+    }
+  }
+
+  if constexpr (FQ) {
+    // the new token, folded into wave 0's online softmax: score per head from the LDS copies (the
+    // 4 lanes of a head column each take 32 dims), then the usual rescale + p * v_new update
+    if (owns_new && wave == 0) {
+      const int hc = col < G ? col : 0;
+      float sc = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < D / 4; ++j) {
+        const int d = kg * (D / 4) + j;
+        sc += bf2f(s_q[hc][d]) * bf2f(s_kv[0][d]);
+      }
+      sc += __shfl_xor(sc, 16, 64);
+      sc += __shfl_xor(sc, 32, 64);
+      sc *= scale_log2;
+      const float mnew = fmaxf(m, sc);
+      const float alpha = exp2f(m - mnew);
+      const float pn = bf2f(f2bf(exp2f(sc - mnew)));  // P enters the PV product as bf16
+      l = l * alpha + pn;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) oacc[dt][r] = oacc[dt][r] * alpha + pn * bf2f(s_kv[1][16 * dt + 4 * kg + r]);
     }
   }
 
@@ -250,6 +336,15 @@ using namespace k8sllm;
 
 // S = number of splits per (sequence, kv head); part buffers hold [B][Hq][S][D].
 // out_stride < 0: write the output fragment-packed for gemm_skinny (common.h act_index).
+// slabs != nullptr: the fused q/k/v form (D = 128; see DecodeFuse) - q is ignored, the new token's
+// q / k / v come from the qkv projection's nslabs fp32 slabs [nslabs][B][(Hq + 2 Hkv) * D], are
+// rotated at `positions` and k / v written to the cache at `slot_mapping` (nullptr: no write).
+extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml,
+                                         const float* slabs, int nslabs, const int* positions, const float* cos_sin,
+                                         const int* slot_mapping, void* k_cache, void* v_cache,
+                                         const int* block_tables, int bt_stride, const int* seq_lens, int B, int Hq,
+                                         int Hkv, int D, int S, float scale, hipStream_t s);
+
 extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q,
                                    long q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                                    int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int S,
@@ -258,11 +353,12 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
   if (S < 1 || S > 64) return -2;
   const int G = Hq / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
+  const DecodeFuse fz{};
   dim3 grid(S, Hkv, B), blk(256);
 #define K8S_DEC(DD, GG)                                                                                              \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, part_ml,    \
-                     (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,       \
-                     bt_stride, seq_lens, Hq, Hkv, S, sl2);                                                          \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, false>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out,      \
+                     part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,            \
+                     block_tables, bt_stride, seq_lens, Hq, Hkv, S, sl2, fz);                                        \
   if (S > 1)                                                                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,      \
                        part_out, part_ml, seq_lens, Hq, S);
@@ -287,5 +383,35 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
     return -1;
   }
 #undef K8S_DEC
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml,
+                                         const float* slabs, int nslabs, const int* positions, const float* cos_sin,
+                                         const int* slot_mapping, void* k_cache, void* v_cache,
+                                         const int* block_tables, int bt_stride, const int* seq_lens, int B, int Hq,
+                                         int Hkv, int D, int S, float scale, hipStream_t s) {
+  if (B <= 0) return 0;
+  if (S < 1 || S > 64) return -2;
+  if (D != 128 || slabs == nullptr || nslabs < 1 || positions == nullptr || cos_sin == nullptr) return -3;
+  const int G = Hq / Hkv;
+  const float sl2 = scale * 1.4426950408889634f;
+  const DecodeFuse fz{slabs, nslabs, positions, cos_sin, slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache};
+  dim3 grid(S, Hkv, B), blk(256);
+#define K8S_DECF(GG)                                                                                                 \
+  hipLaunchKernelGGL((paged_decode_kernel<128, GG, true>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out,      \
+                     part_ml, nullptr, 0, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride,   \
+                     seq_lens, Hq, Hkv, S, sl2, fz);                                                                 \
+  if (S > 1)                                                                                                         \
+    hipLaunchKernelGGL((paged_decode_reduce_kernel<128, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,     \
+                       part_out, part_ml, seq_lens, Hq, S);
+  switch (G) {
+    case 1: K8S_DECF(1); break;
+    case 2: K8S_DECF(2); break;
+    case 4: K8S_DECF(4); break;
+    case 8: K8S_DECF(8); break;
+    default: return -1;
+  }
+#undef K8S_DECF
   return (int)hipGetLastError();
 }

@@ -125,6 +125,38 @@ def test_paged_decode_zero_len_rows():
     _close(y, r.to(DEV), atol=2e-2, rtol=2e-2, what="paged_decode pad rows")
 
 
+@pytest.mark.parametrize("lens,hq,hkv,splits,nslabs", [([1, 2, 17, 256, 257, 1800], 32, 8, None, 2),
+                                                        ([300, 77, 1024, 513], 32, 8, 4, 3),
+                                                        ([40, 600], 64, 8, 2, 1), ([129, 64], 8, 8, None, 2)])
+def test_paged_decode_fused_matches_rope_then_decode(lens, hq, hkv, splits, nslabs):
+    """paged_decode_fused (slab reduce + RoPE + KV write + attention over cache + new token in
+    one kernel) == rope_and_cache from the slabs, then paged_decode - outputs and cache contents."""
+    d, bs = 128, 16
+    B = len(lens)
+    max_blocks = (max(lens) + bs - 1) // bs + 1
+    nb = B * max_blocks + 4
+    kc, vc = _make_cache(nb, hkv, d, bs)
+    lens_t = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    bt = torch.randperm(nb, device=DEV)[: B * max_blocks].view(B, max_blocks).to(torch.int32)
+    pos = lens_t - 1
+    slots = torch.stack([bt[b, (lens[b] - 1) // bs] * bs + (lens[b] - 1) % bs for b in range(B)]).to(torch.int32)
+    n = (hq + 2 * hkv) * d
+    slabs = torch.randn(nslabs, B, n, device=DEV, dtype=torch.float32) * 0.5
+    cs = ref.rope_cos_sin(4096, d, 500000.0, None, device=DEV)
+    scale = 1.0 / math.sqrt(d)
+    kc2, vc2 = kc.clone(), vc.clone()
+    y = ops.paged_decode_fused(slabs.reshape(-1), nslabs, pos, cs, slots, kc, vc, bt, lens_t, hq, hkv, d, scale,
+                               splits=splits)
+    qkv = torch.empty(B, n, device=DEV, dtype=torch.bfloat16)
+    ops.rope_and_cache(qkv, pos, cs, kc2, vc2, slots, hq, hkv, d, partial=slabs.reshape(-1), nslabs=nslabs)
+    r = ops.paged_decode(qkv, kc2, vc2, bt, lens_t, hq, hkv, d, scale, splits=splits)
+    _close(kc, kc2, atol=1e-2, rtol=1e-2, what="k cache")
+    _close(vc, vc2, atol=1e-2, rtol=1e-2, what="v cache")
+    _close(y, r, atol=2e-2, rtol=2e-2, what="fused decode vs rope + decode")
+    rr = ref.paged_decode(qkv.cpu(), kc2.cpu(), vc2.cpu(), bt.cpu(), lens_t.cpu(), hq, hkv, d, scale)
+    _close(y.cpu(), rr, atol=2e-2, rtol=2e-2, what="fused decode vs fp32 reference")
+
+
 @pytest.mark.parametrize("lens,hq,hkv", [([1], 32, 8), ([128], 32, 8), ([300, 77, 1024], 32, 8),
                                          ([513, 200], 64, 8), ([129, 64], 8, 8)])
 def test_flash_prefill(lens, hq, hkv):
@@ -291,8 +323,10 @@ def test_llama_decode_skinny_matches_generic(monkeypatch, fused):
     lens = torch.tensor([3, 17, 1, 30, 9], dtype=torch.int32, device=DEV)
     bt = torch.arange(B * 2, dtype=torch.int32, device=DEV).view(B, 2) % nb
     ids = torch.randint(0, cfg.vocab_size, (B,), dtype=torch.int32, device=DEV)
-    meta = AttnMeta(is_prefill=False, positions=lens - 1, slot_mapping=torch.full((B,), -1, dtype=torch.int32,
-                                                                                 device=DEV),
+    # the new token's slot inside each sequence's last block (decode rows always write the cache;
+    # the fused attention reads the new token from registers, the generic path from the cache)
+    slots = torch.stack([bt[b, (int(lens[b]) - 1) // bs] * bs + (int(lens[b]) - 1) % bs for b in range(B)])
+    meta = AttnMeta(is_prefill=False, positions=lens - 1, slot_mapping=slots.to(torch.int32),
                     block_tables=bt, seq_lens=lens,
                     decode_ws=ops.decode_workspace(B, m.hq, m.D, device=DEV, Hkv=m.hkv))
     a = m.forward(ids, meta, kv).float()
