@@ -94,6 +94,37 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   const int n_cached = FQ ? seq_len - 1 : seq_len;
   const bool owns_new = FQ && c1 == (seq_len + kCH - 1) / kCH;
 
+  // ---- every K and V load of a wave's 64 tokens of chunk c, issued up front (32 KiB per wave)
+  bf16x8 kf[4][KS];
+  uint2 vlo[2][DT], vhi[2][DT];
+  auto issue = [&](int c) {
+    const int wtok0 = c * kCH + wave * 64;
+    int phys[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int bi = (wtok0 >> 4) + i;
+      phys[i] = bi < nblk ? bt[bi] : first_blk;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[i][s] = *reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
+      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        vlo[s][dt] = *reinterpret_cast<const uint2*>(va + 16 * dt * kBS);
+        vhi[s][dt] = *reinterpret_cast<const uint2*>(vb + 16 * dt * kBS);
+      }
+    }
+  };
+  // the first chunk's K/V loads fly while q is loaded (FQ: reduced from the slabs and rotated)
+  issue(c0);
+
   bf16x8 qf[KS];
   if constexpr (FQ) {
     // q (G heads) + the new k (rotated) + v of kv head kvh from the qkv slabs: (G + 1) * D/2
@@ -147,31 +178,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
 
   for (int c = c0; c < c1; ++c) {
     const int wtok0 = c * kCH + wave * 64;
-    int phys[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int bi = (wtok0 >> 4) + i;
-      phys[i] = bi < nblk ? bt[bi] : first_blk;
-    }
-    // ---- issue every K and V load of this wave's 64 tokens up front
-    bf16x8 kf[4][KS];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) kf[i][s] = *reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8);
-    }
-    uint2 vlo[2][DT], vhi[2][DT];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
-      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        vlo[s][dt] = *reinterpret_cast<const uint2*>(va + 16 * dt * kBS);
-        vhi[s][dt] = *reinterpret_cast<const uint2*>(vb + 16 * dt * kBS);
-      }
-    }
+    if (c != c0) issue(c);  // chunk c0's loads were issued before the q prologue
     __builtin_amdgcn_sched_barrier(0);  // keep every load above: none may wait behind an MFMA
 
     // ---- scores, online softmax (per lane: head `col`)

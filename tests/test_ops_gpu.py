@@ -317,7 +317,7 @@ def test_llama_decode_skinny_matches_generic(monkeypatch, fused):
     m = CausalLM(cfg, device=DEV, seed=3)
     assert m._skinny_ws is not None and m._fuse_resnorm == (fused == "1")
     B, bs = 5, 16
-    nb = 8
+    nb = 2 * B  # no block shared between sequences (as the block manager guarantees for written blocks)
     kv = [(torch.randn(nb, m.hkv, m.D // 8, bs, 8, device=DEV, dtype=torch.bfloat16),
            torch.randn(nb, m.hkv, m.D, bs, device=DEV, dtype=torch.bfloat16)) for _ in m.layers]
     lens = torch.tensor([3, 17, 1, 30, 9], dtype=torch.int32, device=DEV)
