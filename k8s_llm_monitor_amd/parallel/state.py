@@ -74,10 +74,15 @@ def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optio
     """Initialise torch.distributed (if WORLD_SIZE > 1) and carve the TP / DP groups.
 
     ``device`` defaults to ``cuda:<local_rank>`` when a GPU is visible, else CPU (gloo).
+    Rehearsal overrides (several ranks sharing one GPU, e.g. the DP bench under torchrun on a
+    1-GPU box): ``K8SLLM_DEVICE`` pins every rank's device, ``K8SLLM_DIST_BACKEND`` picks the
+    process-group backend (gloo: RCCL refuses two ranks on one device).
     """
     import datetime
 
     ws, rank, lr = env_world()
+    device = device or os.environ.get("K8SLLM_DEVICE") or None
+    backend = backend or os.environ.get("K8SLLM_DIST_BACKEND") or None
     if device is None:
         device = f"cuda:{lr}" if torch.cuda.is_available() else "cpu"
     dev = torch.device(device)
