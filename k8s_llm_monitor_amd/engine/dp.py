@@ -93,8 +93,9 @@ def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
         except EOFError:
             break
         if kind == "req":
-            prompt, params, rid = body
-            fut = svc.submit(prompt, SamplingParams(**params), rid)
+            prompt, params, rid, stream = body if len(body) == 4 else (*body, False)
+            cb = (lambda ids, k=key: send(("tok", k, ids))) if stream else None
+            fut = svc.submit(prompt, SamplingParams(**params), rid, on_tokens=cb)
             fut.add_done_callback(lambda f, k=key: on_done(k, f))
         elif kind == "stats":
             send(("stats", key, svc.stats()))
@@ -130,6 +131,7 @@ class ReplicaRouter:
         self.engine = _EngineInfo(engine_cfg.model, engine_cfg.model_overrides)
         self._keys = itertools.count()
         self._pending: dict = {}
+        self._streams: dict = {}  # key -> on_tokens of streaming requests
         self._lock = threading.Lock()
         self._error: Optional[str] = None
         self.latencies_ms: list = []
@@ -159,7 +161,9 @@ class ReplicaRouter:
 
     # ------------------------------------------------------------------ EngineService API
     def submit(self, prompt: Union[str, list], params: Optional[SamplingParams] = None,
-               request_id: Optional[str] = None) -> Future:
+               request_id: Optional[str] = None, on_tokens=None) -> Future:
+        """As EngineService.submit; ``on_tokens`` is called on the router's reader thread with the
+        token ids the replica streams back (``tok`` messages) before the answer arrives."""
         fut: Future = Future()
         if self._error is not None:
             fut.set_exception(RuntimeError(f"replica failed: {self._error}"))
@@ -172,7 +176,9 @@ class ReplicaRouter:
             r.outstanding += 1
             r.submitted += 1
             self._pending[key] = (fut, r)
-        r.send(("req", key, (prompt, p, request_id)))
+            if on_tokens is not None:
+                self._streams[key] = on_tokens
+        r.send(("req", key, (prompt, p, request_id, on_tokens is not None)))
         return fut
 
     def _read(self, r: _Replica) -> None:
@@ -181,9 +187,18 @@ class ReplicaRouter:
                 kind, key, body = r.conn.recv()
             except (EOFError, OSError):
                 break
+            if kind == "tok":
+                cb = self._streams.get(key)
+                if cb is not None:
+                    try:
+                        cb(body)
+                    except Exception:  # noqa: BLE001 - a broken consumer must not stop the reader
+                        pass
+                continue
             if kind in ("done", "fail"):
                 with self._lock:
                     fut, _ = self._pending.pop(key, (None, None))
+                    self._streams.pop(key, None)
                     r.outstanding -= 1
                 if fut is None:
                     continue

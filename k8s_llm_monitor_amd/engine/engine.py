@@ -348,15 +348,18 @@ class EngineService:
         self._lock = threading.Lock()
         self._error: Optional[BaseException] = None
         self.latencies_ms: list[float] = []
+        self._streams: dict = {}  # seq_id -> [seq, tokens delivered, on_tokens]
         self._thread.start()
 
     def submit(self, prompt: Union[str, list[int]], params: Optional[SamplingParams] = None,
-               request_id: Optional[str] = None) -> Future:
+               request_id: Optional[str] = None, on_tokens=None) -> Future:
+        """``on_tokens(ids)`` (optional, streaming): called on the engine thread with each batch of
+        newly generated token ids, before the future resolves; keep it cheap (e.g. a queue put)."""
         fut: Future = Future()
         if self._error is not None:
             fut.set_exception(RuntimeError(f"engine failed: {self._error!r}"))
             return fut
-        self._q.put((prompt, params, request_id, fut))
+        self._q.put((prompt, params, request_id, fut, on_tokens))
         return fut
 
     def _drain(self, block: bool) -> None:
@@ -368,9 +371,11 @@ class EngineService:
         coalesce = block and cfg.admit_window_ms > 0  # the engine was idle: let a burst gather
         t_end = time.perf_counter() + cfg.admit_window_ms * 1e-3
         while item is not None:
-            prompt, params, rid, fut = item
+            prompt, params, rid, fut, on_tokens = item
             try:
-                self.engine.add_request(prompt, params, rid, user=fut)
+                seq = self.engine.add_request(prompt, params, rid, user=fut)
+                if on_tokens is not None:
+                    self._streams[seq.seq_id] = [seq, 0, on_tokens]
             except Exception as e:  # noqa: BLE001 - reject this request only
                 fut.set_exception(e)
             try:
@@ -384,6 +389,24 @@ class EngineService:
                     except queue.Empty:
                         item = None
 
+    def _push_streams(self) -> None:
+        for sid, st in list(self._streams.items()):
+            seq, sent, cb = st
+            out = seq.output_ids
+            n = len(out)
+            while n > sent and out[n - 1] < 0:  # pipelined decode: placeholders until read back
+                n -= 1
+            if any(t < 0 for t in out[sent:n]):
+                n = sent + next(i for i, t in enumerate(out[sent:n]) if t < 0)
+            if n > sent:
+                st[1] = n
+                try:
+                    cb(list(seq.output_ids[sent:n]))
+                except Exception:  # noqa: BLE001 - a broken consumer must not stop the engine
+                    pass
+            if seq.status in (SeqStatus.FINISHED, SeqStatus.ABORTED):
+                del self._streams[sid]
+
     def _loop(self) -> None:
         eng = self.engine
         try:
@@ -391,7 +414,10 @@ class EngineService:
                 self._drain(block=not eng.has_work())
                 if not eng.has_work():
                     continue
-                for seq in eng.step():
+                finished = eng.step()
+                if self._streams:
+                    self._push_streams()
+                for seq in finished:
                     fut = seq.user
                     if isinstance(fut, Future) and not fut.done():
                         self.latencies_ms.append(seq.timings()["latency_ms"])

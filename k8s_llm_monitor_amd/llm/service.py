@@ -68,6 +68,73 @@ class LocalEngineBackend:
         return GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason, **t)
 
 
+    def stream(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
+               request_id: Optional[str] = None, ignore_eos: bool = False):
+        """Generator: text deltas (str) as the engine produces tokens, then the final GenResult.
+        The engine thread only enqueues token ids; detokenization runs here, incrementally (a
+        sliding window, so the cost per token does not grow with the answer)."""
+        import queue
+
+        from ..engine import SamplingParams
+
+        d = self.default
+        p = SamplingParams(max_tokens=max_tokens or d.max_tokens,
+                           temperature=d.temperature if temperature is None else temperature,
+                           top_k=d.top_k, top_p=d.top_p, ignore_eos=ignore_eos)
+        q: queue.SimpleQueue = queue.SimpleQueue()
+        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id, on_tokens=q.put)
+        det = IncrementalDetokenizer(self.tokenizer)
+        deadline = time.monotonic() + self.timeout_s if self.timeout_s > 0 else None
+        while True:
+            try:
+                ids = q.get(timeout=0.05)
+            except queue.Empty:
+                if fut.done() and q.empty():
+                    break
+                if deadline is not None and time.monotonic() > deadline:
+                    raise TimeoutError("llm.timeout exceeded while streaming")
+                continue
+            delta = det.add(ids)
+            if delta:
+                yield delta
+        text, seq = fut.result()
+        tail = det.flush()
+        if tail:
+            yield tail
+        yield GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason,
+                        **seq.timings())
+
+
+class IncrementalDetokenizer:
+    """Token ids -> text deltas for streaming: each call re-decodes only the ids since the previous
+    emission boundary (prefix / read offsets, so the cost per token does not grow with the answer)
+    and holds output back while the text ends inside a multi-byte UTF-8 character (U+FFFD)."""
+
+    def __init__(self, tokenizer):
+        self.tok = tokenizer
+        self.ids: list[int] = []
+        self.prefix = 0  # start of the previously emitted chunk (a character boundary)
+        self.read = 0  # ids already emitted as text
+
+    def add(self, ids) -> str:
+        self.ids.extend(int(t) for t in ids)
+        prev = self.tok.decode(self.ids[self.prefix:self.read])
+        cur = self.tok.decode(self.ids[self.prefix:])
+        if len(cur) <= len(prev) or cur.endswith("\ufffd"):
+            return ""
+        self.prefix, self.read = self.read, len(self.ids)
+        return cur[len(prev):]
+
+    def flush(self) -> str:
+        """Whatever is still held back (the answer ended inside a character)."""
+        if self.read == len(self.ids):
+            return ""
+        prev = self.tok.decode(self.ids[self.prefix:self.read])
+        cur = self.tok.decode(self.ids[self.prefix:])
+        self.prefix, self.read = self.read, len(self.ids)
+        return cur[len(prev):]
+
+
 class OpenAIBackend:
     provider = "openai"
 
@@ -218,6 +285,35 @@ class AnalysisService:
                                     error=f"{type(e).__name__}: {e}", timestamp=utcnow())
         self.store.put(resp)
         return resp
+
+    def query_stream(self, question: str, max_tokens: Optional[int] = None, ignore_eos: bool = False,
+                     context_text: Optional[str] = None):
+        """Streaming form of :meth:`query` (``"stream": true``): yields text deltas, then the stored
+        AnalysisResponse.  Backends without token streaming yield the whole answer as one delta."""
+        rid = uuid.uuid4().hex
+        ctx = context_text if context_text else self.cluster_context()
+        prompt = P.build_query_prompt(ctx, question)
+        extra = {"question": question}
+        mt = max_tokens or self.max_tokens
+        try:
+            if hasattr(self.backend, "stream"):
+                g = None
+                for item in self.backend.stream(prompt, max_tokens=mt, request_id=rid, ignore_eos=ignore_eos):
+                    if isinstance(item, str):
+                        yield item
+                    else:
+                        g = item
+            else:
+                g = self.backend.generate(prompt, max_tokens=mt, request_id=rid, ignore_eos=ignore_eos)
+                yield g["text"]
+            result = {"type": "query", "answer": g.pop("text"), **g, **extra}
+            resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
+        except Exception as e:  # noqa: BLE001 - an engine failure becomes an error record
+            log.error("analysis %s failed: %s", rid, e)
+            resp = AnalysisResponse(request_id=rid, status="error", result={"type": "query", **extra},
+                                    error=f"{type(e).__name__}: {e}", timestamp=utcnow())
+        self.store.put(resp)
+        yield resp
 
     def query(self, question: str, max_tokens: Optional[int] = None, ignore_eos: bool = False,
               context_text: Optional[str] = None) -> AnalysisResponse:

@@ -3,7 +3,9 @@
 All 15 reference routes with their status codes, error strings and Go-``encoding/json`` bodies,
 plus the analysis routes the reference only advertised or planned:
 
-  POST /api/v1/query                       {"question", ["max_tokens"]} -> AnalysisResponse
+  POST /api/v1/query                       {"question", ["max_tokens"], ["stream"]} -> AnalysisResponse
+                                           ("stream": true -> text/event-stream: {"delta"} events,
+                                           then event "done" carrying the AnalysisResponse)
   POST /api/v1/analyze                     AnalysisRequest {"type", "parameters", "context"}
   GET  /api/v1/analysis[/<request_id>]     stored AnalysisResponse records
   GET  /api/v1/metrics/engine              engine queue / batch / KV-cache / latency stats
@@ -56,6 +58,24 @@ def _bounded_pool():
 class Reply(Exception):
     def __init__(self, code: int, body: bytes, ctype: str, headers: Optional[dict] = None):
         self.code, self.body, self.ctype, self.headers = code, body, ctype, headers or {}
+
+
+class StreamReply(Reply):
+    """A reply whose body is produced incrementally (``chunks``: an iterator of bytes), written with
+    HTTP/1.1 chunked transfer encoding - the Server-Sent Events stream of ``"stream": true``."""
+
+    def __init__(self, code: int, chunks, ctype: str = "text/event-stream", headers: Optional[dict] = None):
+        super().__init__(code, b"", ctype, headers)
+        self.chunks = chunks
+
+    def collect(self) -> bytes:
+        """The whole stream (transport-free callers and tests)."""
+        return b"".join(self.chunks)
+
+
+def sse_event(data, event: Optional[str] = None) -> bytes:
+    body = data if isinstance(data, (bytes, bytearray)) else gojson.encode(data).rstrip(b"\n")
+    return (b"event: " + event.encode() + b"\n" if event else b"") + b"data: " + bytes(body) + b"\n\n"
 
 
 def http_error(code: int, msg: str) -> Reply:
@@ -316,6 +336,18 @@ class MonitorApp:
         ctx_text = ctx.get("cluster_state") if isinstance(ctx, dict) else None
         if ctx_text is not None and not isinstance(ctx_text, str):
             raise http_error(400, "context.cluster_state must be a string")
+        if d.get("stream") is True:  # Server-Sent Events: {"delta"} events, then event "done" = the record
+            gen = self.analysis.query_stream(question, max_tokens=mt, ignore_eos=bool(d.get("ignore_eos", False)),
+                                             context_text=ctx_text)
+
+            def events():
+                for item in gen:
+                    if isinstance(item, str):
+                        yield sse_event({"delta": item})
+                    else:
+                        yield sse_event(item, "done")
+
+            return StreamReply(200, events(), headers={"Cache-Control": "no-cache"})
         try:
             resp = self._bounded(lambda: self.analysis.query(question, max_tokens=mt,
                                                              ignore_eos=bool(d.get("ignore_eos", False)),
@@ -435,6 +467,18 @@ class _Handler(BaseHTTPRequestHandler):
         for k, v in r.headers.items():
             self.send_header(k, v)
         self.send_header("Date", self.date_time_string())
+        if isinstance(r, StreamReply):
+            self.send_header("Transfer-Encoding", "chunked")
+            self.end_headers()
+            try:
+                for chunk in r.chunks:
+                    if chunk:
+                        self.wfile.write(b"%x\r\n%s\r\n" % (len(chunk), chunk))
+                        self.wfile.flush()
+                self.wfile.write(b"0\r\n\r\n")
+            except (BrokenPipeError, ConnectionResetError):  # client went away mid-stream
+                self.close_connection = True
+            return
         self.send_header("Content-Length", str(len(r.body)))
         self.end_headers()
         if method != "HEAD":

@@ -39,6 +39,11 @@ def test_router_backs_local_engine_backend_concurrently():
         with cf.ThreadPoolExecutor(8) as ex:
             res = list(ex.map(lambda i: be.generate(f"node-{i} NotReady", ignore_eos=True), range(8)))
         assert all(r["completion_tokens"] == 3 and r["provider"] == "local-rocm" for r in res)
+        # streaming through the router: the replica forwards token batches over its pipe
+        items = list(be.stream("node-9 NotReady", max_tokens=5, ignore_eos=True))
+        final = items[-1]
+        assert final["completion_tokens"] == 5
+        assert "".join(x for x in items[:-1] if isinstance(x, str)) == final["text"]
     finally:
         router.close()
 

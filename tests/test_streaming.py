@@ -1,0 +1,87 @@
+"""Token streaming: engine per-request token callbacks, the incremental detokenizer, and
+``POST /api/v1/query {"stream": true}`` as Server-Sent Events over chunked HTTP/1.1."""
+import http.client
+import json
+
+import pytest
+
+from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
+from k8s_llm_monitor_amd.engine.tokenizer import tokenizer_for
+from k8s_llm_monitor_amd.llm.service import IncrementalDetokenizer
+from k8s_llm_monitor_amd.models.config import get_config
+
+
+def test_incremental_detokenizer_multibyte():
+    tok = tokenizer_for(get_config("llama-3-8b"))
+    text = "集群状态概览: node-001 CPU=93.1% [资源压力] 为什么我的pod频繁重启？ 🚀 done"
+    ids = tok.encode(text, bos=False)
+    det = IncrementalDetokenizer(tok)
+    out = []
+    for t in ids:  # one token at a time, as a decode step delivers them
+        d = det.add([t])
+        assert "�" not in d
+        out.append(d)
+    out.append(det.flush())
+    assert "".join(out) == tok.decode(ids) == text
+
+
+@pytest.fixture(scope="module")
+def engine_service():
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=1024, num_blocks=256,
+                                 use_graphs=False, seed=3), device="cpu")
+    svc = EngineService(eng)
+    yield svc
+    svc.close()
+
+
+def test_engine_service_streams_every_token_in_order(engine_service):
+    got = []
+    fut = engine_service.submit("pod default/api CrashLoopBackOff", SamplingParams(max_tokens=9, temperature=0.0,
+                                                                                    ignore_eos=True),
+                                on_tokens=got.append)
+    text, seq = fut.result(timeout=120)
+    flat = [t for chunk in got for t in chunk]
+    assert flat == seq.output_ids and len(flat) == 9
+    plain, seq2 = engine_service.submit("pod default/api CrashLoopBackOff",
+                                        SamplingParams(max_tokens=9, temperature=0.0, ignore_eos=True)).result(120)
+    assert seq2.output_ids == seq.output_ids  # streaming does not change the answer
+
+
+def test_query_stream_over_http():
+    from k8s_llm_monitor_amd.monitor.app import build_app_for_bench
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=8192, num_blocks=2048,
+                                 use_graphs=False, seed=1), device="cpu")
+    svc = EngineService(eng)
+    srv, port = build_app_for_bench(svc)
+    try:
+        body = json.dumps({"question": "为什么我的pod频繁重启？", "max_tokens": 7, "ignore_eos": True, "stream": True,
+                           "context": {"cluster_state": "node-001 CPU=93.1% [资源压力]"}})
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=300)
+        conn.request("POST", "/api/v1/query", body, {"Content-Type": "application/json"})
+        r = conn.getresponse()
+        assert r.status == 200
+        assert r.getheader("Content-Type") == "text/event-stream"
+        assert r.getheader("Transfer-Encoding") == "chunked"
+        raw = r.read().decode()  # http.client de-chunks
+        conn.close()
+        events = [e for e in raw.split("\n\n") if e.strip()]
+        deltas, done = [], None
+        for e in events:
+            lines = e.split("\n")
+            if lines[0] == "event: done":
+                done = json.loads(lines[1][len("data: "):])
+            else:
+                deltas.append(json.loads(lines[0][len("data: "):])["delta"])
+        assert done is not None and done["status"] == "success"
+        assert done["result"]["completion_tokens"] == 7
+        assert "".join(deltas) == done["result"]["answer"]
+        # the streamed record is stored like a synchronous one
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        conn.request("GET", f"/api/v1/analysis/{done['request_id']}")
+        rec = json.loads(conn.getresponse().read())
+        conn.close()
+        assert rec["status"] == "success" and rec["data"]["request_id"] == done["request_id"]
+    finally:
+        svc.close()
+        srv.shutdown()
