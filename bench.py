@@ -204,6 +204,10 @@ def _print_trace(trace: list, t0: float) -> None:
             cur = []
         cur.append(e)
     waves.append(cur)
+    subs = [e[0] for e in ev if e[1] == "submit"]
+    if subs:
+        print(f"[trace] submits {len(subs)}: " + " ".join(f"{(t - t0) * 1e3:.0f}" for t in subs[:200]), file=sys.stderr)
+        print("[trace] adds: " + " ".join(f"{(e[0] - t0) * 1e3:.0f}" for e in adds[:200]), file=sys.stderr)
     for w in waves:
         gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
         print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"

@@ -359,6 +359,9 @@ class EngineService:
         if self._error is not None:
             fut.set_exception(RuntimeError(f"engine failed: {self._error!r}"))
             return fut
+        tr = self.engine.trace
+        if tr is not None:
+            tr.append((time.perf_counter(), "submit", 1, 0))
         self._q.put((prompt, params, request_id, fut, on_tokens))
         return fut
 
