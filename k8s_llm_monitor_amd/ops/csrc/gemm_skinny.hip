@@ -219,7 +219,7 @@ __device__ __forceinline__ void skinny_fused_tail(const float* __restrict__ part
 }
 
 template <int MT, int NT, int EPI, bool APK, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
+__global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
                                                           int kchunk, const float* __restrict__ rn_ss, int rn_nc,
