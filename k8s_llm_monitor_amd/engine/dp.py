@@ -78,7 +78,12 @@ def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
         with send_lock:
             conn.send(msg)
 
+    live: dict = {}  # key -> local future of requests still running
+
     def on_done(key: int, fut: Future) -> None:
+        if fut.cancelled():
+            send(("fail", key, "cancelled"))
+            return
         try:
             text, seq = fut.result()
             send(("done", key, {"text": text, "timings": seq.timings(), "finish_reason": seq.finish_reason,
@@ -96,7 +101,12 @@ def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
             prompt, params, rid, stream = body if len(body) == 4 else (*body, False)
             cb = (lambda ids, k=key: send(("tok", k, ids))) if stream else None
             fut = svc.submit(prompt, SamplingParams(**params), rid, on_tokens=cb)
-            fut.add_done_callback(lambda f, k=key: on_done(k, f))
+            live[key] = fut
+            fut.add_done_callback(lambda f, k=key: (live.pop(k, None), on_done(k, f)))
+        elif kind == "cancel":
+            f = live.get(key)
+            if f is not None:
+                svc.cancel(f)
         elif kind == "stats":
             send(("stats", key, svc.stats()))
         elif kind == "close":
@@ -181,6 +191,16 @@ class ReplicaRouter:
         r.send(("req", key, (prompt, p, request_id, on_tokens is not None)))
         return fut
 
+    def cancel(self, fut: Future) -> bool:
+        """Abort a submitted request (its replica drops the sequence and frees its KV)."""
+        with self._lock:
+            key = next((k for k, (f, _) in self._pending.items() if f is fut), None)
+            rep = self._pending[key][1] if key is not None else None
+        if key is None or not fut.cancel():
+            return False
+        rep.send(("cancel", key, None))
+        return True
+
     def _read(self, r: _Replica) -> None:
         while True:
             try:
@@ -201,6 +221,8 @@ class ReplicaRouter:
                     self._streams.pop(key, None)
                     r.outstanding -= 1
                 if fut is None:
+                    continue
+                if fut.done():  # cancelled by the caller
                     continue
                 if kind == "done":
                     seq = RemoteSeq(body)

@@ -336,6 +336,10 @@ def _params_t(p: SamplingParams) -> tuple:
     return (p.max_tokens, p.temperature, p.top_k, p.top_p, p.ignore_eos, tuple(p.stop_token_ids))
 
 
+class _Skip(Exception):
+    pass
+
+
 class EngineService:
     """Runs an LLMEngine on its own thread; thread-safe ``submit`` returns a Future that resolves
     to ``(text, sequence)``."""
@@ -349,6 +353,8 @@ class EngineService:
         self._error: Optional[BaseException] = None
         self.latencies_ms: list[float] = []
         self._streams: dict = {}  # seq_id -> [seq, tokens delivered, on_tokens]
+        self._cancels: queue.SimpleQueue = queue.SimpleQueue()  # futures whose requests to abort
+        self.cancelled = 0
         self._thread.start()
 
     def submit(self, prompt: Union[str, list[int]], params: Optional[SamplingParams] = None,
@@ -365,6 +371,29 @@ class EngineService:
         self._q.put((prompt, params, request_id, fut, on_tokens))
         return fut
 
+    def cancel(self, fut: Future) -> bool:
+        """Abort the request behind ``fut`` (e.g. its streaming client disconnected): the future
+        is cancelled at once; the engine thread drops the sequence and frees its KV blocks before
+        its next step.  False if the answer was already complete."""
+        if not fut.cancel():
+            return False
+        self._cancels.put(fut)
+        return True
+
+    def _apply_cancels(self) -> None:
+        eng = self.engine
+        futs = set()
+        while True:
+            try:
+                futs.add(self._cancels.get_nowait())
+            except queue.Empty:
+                break
+        for s in list(eng.sched.running) + list(eng.sched.waiting):
+            if s.user in futs:
+                eng.abort(s)
+                self._streams.pop(s.seq_id, None)
+                self.cancelled += 1
+
     def _drain(self, block: bool) -> None:
         try:
             item = self._q.get(block=block, timeout=0.05 if block else None)
@@ -376,9 +405,13 @@ class EngineService:
         while item is not None:
             prompt, params, rid, fut, on_tokens = item
             try:
+                if fut.cancelled():  # cancelled while queued
+                    raise _Skip()
                 seq = self.engine.add_request(prompt, params, rid, user=fut)
                 if on_tokens is not None:
                     self._streams[seq.seq_id] = [seq, 0, on_tokens]
+            except _Skip:
+                pass
             except Exception as e:  # noqa: BLE001 - reject this request only
                 fut.set_exception(e)
             try:
@@ -414,6 +447,8 @@ class EngineService:
         eng = self.engine
         try:
             while not self._stop.is_set():
+                if not self._cancels.empty():
+                    self._apply_cancels()
                 self._drain(block=not eng.has_work())
                 if not eng.has_work():
                     continue
@@ -439,6 +474,7 @@ class EngineService:
             d["p50_latency_ms"] = lat[len(lat) // 2]
             d["p99_latency_ms"] = lat[min(len(lat) - 1, int(len(lat) * 0.99))]
         d["queue_depth"] = self._q.qsize()
+        d["cancelled"] = self.cancelled
         d["healthy"] = self._error is None
         return d
 

@@ -85,18 +85,22 @@ class LocalEngineBackend:
         fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id, on_tokens=q.put)
         det = IncrementalDetokenizer(self.tokenizer)
         deadline = time.monotonic() + self.timeout_s if self.timeout_s > 0 else None
-        while True:
-            try:
-                ids = q.get(timeout=0.05)
-            except queue.Empty:
-                if fut.done() and q.empty():
-                    break
-                if deadline is not None and time.monotonic() > deadline:
-                    raise TimeoutError("llm.timeout exceeded while streaming")
-                continue
-            delta = det.add(ids)
-            if delta:
-                yield delta
+        try:
+            while True:
+                try:
+                    ids = q.get(timeout=0.05)
+                except queue.Empty:
+                    if fut.done() and q.empty():
+                        break
+                    if deadline is not None and time.monotonic() > deadline:
+                        raise TimeoutError("llm.timeout exceeded while streaming")
+                    continue
+                delta = det.add(ids)
+                if delta:
+                    yield delta
+        finally:
+            if not fut.done() and hasattr(self.svc, "cancel"):  # consumer gone / timed out: free the KV
+                self.svc.cancel(fut)
         text, seq = fut.result()
         tail = det.flush()
         if tail:

@@ -134,6 +134,7 @@ class MonitorApp:
                 "/api/v1/analyze": self.analyze,
                 "/api/v1/analysis": self.analysis_list,
                 "/api/v1/metrics/engine": self.metrics_engine,
+                "/metrics": self.prometheus,
             }
             fn = exact.get(path)
             if fn is not None:
@@ -341,11 +342,14 @@ class MonitorApp:
                                              context_text=ctx_text)
 
             def events():
-                for item in gen:
-                    if isinstance(item, str):
-                        yield sse_event({"delta": item})
-                    else:
-                        yield sse_event(item, "done")
+                try:
+                    for item in gen:
+                        if isinstance(item, str):
+                            yield sse_event({"delta": item})
+                        else:
+                            yield sse_event(item, "done")
+                finally:
+                    gen.close()  # a client that went away cancels the generation
 
             return StreamReply(200, events(), headers={"Cache-Control": "no-cache"})
         try:
@@ -401,6 +405,12 @@ class MonitorApp:
             raise http_error(503, "LLM engine not available")
         return json_reply({"status": "success", "data": self.engine_service.stats(), "timestamp": utcnow()}, cors=True)
 
+    def prometheus(self, method, body, q) -> Reply:
+        """Prometheus text exposition (new; the reference only discussed an exporter,
+        docs/uav-collection-summary.md:63-86): HTTP, engine and cluster gauges / counters."""
+        _only(method, "GET")
+        return Reply(200, prometheus_text(self).encode(), "text/plain; version=0.0.4; charset=utf-8")
+
     # ------------------------------------------------------------------ static files
     def static(self, method, path) -> Reply:
         rel = "index.html" if path == "/" else path.lstrip("/")
@@ -415,6 +425,56 @@ class MonitorApp:
         if ctype.startswith("text/"):
             ctype += "; charset=utf-8"
         return Reply(200, data, ctype)
+
+
+_ENGINE_COUNTERS = {"requests": "requests admitted", "finished": "requests finished",
+                    "prompt_tokens": "prompt tokens admitted", "generated_tokens": "tokens generated",
+                    "prefill_steps": "prefill steps run", "decode_steps": "decode steps run",
+                    "preemptions": "sequences preempted (recompute)", "cancelled": "requests cancelled"}
+_ENGINE_GAUGES = {"waiting": "sequences waiting", "running": "sequences running",
+                  "queue_depth": "requests queued before admission", "kv_blocks_total": "KV-cache blocks",
+                  "kv_blocks_free": "free KV-cache blocks", "kv_usage": "KV-cache block usage (0-1)",
+                  "p50_latency_ms": "p50 request latency (ms, last 4096)",
+                  "p99_latency_ms": "p99 request latency (ms, last 4096)", "healthy": "engine thread healthy",
+                  "dp_replicas": "engine replicas behind the router"}
+_CLUSTER_GAUGES = ("total_nodes", "healthy_nodes", "total_pods", "running_pods", "total_cpu", "used_cpu",
+                   "cpu_usage_rate", "total_memory", "used_memory", "memory_usage_rate", "total_gpus",
+                   "available_gpus")
+
+
+def prometheus_text(app: "MonitorApp") -> str:
+    out: list = []
+
+    def metric(name: str, kind: str, help_: str, value, labels: str = "") -> None:
+        if isinstance(value, bool):
+            value = int(value)
+        if not isinstance(value, (int, float)):
+            return
+        out.append(f"# HELP {name} {help_}\n# TYPE {name} {kind}\n{name}{labels} {value}")
+
+    metric("k8sllm_http_requests_total", "counter", "HTTP requests handled", app.requests)
+    if app.engine_service is not None:
+        try:
+            st = app.engine_service.stats()
+        except Exception:  # noqa: BLE001 - a sick engine still exports its health
+            st = {"healthy": False}
+        model = str(st.get("model", "")).replace('"', "")
+        lab = f'{{model="{model}"}}' if model else ""
+        for k, h in _ENGINE_COUNTERS.items():
+            metric(f"k8sllm_engine_{k}_total", "counter", h, st.get(k), lab)
+        for k, h in _ENGINE_GAUGES.items():
+            metric(f"k8sllm_engine_{k}", "gauge", h, st.get(k), lab)
+    if app.manager is not None:
+        try:
+            cm = app.manager.get_cluster_metrics()
+        except Exception:  # noqa: BLE001
+            cm = None
+        if cm is not None:
+            for k in _CLUSTER_GAUGES:
+                metric(f"k8sllm_cluster_{k}", "gauge", f"cluster {k.replace('_', ' ')}", getattr(cm, k, None))
+            metric("k8sllm_cluster_healthy", "gauge", "cluster health_status == healthy",
+                   int(getattr(cm, "health_status", "") == "healthy"))
+    return "\n".join(out) + "\n"
 
 
 def _only(method: str, allowed: str) -> None:
@@ -478,6 +538,7 @@ class _Handler(BaseHTTPRequestHandler):
                 self.wfile.write(b"0\r\n\r\n")
             except (BrokenPipeError, ConnectionResetError):  # client went away mid-stream
                 self.close_connection = True
+                r.chunks.close()
             return
         self.send_header("Content-Length", str(len(r.body)))
         self.end_headers()

@@ -44,6 +44,17 @@ def test_router_backs_local_engine_backend_concurrently():
         final = items[-1]
         assert final["completion_tokens"] == 5
         assert "".join(x for x in items[:-1] if isinstance(x, str)) == final["text"]
+        # a streaming consumer that goes away cancels the request in its replica
+        be_long = LocalEngineBackend(router, max_tokens=200, temperature=0.0, timeout_s=120)
+        g = be_long.stream("node-10 NotReady " * 8, ignore_eos=True)
+        assert next(x for x in g if isinstance(x, str))
+        g.close()
+        import time
+
+        t0 = time.time()
+        while sum(r.get("cancelled", 0) for r in router.stats()["replicas"]) < 1 and time.time() - t0 < 30:
+            time.sleep(0.05)
+        assert sum(r.get("cancelled", 0) for r in router.stats()["replicas"]) == 1
     finally:
         router.close()
 

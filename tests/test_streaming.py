@@ -85,3 +85,69 @@ def test_query_stream_over_http():
     finally:
         svc.close()
         srv.shutdown()
+
+
+def test_cancel_frees_the_sequence(engine_service):
+    eng = engine_service.engine
+    free0 = eng.sched.blocks.num_free
+    got = []
+    fut = engine_service.submit("node-003 NotReady " * 20, SamplingParams(max_tokens=400, temperature=0.0,
+                                                                          ignore_eos=True), on_tokens=got.append)
+    import time
+
+    t0 = time.time()
+    while not got and time.time() - t0 < 60:  # wait until it is decoding
+        time.sleep(0.01)
+    assert got
+    assert engine_service.cancel(fut) and fut.cancelled()
+    t0 = time.time()
+    while (eng.sched.running or eng.sched.waiting) and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert not eng.sched.running and not eng.sched.waiting
+    assert eng.sched.blocks.num_free == free0  # its KV blocks went back to the pool
+    assert engine_service.stats()["cancelled"] >= 1
+    # the engine keeps serving
+    text, seq = engine_service.submit("ok?", SamplingParams(max_tokens=3, temperature=0.0,
+                                                            ignore_eos=True)).result(60)
+    assert len(seq.output_ids) == 3
+
+
+def test_stream_consumer_going_away_cancels(engine_service):
+    from k8s_llm_monitor_amd.llm.service import LocalEngineBackend
+
+    be = LocalEngineBackend(engine_service, max_tokens=500, temperature=0.0, timeout_s=60)
+    before = engine_service.stats()["cancelled"]
+    g = be.stream("pod default/db OOMKilled " * 10, ignore_eos=True)
+    first = next(x for x in g if isinstance(x, str))
+    assert first
+    g.close()  # what the HTTP handler does when the client disconnects
+    import time
+
+    t0 = time.time()
+    while engine_service.stats()["cancelled"] == before and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert engine_service.stats()["cancelled"] == before + 1
+
+
+def test_prometheus_metrics_endpoint(engine_service):
+    from k8s_llm_monitor_amd.monitor.cluster.client import K8sClient
+    from k8s_llm_monitor_amd.monitor.cluster.fake import FakeCluster
+    from k8s_llm_monitor_amd.monitor.config import from_dict
+    from k8s_llm_monitor_amd.monitor.metrics.manager import ManagerConfig, MetricsManager
+    from k8s_llm_monitor_amd.monitor.server import MonitorApp
+
+    fake = FakeCluster.build(seed=0)
+    cfg = from_dict({})
+    mgr = MetricsManager(fake, ManagerConfig(namespaces=["default"]))
+    mgr.collect()
+    app = MonitorApp(K8sClient(fake, cfg.k8s), mgr, None, engine_service)
+    r = app.handle("GET", "/metrics")
+    assert r.code == 200 and r.ctype.startswith("text/plain; version=0.0.4")
+    text = r.body.decode()
+    assert "# TYPE k8sllm_engine_generated_tokens_total counter" in text
+    assert 'k8sllm_engine_healthy{model="llama-tiny"} 1' in text
+    assert "k8sllm_cluster_total_nodes " in text and "k8sllm_http_requests_total 1" in text
+    for line in text.splitlines():  # every sample line is `name[{labels}] number`
+        if not line.startswith("#"):
+            float(line.rsplit(" ", 1)[1])
+    assert app.handle("POST", "/metrics").code == 405
