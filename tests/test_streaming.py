@@ -151,3 +151,43 @@ def test_prometheus_metrics_endpoint(engine_service):
         if not line.startswith("#"):
             float(line.rsplit(" ", 1)[1])
     assert app.handle("POST", "/metrics").code == 405
+
+
+@pytest.mark.gpu
+def test_gpu_streaming_and_cancel_with_graphs():
+    """Token streaming and cancellation on the GPU engine (hipGraph decode, pipelined readback)."""
+    import time
+
+    import torch
+
+    from k8s_llm_monitor_amd import ops
+
+    ops.native()
+    eng = LLMEngine(EngineConfig(model="llama-tiny-d128", max_num_seqs=8, max_model_len=1024, num_blocks=256,
+                                 seed=0), device="cuda:0")
+    eng.warmup()
+    svc = EngineService(eng)
+    try:
+        sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+        got = []
+        text, seq = svc.submit("pod default/api CrashLoopBackOff", sp, on_tokens=got.append).result(120)
+        assert [t for c in got for t in c] == seq.output_ids and len(seq.output_ids) == 24
+        _, seq2 = svc.submit("pod default/api CrashLoopBackOff", sp).result(120)
+        assert seq2.output_ids == seq.output_ids
+        free0 = eng.sched.blocks.num_free
+        got = []
+        fut = svc.submit("node-003 NotReady " * 10, SamplingParams(max_tokens=900, temperature=0.0, ignore_eos=True),
+                         on_tokens=got.append)
+        t0 = time.time()
+        while not got and time.time() - t0 < 60:
+            time.sleep(0.005)
+        assert svc.cancel(fut)
+        t0 = time.time()
+        while (eng.sched.running or eng.sched.waiting) and time.time() - t0 < 30:
+            time.sleep(0.005)
+        assert eng.sched.blocks.num_free == free0
+        _, seq3 = svc.submit("pod default/api CrashLoopBackOff", sp).result(120)
+        assert seq3.output_ids == seq.output_ids  # no state leaked from the cancelled request
+        torch.cuda.synchronize()
+    finally:
+        svc.close()
