@@ -54,7 +54,9 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
   const int cst = PAGED ? ctx_start[seq] : 0;  // absolute position of query row 0
   const int LK = cst + L;                      // keys: positions [0, LK)
   const int* bt = PAGED ? block_tables + (long)seq * bt_stride : nullptr;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform (SGPR): the causal tile skip and the diagonal-mask test become scalar branches
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int myq = qs + wave * 32 + r32;
   const bf16_t* base = qkv + (long)s0 * qkv_stride;
@@ -149,39 +151,47 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
       }
     }
 
+    // scores stay unscaled: the running max is kept in the log2 domain and the scale is folded
+    // into the exponent (one v_fma per score instead of a v_mul + v_sub); exponentials are the raw
+    // v_exp_f32 (arguments are <= 0, flushing tiny results to 0 is what a softmax wants) instead of
+    // exp2f's denormal-range wrapper (cmp + 2 cndmask + ldexp around every v_exp)
     const bool need_mask = (k0 + 63 > wave_q0) || (k0 + 64 > LK);
-    float mx = -1e30f;
+    if (need_mask) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kv = k0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (kv > cst + myq || kv >= LK) sacc[i][r] = -1e30f;
+        }
+    }
+    float mx = sacc[0][0];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = sacc[i][r] * scale_log2;
-        if (need_mask) {
-          const int kv = k0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (kv > cst + myq || kv >= LK) v = -1e30f;
-        }
-        sacc[i][r] = v;
-        mx = fmaxf(mx, v);
-      }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[i][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float alpha = exp2f(m - mnew);
+    const float mnew = fmaxf(m, mx * scale_log2);
+    const float alpha = __builtin_amdgcn_exp2f(m - mnew);
     float rs = 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(sacc[i][r] - mnew);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i][r], scale_log2, -mnew));
         sacc[i][r] = p;
         rs += p;
       }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
+    const bool grew = __builtin_amdgcn_ballot_w64(mnew > m) != 0;  // lazy rescale: O only when a max moved
     m = mnew;
+    if (grew) {
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
 
 #pragma unroll
     for (int i = 0; i < 2; ++i)
