@@ -151,7 +151,7 @@ def load_checkpoint(model, path: PathLike, strict: bool = True) -> list[str]:
     used: set[str] = set()
     c, dev, dt = model.cfg, model.device, model.dtype
     D, tp, r = model.D, model.tp, model.rank
-    from ..parallel.comm import shard_range
+    from ..parallel.comm import kv_head_range, shard_range
 
     def get(k: str) -> torch.Tensor:
         used.add(k)
@@ -167,7 +167,7 @@ def load_checkpoint(model, path: PathLike, strict: bool = True) -> list[str]:
         return put(w[model.v_lo:model.v_hi])
 
     q_lo, q_hi = shard_range(c.n_heads * D, tp, r)
-    kv_lo, kv_hi = shard_range(c.n_kv_heads * D, tp, r)
+    kv_lo, kv_hi = kv_head_range(c.n_kv_heads, D, tp, r)
     f_lo, f_hi = shard_range(c.ffn_dim, tp, r)
 
     if c.arch == "gpt2":

@@ -34,7 +34,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import reference as ref
-from ..parallel.comm import shard_range, tp_all_gather_last, tp_all_gather_rows, tp_all_reduce, tp_all_to_all
+from ..parallel.comm import kv_head_range, shard_range, tp_all_gather_last, tp_all_gather_rows, tp_all_reduce, tp_all_to_all
 from ..parallel.state import ParallelState, get_state
 from .config import ModelConfig
 
@@ -77,11 +77,12 @@ class CausalLM:
         self.seed = seed
         self.ps = pstate or get_state()
         tp, r = self.ps.tp_size, self.ps.tp_rank
-        if cfg.n_heads % tp or cfg.n_kv_heads % tp or cfg.ffn_dim % tp or cfg.vocab_size_padded(tp) % tp:
+        kv_ok = cfg.n_kv_heads % tp == 0 or tp % cfg.n_kv_heads == 0  # shard, or replicate (kv_head_range)
+        if cfg.n_heads % tp or not kv_ok or cfg.ffn_dim % tp or cfg.vocab_size_padded(tp) % tp:
             raise ValueError(f"{cfg.name}: heads/ffn/vocab not divisible by tp={tp}")
         self.tp, self.rank = tp, r
         self.hq = cfg.n_heads // tp
-        self.hkv = cfg.n_kv_heads // tp
+        self.hkv = max(1, cfg.n_kv_heads // tp)
         self.D = cfg.head_dim
         self.f_local = cfg.ffn_dim // tp
         self.vocab_padded = cfg.vocab_size_padded(tp)
@@ -136,7 +137,7 @@ class CausalLM:
         else:
             self.final_norm = self._ones(d)
         q_lo, q_hi = shard_range(c.n_heads * D, tp, r)
-        kv_lo, kv_hi = shard_range(c.n_kv_heads * D, tp, r)
+        kv_lo, kv_hi = kv_head_range(c.n_kv_heads, D, tp, r)
         f_lo, f_hi = shard_range(c.ffn_dim, tp, r)
         for i in range(c.n_layers):
             p = f"layers.{i}."

@@ -92,6 +92,22 @@ def shard_range(n: int, parts: int, idx: int) -> tuple[int, int]:
     return idx * s, (idx + 1) * s
 
 
+def kv_head_range(n_kv_heads: int, head_dim: int, parts: int, idx: int) -> tuple[int, int]:
+    """Rows [lo, hi) of the K (or V) projection held by TP rank ``idx``.
+
+    ``n_kv_heads % parts == 0``: contiguous shards of n_kv_heads / parts heads.  Fewer KV heads
+    than ranks (e.g. 8 KV heads at TP 16, or the 2-KV-head test models at TP 4): each KV head is
+    replicated on ``parts / n_kv_heads`` consecutive ranks - rank r holds head r // (parts /
+    n_kv_heads), which is exactly the KV head of its query heads (the query heads of one GQA group
+    are contiguous and split over those same ranks), so attention stays rank-local."""
+    if n_kv_heads % parts == 0:
+        return shard_range(n_kv_heads * head_dim, parts, idx)
+    if parts % n_kv_heads != 0:
+        raise ValueError(f"{n_kv_heads} KV heads cannot be sharded or replicated over tp_size {parts}")
+    h = idx // (parts // n_kv_heads)
+    return h * head_dim, (h + 1) * head_dim
+
+
 def all_reduce_max_scalar(v: float, group: Optional[object] = None) -> float:
     """Max of a host float over the whole world (bench timing: max over ranks)."""
     if not (dist.is_available() and dist.is_initialized()):

@@ -1,4 +1,4 @@
-"""Tensor parallelism on CPU (gloo, world_size 2): the TP-sharded model must reproduce the
+"""Tensor parallelism on CPU (gloo, world_size 2 and 4): the TP-sharded model must reproduce the
 unsharded one (column/row-parallel linears, vocab-parallel embedding + LM head, expert-parallel
 MoE), and the TP engine (leader schedules, worker mirrors via broadcast) must generate the same
 tokens as a single-rank engine."""
@@ -62,12 +62,14 @@ def _worker(rank, world, port, model, q):
         q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny", "gpt2-tiny"])
-def test_tp2_matches_tp1(model):
+@pytest.mark.parametrize("model,world", [("llama-tiny", 2), ("mixtral-tiny", 2), ("gpt2-tiny", 2),
+                                         # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
+                                         ("llama-tiny", 4), ("mixtral-tiny", 4)])
+def test_tp_matches_tp1(model, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, model, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
