@@ -61,20 +61,19 @@ class ModelRunner:
         B = cfg.max_num_seqs
         self.B = B
         dev = self.device
-        # static decode inputs (graph inputs)
-        self.d_ids = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.d_pos = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.d_slots = torch.full((B,), -1, dtype=torch.int32, device=dev)
-        self.d_bt = torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, device=dev)
-        self.d_lens = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.d_temp = torch.zeros(B, dtype=torch.float32, device=dev)
-        self.d_topk = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.d_topp = torch.ones(B, dtype=torch.float32, device=dev)
+        # static decode inputs (graph inputs): views of ONE device buffer laid out like the pinned
+        # host staging (_Staging), so a step's inputs go over in a single host-to-device copy
+        self.d_all = torch.zeros(_Staging.size(B, self.max_blocks_per_seq), dtype=torch.int32, device=dev)
+        (self.d_ids, self.d_src, self.d_pos, self.d_slots, self.d_lens, self.d_topk, self.d_temp, self.d_topp,
+         self.d_bt) = _Staging.views(self.d_all, B, self.max_blocks_per_seq)
+        self.d_src.fill_(-1)
+        self.d_slots.fill_(-1)
+        self.d_topp.fill_(1.0)
+        self.d_rids = torch.zeros(B, dtype=torch.int32, device=dev)  # resolved input ids (graph-internal)
         self.rng = torch.tensor([cfg.seed, 0], dtype=torch.int64, device=dev)
         self.d_out = torch.zeros(B, dtype=torch.int32, device=dev)
         self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev, model.hkv) \
             if self.is_gpu else None
-        self.d_src = torch.full((B,), -1, dtype=torch.int32, device=dev)
         # pinned host staging, double-buffered: with pipelined decode the host fills step N+1's
         # inputs while step N's host-to-device copies may still be queued
         self.stage = [_Staging(B, self.max_blocks_per_seq, self.is_gpu) for _ in range(2)]
@@ -149,8 +148,7 @@ class ModelRunner:
         # pipelined decode: a row whose input is the token sampled by the previous step (still in
         # flight when this step was enqueued) takes it from d_out on the device (d_src = its row
         # there); other rows take the host-provided id
-        src = self.d_src[:b]
-        ids = torch.where(src >= 0, self.d_out.index_select(0, src.clamp(min=0).long()), self.d_ids[:b])
+        ids = ops.resolve_ids(self.d_ids[:b], self.d_src[:b], self.d_out, out=self.d_rids[:b])
         logits = self.model.forward(ids, meta, self.kv)
         self._sample(logits, self.d_temp[:b], self.d_topk[:b], self.d_topp[:b], out=self.d_out[:b])
 
@@ -217,16 +215,8 @@ class ModelRunner:
             temp[n:b] = 0
             topk[n:b] = 0
             topp[n:b] = 1
-        nb = True
-        self.d_ids[:b].copy_(st.h_ids[:b], non_blocking=nb)
-        self.d_src[:b].copy_(st.h_src[:b], non_blocking=nb)
-        self.d_pos[:b].copy_(st.h_pos[:b], non_blocking=nb)
-        self.d_slots[:b].copy_(st.h_slots[:b], non_blocking=nb)
-        self.d_lens[:b].copy_(st.h_lens[:b], non_blocking=nb)
-        self.d_bt[:b].copy_(st.h_bt[:b], non_blocking=nb)
-        self.d_temp[:b].copy_(st.h_temp[:b], non_blocking=nb)
-        self.d_topk[:b].copy_(st.h_topk[:b], non_blocking=nb)
-        self.d_topp[:b].copy_(st.h_topp[:b], non_blocking=nb)
+        n_el = _Staging.prefix(self.B, self.max_blocks_per_seq, b)  # the per-row fields + b block-table rows
+        self.d_all[:n_el].copy_(st.h_all[:n_el], non_blocking=True)
         g = self.graphs.get(b)
         if g is not None:
             g.replay()
@@ -256,16 +246,38 @@ class ModelRunner:
 
 
 class _Staging:
-    """Pinned host buffers for one decode step's inputs, with numpy views for cheap writes."""
+    """Pinned host buffer for one decode step's inputs, with numpy views for cheap writes.
+
+    One int32 buffer holds every field - ids, src, pos, slots, lens, top_k, temperature and top_p
+    ([B] each; the two float fields bit-cast) followed by the block tables [B, max_blocks] - so the
+    step's inputs reach the device in ONE copy of the per-row fields plus the live block-table rows
+    (nine separate small copies were nine blit kernels of ~4.6 us each in front of every decode
+    graph replay)."""
+
+    NFIELDS = 8
+
+    @staticmethod
+    def size(B: int, max_blocks: int) -> int:
+        return _Staging.NFIELDS * B + B * max_blocks
+
+    @staticmethod
+    def prefix(B: int, max_blocks: int, b: int) -> int:
+        return _Staging.NFIELDS * B + b * max_blocks
+
+    @staticmethod
+    def views(buf, B: int, max_blocks: int) -> tuple:
+        """(ids, src, pos, slots, lens, topk, temp, topp, bt) views of a buffer (torch or numpy)."""
+        f = [buf[i * B:(i + 1) * B] for i in range(_Staging.NFIELDS)]
+        as_f32 = (lambda a: a.view(torch.float32)) if isinstance(buf, torch.Tensor) else (lambda a: a.view(np.float32))
+        f[6], f[7] = as_f32(f[6]), as_f32(f[7])
+        bt = buf[_Staging.NFIELDS * B:_Staging.size(B, max_blocks)]
+        bt = bt.view(B, max_blocks) if isinstance(buf, torch.Tensor) else bt.reshape(B, max_blocks)
+        return (*f, bt)
 
     def __init__(self, B: int, max_blocks: int, pin: bool):
-        z = lambda *shape, dt=torch.int32: torch.zeros(*shape, dtype=dt, pin_memory=pin)  # noqa: E731
-        self.h_ids, self.h_pos, self.h_slots, self.h_lens, self.h_src = z(B), z(B), z(B), z(B), z(B)
-        self.h_bt = z(B, max_blocks)
-        self.h_temp, self.h_topk, self.h_topp = z(B, dt=torch.float32), z(B), z(B, dt=torch.float32)
-        self.n_ids, self.n_pos, self.n_slots = self.h_ids.numpy(), self.h_pos.numpy(), self.h_slots.numpy()
-        self.n_lens, self.n_src, self.n_bt = self.h_lens.numpy(), self.h_src.numpy(), self.h_bt.numpy()
-        self.n_temp, self.n_topk, self.n_topp = self.h_temp.numpy(), self.h_topk.numpy(), self.h_topp.numpy()
+        self.h_all = torch.zeros(self.size(B, max_blocks), dtype=torch.int32, pin_memory=pin)
+        (self.n_ids, self.n_src, self.n_pos, self.n_slots, self.n_lens, self.n_topk, self.n_temp, self.n_topp,
+         self.n_bt) = self.views(self.h_all.numpy(), B, max_blocks)
 
 
 @dataclass

@@ -498,6 +498,18 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int = 0,
     return out
 
 
+def resolve_ids(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode input ids under pipelining: ``prev[src[i]]`` where ``src[i] >= 0`` (the token the
+    previous step sampled in that row, still on the device), else ``ids[i]``."""
+    if not _gpu(ids):
+        return torch.where(src >= 0, prev.index_select(0, src.clamp(min=0).long()), ids)
+    if out is None:
+        out = torch.empty_like(ids)
+    native().resolve_ids(out, ids, src, prev)
+    return out
+
+
 # ---------------------------------------------------------------- attention
 
 def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,

@@ -14,6 +14,7 @@ int k8sllm_silu_mul(void* out, const void* x, long rows, int F, hipStream_t s);
 int k8sllm_gelu_tanh(void* out, const void* x, long n, hipStream_t s);
 int k8sllm_embedding(void* out, const int* ids, const void* weight, long T, int d, int vocab_start, int rows,
                      hipStream_t s);
+int k8sllm_resolve_ids(int* out, const int* ids, const int* src, const int* prev, int n, hipStream_t s);
 int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, void* k_cache,
                       void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D, int block_size,
                       int apply_rope, const float* partial, int S, hipStream_t s);
@@ -130,6 +131,16 @@ void embedding(torch::Tensor out, torch::Tensor ids, torch::Tensor weight, int64
   check(k8sllm_embedding(out.data_ptr(), ids.data_ptr<int>(), weight.data_ptr(), ids.numel(), d, (int)vocab_start,
                          (int)weight.size(0), cur()),
         "embedding");
+}
+
+void resolve_ids(torch::Tensor out, torch::Tensor ids, torch::Tensor src, torch::Tensor prev) {
+  dev_i32(out, "out"); dev_i32(ids, "ids"); dev_i32(src, "src"); dev_i32(prev, "prev");
+  TORCH_CHECK(out.is_contiguous() && ids.is_contiguous() && src.is_contiguous() && prev.is_contiguous(),
+              "resolve_ids: contiguous");
+  TORCH_CHECK(ids.numel() == out.numel() && src.numel() == out.numel(), "resolve_ids: sizes");
+  check(k8sllm_resolve_ids(out.data_ptr<int>(), ids.data_ptr<int>(), src.data_ptr<int>(), prev.data_ptr<int>(),
+                           (int)out.numel(), cur()),
+        "resolve_ids");
 }
 
 void rope_and_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, torch::Tensor k_cache,
@@ -652,6 +663,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("silu_mul", &silu_mul);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("embedding", &embedding);
+  m.def("resolve_ids", &resolve_ids);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);

@@ -151,6 +151,18 @@ __global__ __launch_bounds__(256) void embedding_kernel(bf16_t* __restrict__ out
   for (int i = threadIdx.x; i < (d >> 3); i += 256) dst[i] = in ? src[i] : make_uint4(0, 0, 0, 0);
 }
 
+// Pipelined decode input ids: row i feeds prev[src[i]] (the token the previous, possibly still
+// running, step sampled in row src[i]) when src[i] >= 0, else the host-provided ids[i].  One launch
+// in the decode graph instead of torch's clamp / cast / index_select / compare / where chain.
+__global__ __launch_bounds__(64) void resolve_ids_kernel(int* __restrict__ out, const int* __restrict__ ids,
+                                                         const int* __restrict__ src, const int* __restrict__ prev,
+                                                         int n) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const int r = src[i];
+  out[i] = r >= 0 ? prev[r] : ids[i];
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
@@ -219,6 +231,12 @@ int k8sllm_embedding(void* out, const int* ids, const void* weight, long T, int 
   if (d % 8 != 0) return -1;
   hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, s, (bf16_t*)out, ids, (const bf16_t*)weight, d,
                      vocab_start, rows);
+  return (int)hipGetLastError();
+}
+
+int k8sllm_resolve_ids(int* out, const int* ids, const int* src, const int* prev, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(resolve_ids_kernel, dim3((n + 63) / 64), dim3(64), 0, s, out, ids, src, prev, n);
   return (int)hipGetLastError();
 }
 

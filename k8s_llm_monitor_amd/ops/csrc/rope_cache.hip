@@ -126,6 +126,74 @@ __global__ __launch_bounds__(128) void rope_cache_kernel(bf16_t* __restrict__ qk
   }
 }
 
+// Prefill KV-cache write (the non-SLAB path; rope_cache_kernel then only rotates q / k in place).
+// A token-per-workgroup write scatters V badly: the V^T cache rows ([D][BS] per block) take one
+// token's 128 dims as 128 two-byte stores 32 B apart, and the measured prefill chunk spent 2/3 of
+// rope_and_cache there (tools/bench_rope_cache.py: 174 us with the cache write vs 57 us rope only,
+// 16k tokens).  Here one workgroup owns the cache-block RUNS that start in its 16-token window (a run
+// = consecutive tokens whose slots are consecutive inside one block: a sequence's new tokens,
+// split at block boundaries), so it holds a whole block row of V at once: K goes out as 16-byte
+// pieces, V as one 16-byte store per (dim, 8 tokens) when the run covers them (every interior
+// block), two-byte stores only at a run's ragged ends.  grid = (ceil(T / 16), Hkv), 256 threads.
+template <int D>
+__global__ __launch_bounds__(256) void kv_cache_write_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
+                                                             const int* __restrict__ slot_mapping,
+                                                             bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+                                                             int Hq, int Hkv, int T) {
+  constexpr int BS = 16;
+  __shared__ int s_slot[33];  // slots of tokens t0 - 1 .. t0 + 31
+  const int t0 = blockIdx.x * 16, h = blockIdx.y, tid = threadIdx.x;
+  if (tid < 33) {
+    const int t = t0 - 1 + tid;
+    s_slot[tid] = (t >= 0 && t < T) ? slot_mapping[t] : -1;
+  }
+  __syncthreads();
+  const long koff = (long)(Hq + h) * D, voff = (long)(Hq + Hkv + h) * D;
+  for (int i = 0; i < 16 && t0 + i < T; ++i) {  // uniform: every thread reads the same LDS slots
+    const int sl = s_slot[i + 1];
+    if (sl < 0) continue;
+    if (sl % BS != 0 && s_slot[i] == sl - 1) continue;  // not a run start: an earlier window owns it
+    const int off0 = sl % BS;
+    int len = 1;
+    while (len < BS - off0 && i + 1 + len < 33 && s_slot[i + 1 + len] == sl + len) ++len;
+    const long blk = sl / BS;
+    const int ts = t0 + i;
+    bf16_t* kb = k_cache + (blk * Hkv + h) * (long)(D * BS);  // [D/8][BS][8]
+    for (int e = tid; e < (D / 8) * BS; e += 256) {
+      const int c = e / BS, j = e % BS;
+      if (j < len)
+        *reinterpret_cast<uint4*>(kb + ((long)c * BS + off0 + j) * 8) =
+            *reinterpret_cast<const uint4*>(qkv + (long)(ts + j) * qkv_stride + koff + c * 8);
+    }
+    bf16_t* vb = v_cache + (blk * Hkv + h) * (long)(D * BS);  // [D][BS]
+    for (int e = tid; e < D * 2; e += 256) {
+      const int d = e >> 1, o0 = (e & 1) * 8;  // block offsets o0 .. o0 + 7 of dim d
+      if (off0 + len <= o0 || off0 >= o0 + 8) continue;
+      bf16_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = o0 + q - off0;
+        v[q] = (j >= 0 && j < len) ? qkv[(long)(ts + j) * qkv_stride + voff + d] : (bf16_t)0;
+      }
+      bf16_t* dst = vb + (long)d * BS + o0;
+      if (off0 <= o0 && off0 + len >= o0 + 8) {
+        uint4 w;
+        w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+        w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+        w.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16);
+        w.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
+        *reinterpret_cast<uint4*>(dst) = w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int j = o0 + q - off0;
+          if (j >= 0 && j < len) dst[q] = v[q];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
@@ -134,11 +202,15 @@ extern "C" int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* position
                                  void* v_cache, const int* slot_mapping, long T, int Hq, int Hkv, int D,
                                  int block_size, int apply_rope, const float* partial, int S, hipStream_t s) {
   if (T <= 0) return 0;
-  const int items = (Hq + 2 * Hkv) * (D / 8);
+  if (D != 128 && D != 64) return -1;
+  // prefill (no slabs, 16-token blocks): rotate in place, then write the cache block-run-wise
+  const bool runs = partial == nullptr && slot_mapping != nullptr && block_size == 16;
+  const int* rope_slots = runs ? nullptr : slot_mapping;
+  const int items = (Hq + (runs ? 1 : 2) * Hkv) * (D / 8);
   dim3 grid((unsigned)T, (items + 127) / 128);
 #define K8S_ROPE(DV, SL)                                                                                       \
   hipLaunchKernelGGL((rope_cache_kernel<DV, SL>), grid, dim3(128), 0, s, (bf16_t*)qkv, qkv_stride, positions,  \
-                     cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope, \
+                     cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, rope_slots, Hq, Hkv, block_size, apply_rope,   \
                      partial, S, (int)T)
   if (D == 128) {
     if (partial) K8S_ROPE(128, true); else K8S_ROPE(128, false);
@@ -148,5 +220,14 @@ extern "C" int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* position
     return -1;
   }
 #undef K8S_ROPE
+  if (runs) {
+    dim3 g2((unsigned)((T + 15) / 16), Hkv);
+    if (D == 128)
+      hipLaunchKernelGGL((kv_cache_write_kernel<128>), g2, dim3(256), 0, s, (const bf16_t*)qkv, qkv_stride,
+                         slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, (int)T);
+    else
+      hipLaunchKernelGGL((kv_cache_write_kernel<64>), g2, dim3(256), 0, s, (const bf16_t*)qkv, qkv_stride,
+                         slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, (int)T);
+  }
   return (int)hipGetLastError();
 }

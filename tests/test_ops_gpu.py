@@ -519,3 +519,46 @@ def test_skinny_grouped_moe(M, E):
         _close(ops.unpack_skinny(act[e])[:M].cpu(), a, atol=3e-2, rtol=2e-2, what=f"expert {e} act")
         ref_out += torch.nn.functional.linear(a.float(), w2[e].cpu().float()) * wd[:, e:e + 1].cpu()
     _close(out.cpu(), ref_out, atol=6e-2, rtol=3e-2, what="weighted combine")
+
+
+@pytest.mark.parametrize("n", [1, 37, 64])
+def test_resolve_ids(n):
+    ids = torch.randint(0, 1000, (n,), dtype=torch.int32, device=DEV)
+    prev = torch.randint(0, 1000, (64,), dtype=torch.int32, device=DEV)
+    src = torch.randint(-1, 64, (n,), dtype=torch.int32, device=DEV)
+    y = ops.resolve_ids(ids, src, prev)
+    r = torch.where(src.cpu() >= 0, prev.cpu()[src.cpu().clamp(min=0).long()], ids.cpu())
+    assert torch.equal(y.cpu(), r)
+
+
+@pytest.mark.parametrize("d", [128, 64])
+def test_rope_and_cache_prefill_block_runs(d):
+    """Prefill layout: sequences' new tokens are consecutive slots inside their blocks, chunks start
+    mid-block and sequences at arbitrary rows - the block-run cache writer must match the reference
+    (full 16-token runs, ragged starts / ends, runs crossing the 16-row windows, padding rows)."""
+    hq, hkv, bs = 8, 4, 16
+    starts, lens = [0, 5, 16, 37, 3], [40, 27, 16, 1, 70]  # ctx_start (first position), new tokens
+    nb = 64
+    perm = torch.randperm(nb)
+    ids_slots, pos_l, used = [], [], 0
+    for c, n in zip(starts, lens):
+        nblk = (c + n + bs - 1) // bs
+        bt = perm[used:used + nblk]
+        used += nblk
+        p = torch.arange(c, c + n)
+        pos_l.append(p)
+        ids_slots.append(bt[p // bs] * bs + p % bs)
+    slots = torch.cat(ids_slots).to(torch.int32)
+    slots[7] = -1  # a padding row inside a run
+    pos = torch.cat(pos_l).to(torch.int32)
+    T = slots.numel()
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    cs = ref.rope_cos_sin(4096, d, 500000.0, device=DEV)
+    kc, vc = _make_cache(nb, hkv, d)
+    kc0, vc0 = kc.clone().cpu(), vc.clone().cpu()
+    q2 = qkv.clone().cpu()
+    ops.rope_and_cache(qkv, pos.to(DEV), cs, kc, vc, slots.to(DEV), hq, hkv, d)
+    ref.rope_and_cache(q2, pos, cs.cpu(), kc0, vc0, slots, hq, hkv, d)
+    _close(qkv, q2.to(DEV), atol=2e-2, rtol=1e-2, what="rope qkv")
+    _close(kc, kc0.to(DEV), atol=2e-2, rtol=1e-2, what="k_cache")
+    assert torch.equal(vc.cpu(), vc0), "v_cache"
