@@ -137,15 +137,19 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
     if (k0 + 64 < kv_end) fetch(k0 + 64);
     if (k0 > wave_q0 + 31) continue;  // every key of this tile is in the future of every row of this wave
 
+    // the two 32-key halves are independent accumulation chains: interleave them (k-step outer)
+    // so consecutive MFMAs never wait on each other's result
     f32x16 sacc[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[i][r] = 0.f;
-      const int kr = 32 * i + r32;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int ch = 2 * ks + hh;
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ch = 2 * ks + hh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kr = 32 * i + r32;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (kr * CH + (ch ^ (kr & 15))) * 8);
         sacc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[i], 0, 0, 0);
       }
