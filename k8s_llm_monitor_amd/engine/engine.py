@@ -414,6 +414,8 @@ class EngineService:
                 pass
             except Exception as e:  # noqa: BLE001 - reject this request only
                 fut.set_exception(e)
+            if coalesce and self._waiting_tokens() >= cfg.max_prefill_tokens:
+                coalesce = False  # a full prefill step is already queued: start it now
             try:
                 item = self._q.get_nowait()
             except queue.Empty:
@@ -424,6 +426,9 @@ class EngineService:
                         item = self._q.get(timeout=wait)
                     except queue.Empty:
                         item = None
+
+    def _waiting_tokens(self) -> int:
+        return sum(q.num_tokens for q in self.engine.sched.waiting)
 
     def _push_streams(self) -> None:
         for sid, st in list(self._streams.items()):
