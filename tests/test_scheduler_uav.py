@@ -104,3 +104,31 @@ def test_agent_api_routes():
     h = json.loads(api.handle("GET", "/health")[2])
     assert h == {**h, "status": "healthy", "uav_id": "UAV-n", "node_ip": "1.2.3.4"}
     assert api.handle("GET", "/nope")[0] == 404
+
+
+def test_deployment_manifests_parse_and_configmap_current():
+    """Every manifest is valid YAML with kind/apiVersion; the simulator ConfigMap embeds the current
+    mock_server.py (tools/gen_uav_configmap.py), and every example SchedulingRequest satisfies the
+    CRD's required fields."""
+    import glob
+    import os
+    import subprocess
+    import sys
+
+    import yaml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for path in glob.glob(os.path.join(root, "deployments", "*.yaml")) + glob.glob(os.path.join(root, "examples",
+                                                                                                 "*.yaml")):
+        with open(path, encoding="utf-8") as f:
+            docs = [d for d in yaml.safe_load_all(f) if d]
+        assert docs, path
+        for d in docs:
+            assert d.get("apiVersion") and d.get("kind"), path
+            if d["kind"] == "SchedulingRequest":
+                w = d["spec"]["workload"]
+                assert w["name"] and w["namespace"], path
+                assert 0 <= d["spec"].get("minBatteryPercent", 0) <= 100, path
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_uav_configmap.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
