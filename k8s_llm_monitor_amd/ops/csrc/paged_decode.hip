@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
     for (int i = 0; i < 4; ++i) {
       const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[i][s] = *reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8);
+      for (int s = 0; s < KS; ++s)
+        kf[i][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8));
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -117,8 +118,11 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
       const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        vlo[s][dt] = *reinterpret_cast<const uint2*>(va + 16 * dt * kBS);
-        vhi[s][dt] = *reinterpret_cast<const uint2*>(vb + 16 * dt * kBS);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t a2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(va + 16 * dt * kBS));
+        const u32x2_t b2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + 16 * dt * kBS));
+        vlo[s][dt] = make_uint2(a2.x, a2.y);
+        vhi[s][dt] = make_uint2(b2.x, b2.y);
       }
     }
   };
