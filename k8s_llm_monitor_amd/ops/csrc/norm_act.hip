@@ -113,8 +113,12 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
   for (long r = blockIdx.y; r < rows; r += gridDim.y) {
     const bf16_t* xr = x + r * 2 * F;
     float g[8], u[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(xr + c), g);
-    unpack8(*reinterpret_cast<const uint4*>(xr + F + c), u);
+    // the gate_up activations are read exactly once: non-temporal loads
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t ga = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + c));
+    const u32x4_t ua = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + F + c));
+    unpack8(make_uint4(ga.x, ga.y, ga.z, ga.w), g);
+    unpack8(make_uint4(ua.x, ua.y, ua.z, ua.w), u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
     *reinterpret_cast<uint4*>(out + r * F + c) = pack8(o);
