@@ -580,10 +580,10 @@ __global__ __launch_bounds__(64) void add_norm_partial_kernel(bf16_t* __restrict
   float acc[8];
   unpack8(*reinterpret_cast<const uint4*>(rr), acc);
 #pragma unroll 4
-  for (int s = 0; s < S; ++s) {
+  for (int s = 0; s < S; ++s) {  // the slabs are read exactly once: non-temporal
     const float* p = partial + ((long)s * M + row) * d + col;
-    const float4 a = *reinterpret_cast<const float4*>(p);
-    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
     acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
     acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
   }
