@@ -161,9 +161,11 @@ __global__ __launch_bounds__(256) void kv_cache_write_kernel(const bf16_t* __res
     bf16_t* kb = k_cache + (blk * Hkv + h) * (long)(D * BS);  // [D/8][BS][8]
     for (int e = tid; e < (D / 8) * BS; e += 256) {
       const int c = e / BS, j = e % BS;
-      if (j < len)
-        *reinterpret_cast<uint4*>(kb + ((long)c * BS + off0 + j) * 8) =
-            *reinterpret_cast<const uint4*>(qkv + (long)(ts + j) * qkv_stride + koff + c * 8);
+      if (j < len) {  // the cache is next read by a later step: non-temporal stores
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(qkv + (long)(ts + j) * qkv_stride + koff + c * 8),
+                                    reinterpret_cast<u32x4_t*>(kb + ((long)c * BS + off0 + j) * 8));
+      }
     }
     bf16_t* vb = v_cache + (blk * Hkv + h) * (long)(D * BS);  // [D][BS]
     for (int e = tid; e < D * 2; e += 256) {
@@ -177,12 +179,13 @@ __global__ __launch_bounds__(256) void kv_cache_write_kernel(const bf16_t* __res
       }
       bf16_t* dst = vb + (long)d * BS + o0;
       if (off0 <= o0 && off0 + len >= o0 + 8) {
-        uint4 w;
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        u32x4_t w;
         w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
         w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
         w.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16);
         w.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
-        *reinterpret_cast<uint4*>(dst) = w;
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(dst));
       } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
