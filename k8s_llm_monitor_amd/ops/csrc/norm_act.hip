@@ -26,15 +26,22 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16_t* __restrict__ out, 
   for (int c = 0; c < NC; ++c) {
     const int idx = (c * 256 + tid) * 8;
     if (idx < d) {
-      uint4 a = *reinterpret_cast<const uint4*>(xr + idx);
-      unpack8(a, v[c]);
+      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
       if (ADD) {
+        // fused residual add (the prefill path): x (a projection output) and the old residual are
+        // read once, and the new residual is not read again before the next layer half - all three
+        // streams non-temporal; only the normalised output (the next GEMM's input) stays cached
+        const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + idx));
+        const u32x4_t b = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(rr + idx));
         float r[8];
-        uint4 b = *reinterpret_cast<const uint4*>(rr + idx);
-        unpack8(b, r);
+        unpack8(make_uint4(a.x, a.y, a.z, a.w), v[c]);
+        unpack8(make_uint4(b.x, b.y, b.z, b.w), r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j] + r[j]));
-        *reinterpret_cast<uint4*>(rr + idx) = pack8(v[c]);
+        const uint4 q = pack8(v[c]);
+        __builtin_nontemporal_store(u32x4_t{q.x, q.y, q.z, q.w}, reinterpret_cast<u32x4_t*>(rr + idx));
+      } else {
+        unpack8(*reinterpret_cast<const uint4*>(xr + idx), v[c]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
