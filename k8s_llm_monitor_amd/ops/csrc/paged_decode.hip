@@ -132,31 +132,37 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   bf16x8 qf[KS];
   if constexpr (FQ) {
     // q (G heads) + the new k (rotated) + v of kv head kvh from the qkv slabs: (G + 1) * D/2
-    // rotary pairs and D/2 value pairs, one item per thread
+    // rotary pairs and D/2 value pairs
     const int ncols = (Hq + 2 * Hkv) * D;
     const long slab = (long)gridDim.z * ncols;
     const float* row = fz.slabs + (long)b * ncols;
     const float* cs = fz.cos_sin + (long)fz.positions[b] * D;
     constexpr int HALF = D / 2;
-    for (int it = threadIdx.x; it < (G + 2) * HALF; it += 256) {
-      const int h = it / HALF, p = it - h * HALF;  // h < G: q head kvh*G+h; h == G: k; h == G+1: v
+    // 4 rotary pairs per item: 16-byte (non-temporal: read once) slab loads, one round for G <= 8
+    constexpr int QP = HALF / 4;
+    for (int it = threadIdx.x; it < (G + 2) * QP; it += 256) {
+      const int h = it / QP, p = (it - h * QP) * 4;  // h < G: q head kvh*G+h; h == G: k; h == G+1: v
       const int c = h < G ? (kvh * G + h) * D : (h == G ? (Hq + kvh) * D : (Hq + Hkv + kvh) * D);
-      float x1 = 0.f, x2 = 0.f;
+      f32x4 x1 = {0.f, 0.f, 0.f, 0.f}, x2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
       for (int z = 0; z < fz.nslabs; ++z) {
-        x1 += row[z * slab + c + p];
-        x2 += row[z * slab + c + HALF + p];
-      }
-      x1 = bf2f(f2bf(x1));  // rounded as the unfused GEMM output -> rope_cache path is
-      x2 = bf2f(f2bf(x2));
-      if (h <= G) {
-        const float cc = cs[p], sn = cs[HALF + p];
-        const float o1 = x1 * cc - x2 * sn, o2 = x2 * cc + x1 * sn;
-        x1 = o1;
-        x2 = o2;
+        x1 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + z * slab + c + p));
+        x2 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + z * slab + c + HALF + p));
       }
       bf16_t* dst = h < G ? s_q[h] : s_kv[h - G];
-      dst[p] = f2bf(x1);
-      dst[HALF + p] = f2bf(x2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = bf2f(f2bf(x1[j]));  // rounded as the unfused GEMM output -> rope_cache path is
+        float e = bf2f(f2bf(x2[j]));
+        if (h <= G) {
+          const float cc = cs[p + j], sn = cs[HALF + p + j];
+          const float o1 = a * cc - e * sn, o2 = e * cc + a * sn;
+          a = o1;
+          e = o2;
+        }
+        dst[p + j] = f2bf(a);
+        dst[HALF + p + j] = f2bf(e);
+      }
     }
     __syncthreads();
     const int hc = col < G ? col : 0;
