@@ -214,3 +214,61 @@ def test_service_coalesces_a_burst_into_one_prefill():
     svc.close()
     first = next(e for e in eng.trace if e[1] == "prefill")
     assert first[2] == 8
+
+
+def test_service_coalescing_stops_at_a_full_prefill_budget():
+    """Admission coalescing ends as soon as the queued prompts fill one prefill step
+    (max_prefill_tokens): the first prefill does not wait out the window for the rest of a burst."""
+    import time
+
+    from k8s_llm_monitor_amd.engine import EngineService
+
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=16, max_model_len=256, num_blocks=256,
+                                 use_graphs=False, max_prefill_tokens=64, admit_gap_ms=400.0,
+                                 admit_window_ms=2000.0), device="cpu")
+    eng.trace = []
+    svc = EngineService(eng)
+    prompt = "pod default/api-gateway CrashLoopBackOff restarted 12 times " * 3  # > 64 tokens alone
+    t0 = time.perf_counter()
+    fut = svc.submit(prompt, SamplingParams(max_tokens=1, ignore_eos=True))
+    fut.result(timeout=60)
+    dt = time.perf_counter() - t0
+    svc.close()
+    assert dt < 0.4, f"first prefill waited {dt:.3f} s for more arrivals with a full budget queued"
+
+
+def test_decode_staging_layout_and_resolve_ids_cpu():
+    """The packed decode-input buffer: field views are disjoint, in the documented order, float
+    fields bit-cast, and the copied prefix covers the per-row fields plus the live block-table rows;
+    resolve_ids' CPU path picks the previous step's token where src >= 0."""
+    import numpy as np
+    import torch
+
+    from k8s_llm_monitor_amd import ops
+    from k8s_llm_monitor_amd.engine.runner import _Staging
+
+    B, mb = 8, 5
+    st = _Staging(B, mb, pin=False)
+    assert st.h_all.numel() == _Staging.size(B, mb) == 8 * B + B * mb
+    st.n_ids[:] = 1
+    st.n_src[:] = 2
+    st.n_pos[:] = 3
+    st.n_slots[:] = 4
+    st.n_lens[:] = 5
+    st.n_topk[:] = 6
+    st.n_temp[:] = 0.5
+    st.n_topp[:] = 0.25
+    st.n_bt[:] = 9
+    raw = st.h_all.numpy()
+    for i, v in enumerate([1, 2, 3, 4, 5, 6]):
+        assert (raw[i * B:(i + 1) * B] == v).all()
+    assert (raw[6 * B:7 * B].view(np.float32) == 0.5).all() and (raw[7 * B:8 * B].view(np.float32) == 0.25).all()
+    assert (raw[8 * B:] == 9).all()
+    assert _Staging.prefix(B, mb, 3) == 8 * B + 3 * mb
+    dev = torch.zeros(_Staging.size(B, mb), dtype=torch.int32)
+    views = _Staging.views(dev, B, mb)
+    assert views[6].dtype == torch.float32 and views[8].shape == (B, mb)
+    ids = torch.tensor([10, 11, 12, 13], dtype=torch.int32)
+    src = torch.tensor([-1, 2, -1, 0], dtype=torch.int32)
+    prev = torch.tensor([100, 101, 102, 103], dtype=torch.int32)
+    assert ops.resolve_ids(ids, src, prev).tolist() == [10, 102, 12, 100]
