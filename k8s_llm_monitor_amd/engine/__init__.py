@@ -1,3 +1,3 @@
 """Continuous-batching inference engine (paged KV cache, hipGraph decode, TP over RCCL)."""
-from .engine import EngineConfig, EngineService, LLMEngine  # noqa: F401
+from .engine import EngineConfig, EngineOverloaded, EngineService, EngineUnavailable, LLMEngine  # noqa: F401
 from .sequence import SamplingParams, Sequence, SeqStatus  # noqa: F401

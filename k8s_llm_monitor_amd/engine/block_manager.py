@@ -71,6 +71,15 @@ class PyBlockPool:
             n += 1
         return n
 
+    def peek_idle(self, hashes: list) -> int:
+        n = 0
+        for h in hashes:
+            b = self._map.get(h)
+            if b is None:
+                break
+            n += self._ref[b] == 0
+        return n
+
     def match(self, hashes: list) -> list:
         out = []
         self._stats["queries"] += 1
@@ -179,10 +188,13 @@ class BlockManager:
 
     # ------------------------------------------------------------------ allocation
     def can_allocate(self, seq: Sequence) -> bool:
+        """Fresh blocks needed beyond the prefix-cache hits, PLUS the hits that sit unreferenced in
+        the LRU: ``match`` takes those out of the free pool too (they are counted in num_free)."""
         hs = self._prefix_hashes(seq)
         hit = self.pool.peek(hs) if hs else 0
+        idle = self.pool.peek_idle(hs) if hit else 0
         need = self.blocks_needed(seq.num_tokens + 1) - hit
-        return self.pool.num_free - need >= self.watermark_blocks
+        return self.pool.num_free - need - idle >= self.watermark_blocks
 
     def allocate(self, seq: Sequence) -> bool:
         hs = self._prefix_hashes(seq)

@@ -21,6 +21,7 @@ import itertools
 import multiprocessing as mp
 import threading
 import time
+from collections import deque
 from concurrent.futures import Future
 from dataclasses import asdict
 from typing import Optional, Sequence as Seq, Union
@@ -43,24 +44,29 @@ class RemoteSeq:
 
 
 class _EngineInfo:
-    """``router.engine``: the model config and tokenizer (built locally, CPU only)."""
+    """``router.engine``: the model config and tokenizer (built locally, CPU only) - resolved
+    exactly as each replica's LLMEngine resolves them (engine.py), so token counts and streamed
+    detokenization use the replicas' vocabulary: a Hugging Face ``weights`` directory wins over
+    the built-in model name."""
 
-    def __init__(self, model: str, overrides: dict):
+    def __init__(self, model: str, overrides: dict, weights: Optional[str] = None, cfg=None):
+        from ..models.checkpoint import config_from_hf
         from ..models.config import get_config
-        from .tokenizer import tokenizer_for
+        from .tokenizer import tokenizer_for, tokenizer_from_dir
 
-        mc = get_config(model)
+        mc = config_from_hf(weights) if weights else get_config(model)
         if overrides:
             mc = mc.replace(**overrides)
         self.model_cfg = mc
-        self.tokenizer = tokenizer_for(mc)
+        self.cfg = cfg
+        self.tokenizer = tokenizer_from_dir(weights, mc) if weights else tokenizer_for(mc)
 
 
 def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
     """Child process: one engine replica serving the router's pipe until ``close``."""
     import torch
 
-    from .engine import EngineConfig, EngineService, LLMEngine
+    from .engine import EngineConfig, EngineOverloaded, EngineService, EngineUnavailable, LLMEngine
 
     try:
         if device.startswith("cuda"):
@@ -89,6 +95,8 @@ def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
             send(("done", key, {"text": text, "timings": seq.timings(), "finish_reason": seq.finish_reason,
                                 "output_ids": list(seq.output_ids), "prompt_ids": list(seq.prompt_ids),
                                 "replica": idx}))
+        except (EngineOverloaded, EngineUnavailable) as e:
+            send(("busy", key, str(e)))
         except BaseException as e:  # noqa: BLE001
             send(("fail", key, repr(e)))
 
@@ -98,9 +106,10 @@ def _replica_main(conn, idx: int, cfg: dict, device: str) -> None:
         except EOFError:
             break
         if kind == "req":
-            prompt, params, rid, stream = body if len(body) == 4 else (*body, False)
+            prompt, params, rid, stream, budget = (tuple(body) + (False, None))[:5]
             cb = (lambda ids, k=key: send(("tok", k, ids))) if stream else None
-            fut = svc.submit(prompt, SamplingParams(**params), rid, on_tokens=cb)
+            deadline = time.perf_counter() + budget if budget is not None else None
+            fut = svc.submit(prompt, SamplingParams(**params), rid, on_tokens=cb, deadline=deadline)
             live[key] = fut
             fut.add_done_callback(lambda f, k=key: (live.pop(k, None), on_done(k, f)))
         elif kind == "cancel":
@@ -138,13 +147,13 @@ class ReplicaRouter:
         assert isinstance(engine_cfg, EngineConfig)
         if not devices:
             raise ValueError("ReplicaRouter needs at least one device")
-        self.engine = _EngineInfo(engine_cfg.model, engine_cfg.model_overrides)
+        self.engine = _EngineInfo(engine_cfg.model, engine_cfg.model_overrides, engine_cfg.weights, engine_cfg)
         self._keys = itertools.count()
         self._pending: dict = {}
         self._streams: dict = {}  # key -> on_tokens of streaming requests
         self._lock = threading.Lock()
         self._error: Optional[str] = None
-        self.latencies_ms: list = []
+        self.latencies_ms: deque = deque(maxlen=4096)
         ctx = mp.get_context("spawn")
         cfg = asdict(engine_cfg)
         self.replicas: list[_Replica] = []
@@ -170,8 +179,12 @@ class ReplicaRouter:
             r.reader.start()
 
     # ------------------------------------------------------------------ EngineService API
+    @property
+    def healthy(self) -> bool:
+        return self._error is None and all(r.proc.is_alive() for r in self.replicas)
+
     def submit(self, prompt: Union[str, list], params: Optional[SamplingParams] = None,
-               request_id: Optional[str] = None, on_tokens=None) -> Future:
+               request_id: Optional[str] = None, on_tokens=None, deadline: Optional[float] = None) -> Future:
         """As EngineService.submit; ``on_tokens`` is called on the router's reader thread with the
         token ids the replica streams back (``tok`` messages) before the answer arrives."""
         fut: Future = Future()
@@ -188,7 +201,8 @@ class ReplicaRouter:
             self._pending[key] = (fut, r)
             if on_tokens is not None:
                 self._streams[key] = on_tokens
-        r.send(("req", key, (prompt, p, request_id, on_tokens is not None)))
+        budget = deadline - time.perf_counter() if deadline is not None else None  # replica clocks differ
+        r.send(("req", key, (prompt, p, request_id, on_tokens is not None, budget)))
         return fut
 
     def cancel(self, fut: Future) -> bool:
@@ -215,7 +229,7 @@ class ReplicaRouter:
                     except Exception:  # noqa: BLE001 - a broken consumer must not stop the reader
                         pass
                 continue
-            if kind in ("done", "fail"):
+            if kind in ("done", "fail", "busy"):
                 with self._lock:
                     fut, _ = self._pending.pop(key, (None, None))
                     self._streams.pop(key, None)
@@ -228,6 +242,10 @@ class ReplicaRouter:
                     seq = RemoteSeq(body)
                     self.latencies_ms.append(seq.timings().get("latency_ms", 0.0))
                     fut.set_result((body["text"], seq))
+                elif kind == "busy":
+                    from .engine import EngineOverloaded
+
+                    fut.set_exception(EngineOverloaded(f"replica {r.idx}: {body}"))
                 else:
                     fut.set_exception(RuntimeError(f"replica {r.idx}: {body}"))
             elif kind == "stats":
@@ -270,9 +288,10 @@ class ReplicaRouter:
         agg: dict = {"dp_replicas": len(self.replicas), "replicas": per,
                      "healthy": all(p.get("healthy", False) for p in per) and self._error is None}
         for k in ("requests", "finished", "prompt_tokens", "generated_tokens", "prefill_steps", "decode_steps",
-                  "preemptions", "running", "waiting", "queue_depth"):
+                  "mixed_steps", "preemptions", "running", "waiting", "queue_depth", "rejected", "expired",
+                  "cancelled", "deadline_stops"):
             agg[k] = sum(int(p.get(k, 0) or 0) for p in per)
-        lat = sorted(self.latencies_ms[-4096:])
+        lat = sorted(self.latencies_ms)
         if lat:
             agg["p50_latency_ms"] = lat[len(lat) // 2]
             agg["p99_latency_ms"] = lat[min(len(lat) - 1, int(len(lat) * 0.99))]

@@ -19,6 +19,7 @@ import queue
 import threading
 import time
 import uuid
+from collections import deque
 from concurrent.futures import Future
 from dataclasses import dataclass, field
 from typing import Optional, Union
@@ -44,6 +45,8 @@ class EngineConfig:
     max_model_len: int = 8192
     max_prefill_tokens: int = 16384
     chunked_prefill: bool = True  # prompts beyond a step's token budget prefill in chunks (scheduler.py)
+    # prefill budget of a mixed prefill+decode step (scheduler.py); 0 = prefill steps stall decodes
+    mixed_prefill_tokens: int = 8192
     kv_cache_gb: float = 32.0
     num_blocks: Optional[int] = None
     use_graphs: bool = True
@@ -102,12 +105,14 @@ class LLMEngine:
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
                                                max_prefill_tokens=cfg.max_prefill_tokens,
                                                max_model_len=self.runner.max_len,
-                                               chunked_prefill=cfg.chunked_prefill), self.blocks)
+                                               chunked_prefill=cfg.chunked_prefill,
+                                               mixed_prefill_tokens=cfg.mixed_prefill_tokens), self.blocks)
         self.tokenizer = tokenizer_from_dir(cfg.weights, mc) if cfg.weights else tokenizer_for(mc)
         self.eos = set(mc.eos_ids)
         self.init_s = time.perf_counter() - t0
         self.counters = {"requests": 0, "finished": 0, "prompt_tokens": 0, "generated_tokens": 0,
-                         "prefill_steps": 0, "decode_steps": 0, "preemptions": 0}
+                         "prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "preemptions": 0,
+                         "deadline_stops": 0, "step_failures": 0}
         self.is_leader = self.ps.tp_rank == 0
         self._inflight = None  # (seqs, DecodeHandle) of the enqueued, not yet read back decode step
         self.trace: Optional[list] = [] if os.environ.get("K8SLLM_TRACE") else None  # (t, kind, n, tokens)
@@ -121,14 +126,17 @@ class LLMEngine:
         self.graph_s = time.perf_counter() - t0
 
     def add_request(self, prompt: Union[str, list[int]], params: Optional[SamplingParams] = None,
-                    request_id: Optional[str] = None, user=None) -> Sequence:
+                    request_id: Optional[str] = None, user=None, deadline: Optional[float] = None) -> Sequence:
+        """``deadline`` (time.perf_counter clock): the sequence stops with finish_reason "deadline"
+        at the first step resolved after it - an answer truncated to what fits the caller's time
+        budget instead of work the caller has stopped waiting for."""
         ids = self.tokenizer.encode(prompt) if isinstance(prompt, str) else list(prompt)
         limit = self.runner.max_len - 1
         if len(ids) > limit - 1:  # keep room for at least one generated token; trim the middle
             keep = limit - 1
             ids = ids[: keep // 2] + ids[len(ids) - (keep - keep // 2):]
         seq = Sequence(prompt_ids=ids, params=params or SamplingParams(),
-                       request_id=request_id or uuid.uuid4().hex[:16], user=user)
+                       request_id=request_id or uuid.uuid4().hex[:16], user=user, deadline=deadline)
         self.sched.add(seq)
         if self.trace is not None:
             self.trace.append((time.perf_counter(), "add", 1, len(ids)))
@@ -209,7 +217,7 @@ class LLMEngine:
             self.counters["generated_tokens"] += 1
             if q.t_first_token is None:
                 q.t_first_token = now
-            reason = self._stop_reason(q, tok, n_out=i + 1)
+            reason = self._stop_reason(q, tok, n_out=i + 1, now=now)
             if reason:
                 del q.output_ids[i + 1:]  # drop the token of a step launched past the stop
                 q.t_finish = now
@@ -237,31 +245,37 @@ class LLMEngine:
         if self.ps.tp_size > 1:
             tp_broadcast_object(self._pack(plan), ps=self.ps)
         if plan.is_prefill:
-            toks = self.runner.prefill(plan.seqs)
+            toks = self.runner.prefill(plan.seqs, plan.decode)
             self.counters["prefill_steps"] += 1
+            if plan.decode:
+                self.counters["mixed_steps"] += 1
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), "prefill", len(plan.seqs),
                                    sum(q.chunk for q in plan.seqs)))
+            rows = list(plan.decode) + list(plan.seqs)
+            nd = len(plan.decode)
         else:
             toks = self.runner.decode(plan.seqs)
             self.counters["decode_steps"] += 1
+            rows, nd = plan.seqs, len(plan.seqs)
         now = time.perf_counter()
         done = []
-        for seq, tok in zip(plan.seqs, toks):
-            if plan.is_prefill and not self.sched.chunk_done(seq):
+        for i, (seq, tok) in enumerate(zip(rows, toks)):
+            if i >= nd and not self.sched.chunk_done(seq):
                 continue  # a chunk short of the prompt's end: no token yet
             seq.output_ids.append(int(tok))
             self.counters["generated_tokens"] += 1
             if seq.t_first_token is None:
                 seq.t_first_token = now
-            reason = self._stop_reason(seq, int(tok))
+            reason = self._stop_reason(seq, int(tok), now=now)
             if reason:
                 seq.t_finish = now
                 self._finish(seq, reason)
                 done.append(seq)
         return done
 
-    def _stop_reason(self, seq: Sequence, tok: int, n_out: Optional[int] = None) -> Optional[str]:
+    def _stop_reason(self, seq: Sequence, tok: int, n_out: Optional[int] = None,
+                     now: Optional[float] = None) -> Optional[str]:
         p = seq.params
         n = len(seq.output_ids) if n_out is None else n_out
         if not p.ignore_eos and (tok in self.eos or tok in p.stop_token_ids):
@@ -270,10 +284,28 @@ class LLMEngine:
             return "length"
         if len(seq.prompt_ids) + n >= self.runner.max_len:
             return "length"
+        if seq.deadline is not None and now is not None and now >= seq.deadline:
+            self.counters["deadline_stops"] += 1
+            return "deadline"
         return None
 
     def abort(self, seq: Sequence) -> None:
         self.sched.abort(seq)
+
+    def reset(self) -> list[Sequence]:
+        """After a failed step: drop the in-flight decode and abort every running and waiting
+        sequence (their KV blocks return to the pool).  Returns the aborted sequences."""
+        self._inflight = None
+        self._inflight_rows = {}
+        if self.device.type == "cuda":
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:  # noqa: BLE001 - a sticky device error: the blocks are still freed
+                pass
+        seqs = list(self.sched.running) + list(self.sched.waiting)
+        for q in seqs:
+            self.sched.abort(q)
+        return seqs
 
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list[Sequence]:
         seqs = [self.add_request(p, params) for p in prompts]
@@ -299,7 +331,8 @@ class LLMEngine:
     def _pack(plan) -> tuple:
         if plan.is_prefill:
             return (True, [(s.all_ids, s.block_table, _params_t(s.params), s.num_computed, s.chunk)
-                           for s in plan.seqs])
+                           for s in plan.seqs],
+                    [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.decode])
         return (False, [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.seqs])
 
     def worker_loop(self) -> None:
@@ -316,7 +349,8 @@ class LLMEngine:
                     pending = None
                 views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p), nc, ch)
                          for ids, bt, p, nc, ch in items]
-                self.runner.prefill(views)
+                dec = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in msg[2]]
+                self.runner.prefill(views, dec)
             else:
                 src = msg[2] if len(msg) > 2 else None
                 views = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in items]
@@ -340,41 +374,95 @@ class _Skip(Exception):
     pass
 
 
+class EngineOverloaded(RuntimeError):
+    """Admission refused: the queue is full or the request cannot start within its deadline
+    (the HTTP layer answers 503 - SURVEY.md §5 failure detection: reject, never crash or hang)."""
+
+
+class EngineUnavailable(RuntimeError):
+    """The engine is unhealthy (repeated step failures) and accepts no work (HTTP 503)."""
+
+
 class EngineService:
     """Runs an LLMEngine on its own thread; thread-safe ``submit`` returns a Future that resolves
-    to ``(text, sequence)``."""
+    to ``(text, sequence)``.
 
-    def __init__(self, engine: LLMEngine):
+    Serving robustness:
+    * bounded admission - at most ``max_queue`` requests wait (queued + scheduler-waiting); beyond
+      that, and for a request whose estimated time to first token already exceeds its deadline,
+      ``submit`` fails the future with EngineOverloaded at once;
+    * deadlines - ``submit(deadline=...)`` stops the sequence at the deadline with finish_reason
+      "deadline" (a truncated answer, KV freed), and a request still waiting when its deadline
+      passes is dropped with EngineOverloaded;
+    * cancellation - ``cancel(fut)`` aborts the sequence and frees its KV blocks before the next
+      step;
+    * step failures - an exception inside a step fails only the requests in flight, resets the
+      engine's batch and keeps serving; ``max_failures`` failures within ``failure_window_s`` (or
+      any failure at TP > 1, where the workers' mirrored state is unknown) mark the service
+      unhealthy: ``healthy`` turns False and every later submit fails with EngineUnavailable.
+    """
+
+    def __init__(self, engine: LLMEngine, max_queue: Optional[int] = None, max_failures: int = 3,
+                 failure_window_s: float = 60.0):
         self.engine = engine
+        self.max_queue = max_queue if max_queue is not None else 4 * engine.cfg.max_num_seqs
+        self.max_failures, self.failure_window_s = max_failures, failure_window_s
         self._q: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
         self._lock = threading.Lock()
         self._error: Optional[BaseException] = None
-        self.latencies_ms: list[float] = []
+        self._failures: deque = deque()
+        self.latencies_ms: deque = deque(maxlen=4096)
         self._streams: dict = {}  # seq_id -> [seq, tokens delivered, on_tokens]
         self._cancels: queue.SimpleQueue = queue.SimpleQueue()  # futures whose requests to abort
         self.cancelled = 0
+        self.rejected = 0
+        self.expired = 0
+        # prefill throughput estimate (tokens/s, EWMA over prefill steps) for deadline admission
+        self._prefill_tps: Optional[float] = None
+        self._waiting_est = 0  # prompt tokens waiting in the scheduler (engine thread writes)
         self._thread.start()
 
+    @property
+    def healthy(self) -> bool:
+        return self._error is None and self._thread.is_alive()
+
+    def pending(self) -> int:
+        """Requests admitted but not yet running (HTTP queue + scheduler waiting list)."""
+        return self._q.qsize() + len(self.engine.sched.waiting)
+
     def submit(self, prompt: Union[str, list[int]], params: Optional[SamplingParams] = None,
-               request_id: Optional[str] = None, on_tokens=None) -> Future:
+               request_id: Optional[str] = None, on_tokens=None, deadline: Optional[float] = None) -> Future:
         """``on_tokens(ids)`` (optional, streaming): called on the engine thread with each batch of
-        newly generated token ids, before the future resolves; keep it cheap (e.g. a queue put)."""
+        newly generated token ids, before the future resolves; keep it cheap (e.g. a queue put).
+        ``deadline``: time.perf_counter() value by which the answer is due (see class docstring)."""
         fut: Future = Future()
-        if self._error is not None:
-            fut.set_exception(RuntimeError(f"engine failed: {self._error!r}"))
+        if not self.healthy:
+            fut.set_exception(EngineUnavailable(f"engine unhealthy: {self._error!r}"))
             return fut
+        if self.pending() >= self.max_queue:
+            self.rejected += 1
+            fut.set_exception(EngineOverloaded(f"request queue full ({self.max_queue} waiting)"))
+            return fut
+        if deadline is not None and self._prefill_tps:
+            # queued prompt tokens ahead of this one at the measured prefill rate: if even the first
+            # token cannot arrive before the deadline, say so now instead of timing out later
+            ahead = self._waiting_est + self._q.qsize() * 1024
+            if time.perf_counter() + ahead / self._prefill_tps > deadline:
+                self.rejected += 1
+                fut.set_exception(EngineOverloaded("estimated time to first token exceeds the deadline"))
+                return fut
         tr = self.engine.trace
         if tr is not None:
             tr.append((time.perf_counter(), "submit", 1, 0))
-        self._q.put((prompt, params, request_id, fut, on_tokens))
+        self._q.put((prompt, params, request_id, fut, on_tokens, deadline))
         return fut
 
     def cancel(self, fut: Future) -> bool:
-        """Abort the request behind ``fut`` (e.g. its streaming client disconnected): the future
-        is cancelled at once; the engine thread drops the sequence and frees its KV blocks before
-        its next step.  False if the answer was already complete."""
+        """Abort the request behind ``fut`` (e.g. its streaming client disconnected or its caller
+        timed out): the future is cancelled at once; the engine thread drops the sequence and frees
+        its KV blocks before its next step.  False if the answer was already complete."""
         if not fut.cancel():
             return False
         self._cancels.put(fut)
@@ -394,6 +482,16 @@ class EngineService:
                 self._streams.pop(s.seq_id, None)
                 self.cancelled += 1
 
+    def _expire_waiting(self) -> None:
+        """Drop waiting (not yet admitted) requests whose deadline has passed."""
+        now = time.perf_counter()
+        for s in [s for s in self.engine.sched.waiting if s.deadline is not None and now >= s.deadline]:
+            self.engine.abort(s)
+            self._streams.pop(s.seq_id, None)
+            self.expired += 1
+            if isinstance(s.user, Future) and not s.user.done():
+                s.user.set_exception(EngineOverloaded("request expired in the queue before it could start"))
+
     def _drain(self, block: bool) -> None:
         try:
             item = self._q.get(block=block, timeout=0.05 if block else None)
@@ -403,11 +501,11 @@ class EngineService:
         coalesce = block and cfg.admit_window_ms > 0  # the engine was idle: let a burst gather
         t_end = time.perf_counter() + cfg.admit_window_ms * 1e-3
         while item is not None:
-            prompt, params, rid, fut, on_tokens = item
+            prompt, params, rid, fut, on_tokens, deadline = item
             try:
                 if fut.cancelled():  # cancelled while queued
                     raise _Skip()
-                seq = self.engine.add_request(prompt, params, rid, user=fut)
+                seq = self.engine.add_request(prompt, params, rid, user=fut, deadline=deadline)
                 if on_tokens is not None:
                     self._streams[seq.seq_id] = [seq, 0, on_tokens]
             except _Skip:
@@ -448,39 +546,82 @@ class EngineService:
             if seq.status in (SeqStatus.FINISHED, SeqStatus.ABORTED):
                 del self._streams[sid]
 
-    def _loop(self) -> None:
+    def _step_once(self) -> None:
         eng = self.engine
-        try:
-            while not self._stop.is_set():
-                if not self._cancels.empty():
-                    self._apply_cancels()
-                self._drain(block=not eng.has_work())
-                if not eng.has_work():
-                    continue
-                finished = eng.step()
-                if self._streams:
-                    self._push_streams()
-                for seq in finished:
-                    fut = seq.user
-                    if isinstance(fut, Future) and not fut.done():
-                        self.latencies_ms.append(seq.timings()["latency_ms"])
-                        fut.set_result((eng.decode_text(seq), seq))
-        except BaseException as e:  # noqa: BLE001 - surface to every waiter
+        if not self._cancels.empty():
+            self._apply_cancels()
+        self._drain(block=not eng.has_work())
+        if eng.sched.waiting:
+            self._expire_waiting()
+        self._waiting_est = self._waiting_tokens()
+        if not eng.has_work():
+            return
+        p0, t0 = eng.counters["prefill_steps"], time.perf_counter()
+        ptok0 = eng.runner.n_steps.get("prefill_tokens", 0)
+        finished = eng.step()
+        if eng.counters["prefill_steps"] > p0:
+            dt = time.perf_counter() - t0
+            n = eng.runner.n_steps.get("prefill_tokens", 0) - ptok0
+            if n > 0 and dt > 0:
+                r = n / dt
+                self._prefill_tps = r if self._prefill_tps is None else 0.8 * self._prefill_tps + 0.2 * r
+        if self._streams:
+            self._push_streams()
+        for seq in finished:
+            fut = seq.user
+            if isinstance(fut, Future) and not fut.done():
+                self.latencies_ms.append(seq.timings()["latency_ms"])
+                fut.set_result((eng.decode_text(seq), seq))
+
+    def _on_failure(self, e: BaseException) -> None:
+        """A step raised: fail the requests in flight, reset the batch, maybe go unhealthy."""
+        eng = self.engine
+        eng.counters["step_failures"] += 1
+        import logging
+
+        logging.getLogger("engine").error("engine step failed: %r", e, exc_info=e)
+        err = RuntimeError(f"engine step failed: {e!r}")
+        for s in eng.reset():
+            if isinstance(s.user, Future) and not s.user.done():
+                s.user.set_exception(err)
+        self._streams.clear()
+        now = time.monotonic()
+        self._failures.append(now)
+        while self._failures and now - self._failures[0] > self.failure_window_s:
+            self._failures.popleft()
+        if len(self._failures) >= self.max_failures or eng.ps.tp_size > 1:
             self._error = e
-            for s in list(eng.sched.running) + list(eng.sched.waiting):
-                if isinstance(s.user, Future) and not s.user.done():
-                    s.user.set_exception(RuntimeError(f"engine failed: {e!r}"))
-            raise
+
+    def _loop(self) -> None:
+        while not self._stop.is_set() and self._error is None:
+            try:
+                self._step_once()
+            except Exception as e:  # noqa: BLE001 - one bad step must not end serving
+                self._on_failure(e)
+        if self._error is not None:  # unhealthy: refuse what is still queued
+            while True:
+                try:
+                    item = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if not item[3].done():
+                    item[3].set_exception(EngineUnavailable(f"engine unhealthy: {self._error!r}"))
 
     def stats(self) -> dict:
         d = self.engine.stats()
-        lat = sorted(self.latencies_ms[-4096:])
+        lat = sorted(self.latencies_ms)
         if lat:
             d["p50_latency_ms"] = lat[len(lat) // 2]
             d["p99_latency_ms"] = lat[min(len(lat) - 1, int(len(lat) * 0.99))]
         d["queue_depth"] = self._q.qsize()
+        d["max_queue"] = self.max_queue
         d["cancelled"] = self.cancelled
-        d["healthy"] = self._error is None
+        d["rejected"] = self.rejected
+        d["expired"] = self.expired
+        d["prefill_tokens_per_s_est"] = round(self._prefill_tps, 1) if self._prefill_tps else None
+        d["healthy"] = self.healthy
+        if self._error is not None:
+            d["error"] = repr(self._error)
         return d
 
     def close(self) -> None:

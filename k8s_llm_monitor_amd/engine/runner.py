@@ -98,31 +98,44 @@ class ModelRunner:
         return tok
 
     # --------------------------------------------------------------------- prefill
-    def prefill(self, seqs: list[Sequence]) -> list[int]:
+    def prefill(self, seqs: list[Sequence], decode: Optional[list] = None) -> list[int]:
         """Run each sequence's scheduled prefill chunk: tokens [num_computed, num_computed + chunk)
         of its prompt (+ any tokens generated before a preemption); the first num_computed tokens
         already have their KV in the cache (prefix-cache hits, earlier chunks) and are attended
-        through the paged flash prefill.  Returns the token sampled after each chunk (the first
-        output token of sequences whose prompt this step completes)."""
+        through the paged flash prefill.  ``decode`` (a mixed step): running sequences that also
+        get their next token in this forward - their rows come first and attend through
+        paged_decode.  Returns the sampled token of every decode row, then of every chunk (the
+        first output token of the sequences whose prompt this step completes)."""
         dev = self.device
+        decode = decode or []
+        nd = len(decode)
         starts = [s.num_computed for s in seqs]
         lens = [s.chunk or (s.num_tokens - c) for s, c in zip(seqs, starts)]
-        ids = np.concatenate([np.asarray(s.all_ids[c:c + n], dtype=np.int32) for s, c, n in zip(seqs, starts, lens)])
-        pos = np.concatenate([np.arange(c, c + n, dtype=np.int32) for c, n in zip(starts, lens)])
-        slots = np.empty(ids.shape[0], dtype=np.int32)
-        o = 0
+        T = nd + sum(lens)
+        ids = np.empty(T, dtype=np.int32)
+        pos = np.empty(T, dtype=np.int32)
+        slots = np.empty(T, dtype=np.int32)
+        for i, q in enumerate(decode):  # the token being fed is the last generated one
+            p = q.num_tokens - 1
+            ids[i] = q.last_token
+            pos[i] = p
+            slots[i] = q.block_table[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
+        o = nd
         for s, c, n in zip(seqs, starts, lens):
-            bt = np.asarray(s.block_table, dtype=np.int64)
-            p = np.arange(c, c + n)
+            ids[o:o + n] = s.all_ids[c:c + n]
+            p = np.arange(c, c + n, dtype=np.int32)
+            pos[o:o + n] = p
+            bt = np.asarray(s.block_table, dtype=np.int32)
             slots[o:o + n] = bt[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
             o += n
         cu = np.zeros(len(seqs) + 1, dtype=np.int32)
         cu[1:] = np.cumsum(lens)
         qs, st = ops.prefill_qblocks(cu.tolist())
         t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dt, non_blocking=True)
+        logits_idx = np.concatenate([np.arange(nd, dtype=np.int64), nd + cu[1:].astype(np.int64) - 1])
         meta = AttnMeta(is_prefill=True, positions=t(pos), slot_mapping=t(slots), cu_seqlens=t(cu),
                         qb_seq=t(np.asarray(qs, dtype=np.int32)), qb_start=t(np.asarray(st, dtype=np.int32)),
-                        logits_idx=t(cu[1:] - 1, torch.int64))
+                        logits_idx=t(logits_idx, torch.int64))
         if any(starts):
             W = max(len(s.block_table) for s in seqs)
             bt = np.zeros((len(seqs), W), dtype=np.int32)
@@ -130,16 +143,27 @@ class ModelRunner:
                 bt[i, : len(s.block_table)] = s.block_table
             meta.ctx_start = t(np.asarray(starts, dtype=np.int32))
             meta.block_tables = t(bt)
+        if nd:
+            W = max(len(q.block_table) for q in decode)
+            bt = np.zeros((nd, W), dtype=np.int32)
+            for i, q in enumerate(decode):
+                bt[i, : len(q.block_table)] = q.block_table
+            meta.num_decode = nd
+            meta.dec_block_tables = t(bt)
+            meta.dec_seq_lens = t(np.asarray([q.num_tokens for q in decode], dtype=np.int32))
+            meta.decode_ws = self.decode_ws
+            self.n_steps["mixed"] = self.n_steps.get("mixed", 0) + 1
         # tokens attended from the paged cache instead of recomputed (prefix hits + earlier chunks)
         self.n_steps["prefill_context_tokens"] = self.n_steps.get("prefill_context_tokens", 0) + sum(starts)
+        self.n_steps["prefill_tokens"] = self.n_steps.get("prefill_tokens", 0) + T
         logits = self.model.forward(t(ids), meta, self.kv)
-        S = len(seqs)
-        temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32).to(dev)
-        topk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int32).to(dev)
-        topp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32).to(dev)
+        rows = list(decode) + list(seqs)
+        temp = torch.tensor([s.params.temperature for s in rows], dtype=torch.float32).to(dev)
+        topk = torch.tensor([s.params.top_k for s in rows], dtype=torch.int32).to(dev)
+        topp = torch.tensor([s.params.top_p for s in rows], dtype=torch.float32).to(dev)
         tok = self._sample(logits, temp, topk, topp)
         self.n_steps["prefill"] += 1
-        return tok[:S].cpu().tolist()
+        return tok[: len(rows)].cpu().tolist()
 
     # --------------------------------------------------------------------- decode
     def _decode_body(self, b: int) -> None:

@@ -1,14 +1,20 @@
 """Continuous-batching scheduler.
 
-Each engine step is either a *prefill* step (admit waiting requests while the token budget and
-the free KV blocks last; a prompt larger than the remaining budget is prefilled in chunks over
-several steps) or a *decode* step (one token for every fully prefilled running sequence).
-Prefill has priority so newly arrived diagnostic queries join the running batch at the next
-step; decode steps are captured hipGraphs, so keeping them homogeneous keeps them replayable.
-When the cache runs out during decode the most recently admitted sequence is preempted
-(blocks freed, re-queued at the front, recomputed later) - a full cache degrades throughput, it
-never fails requests ("OOM on KV-cache allocation leads to request rejection with
-503, not a crash"; here it does not even reject).
+A step is one of
+* *decode*  - one token for every fully prefilled running sequence (replayed from a hipGraph);
+* *prefill* - prompt chunks of newly admitted (or partially prefilled) sequences within the
+  step's token budget; a prompt larger than the remaining budget is prefilled in chunks;
+* *mixed*   - prefill chunks AND one decode token for every running sequence, in one forward
+  (SURVEY.md §7.2 step 10): the decode rows ride along the prefill GEMMs, so running answers keep
+  streaming while new queries are admitted instead of stalling behind every prefill step.  The
+  prefill budget of a mixed step is ``mixed_prefill_tokens`` (a bound on the TPOT hiccup a new
+  arrival costs the running decodes); a prefill-only step uses ``max_prefill_tokens``.
+
+When the KV cache runs out during decode the most recently admitted sequence is preempted (blocks
+freed, re-queued at the front, recomputed later).  Admission of a new sequence requires its
+blocks (fresh + prefix-cache hits parked in the LRU) to be free beyond a small watermark; the
+serving layer (EngineService) bounds the waiting queue and rejects with 503 beyond it
+("OOM on KV-cache allocation leads to request rejection with 503, not a crash").
 """
 from __future__ import annotations
 
@@ -30,13 +36,23 @@ class SchedulerConfig:
     # prefill), so every prefill step computes at most max_prefill_tokens tokens - a bound on the
     # step's activation memory and on how long running decodes wait behind a long prompt
     chunked_prefill: bool = True
+    # mixed prefill+decode steps (see the module docstring); 0 = prefill steps stall decodes
+    mixed_prefill_tokens: int = 8192
 
 
 @dataclass
 class StepPlan:
+    """``is_prefill``: the step runs the eager prefill path over ``seqs`` (prompt chunks), plus one
+    token for each of ``decode`` (a mixed step).  Otherwise ``seqs`` are the decode rows."""
+
     is_prefill: bool
     seqs: list[Sequence] = field(default_factory=list)
     preempted: list[Sequence] = field(default_factory=list)
+    decode: list[Sequence] = field(default_factory=list)
+
+    @property
+    def is_mixed(self) -> bool:
+        return self.is_prefill and bool(self.decode)
 
     @property
     def empty(self) -> bool:
@@ -79,13 +95,20 @@ class Scheduler:
             not q.prefilled for q in self.running)
 
     def schedule(self) -> StepPlan:
-        # 1. prefill: first the next chunks of partially prefilled sequences, then newly arrived
-        #    (or preempted) requests, within the step's token budget
-        partial = [q for q in self.running if not q.prefilled]
-        if partial or (self.waiting and len(self.running) < self.cfg.max_num_seqs):
-            plan = StepPlan(is_prefill=True)
+        want_prefill = self.prefill_pending()
+        ready = any(q.prefilled for q in self.running)
+        mix = want_prefill and ready and self.cfg.mixed_prefill_tokens > 0
+        plan = StepPlan(is_prefill=False)
+        if mix:  # reserve the decode rows' slots first: preemption here frees blocks for admission
+            plan.decode = self._reserve_decode(plan)
+            mix = bool(plan.decode)
+        if want_prefill:
+            # prefill: first the next chunks of partially prefilled sequences, then newly arrived
+            # (or preempted) requests, within the step's token budget
             budget = self.cfg.max_prefill_tokens
-            for seq in partial:
+            if mix:
+                budget = min(budget, self.cfg.mixed_prefill_tokens)
+            for seq in [q for q in self.running if not q.prefilled]:
                 if budget <= 0:
                     break
                 self._take_chunk(seq, budget, plan)
@@ -95,30 +118,34 @@ class Scheduler:
                 n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens left to compute
                 if n > budget and not self.cfg.chunked_prefill and plan.seqs:
                     break
-                if not self.blocks.can_allocate(seq):
-                    break
+                if not self.blocks.can_allocate(seq) or not self.blocks.allocate(seq):
+                    break  # allocate() undoes its prefix matches on failure: seq stays queued
                 self.waiting.popleft()
-                self.blocks.allocate(seq)
                 seq.status = SeqStatus.RUNNING
                 self.running.append(seq)
                 self._take_chunk(seq, budget if self.cfg.chunked_prefill else n, plan)
                 budget -= seq.chunk
             if plan.seqs:
+                plan.is_prefill = True
                 return plan
-        # 2. decode every running sequence
-        plan = StepPlan(is_prefill=False)
+        # decode every running (fully prefilled) sequence
+        rows = plan.decode if mix else self._reserve_decode(plan)
+        return StepPlan(is_prefill=False, seqs=rows, preempted=plan.preempted)
+
+    def _reserve_decode(self, plan: StepPlan) -> list[Sequence]:
+        """Make room for one more token of every prefilled running sequence, preempting the
+        youngest running sequence while the cache is short; returns the decode rows."""
         i = 0
         while i < len(self.running):
             seq = self.running[i]
-            if self.blocks.ensure_slot(seq):
+            if not seq.prefilled or self.blocks.ensure_slot(seq):
                 i += 1
                 continue
             victim = self.running.pop()  # youngest
             self._preempt(victim)
             plan.preempted.append(victim)
             # retry the same index (the victim may have been this very sequence)
-        plan.seqs = list(self.running)
-        return plan
+        return [q for q in self.running if q.prefilled]
 
     def _take_chunk(self, seq: Sequence, budget: int, plan: StepPlan) -> None:
         """Schedule seq's next prefill chunk (at most ``budget`` tokens) into ``plan``."""

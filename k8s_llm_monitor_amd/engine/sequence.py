@@ -53,6 +53,7 @@ class Sequence:
     chunk: int = 0
     prefilled: bool = False
     user: object = None  # opaque payload for the caller (future, callback, ...)
+    deadline: Optional[float] = None  # time.perf_counter() by which the answer is due (engine.add_request)
 
     @property
     def num_tokens(self) -> int:

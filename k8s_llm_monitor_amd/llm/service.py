@@ -24,6 +24,7 @@ import time
 import urllib.request
 import uuid
 from collections import OrderedDict
+from concurrent.futures import TimeoutError as FutTimeout
 from typing import Optional
 
 from ..monitor.types import AnalysisRequest, AnalysisResponse
@@ -42,13 +43,19 @@ class LocalEngineBackend:
     provider = "local-rocm"
 
     def __init__(self, service, max_tokens: int = 2000, temperature: float = 0.1, top_p: float = 1.0,
-                 top_k: int = 0, timeout_s: float = 30.0):
+                 top_k: int = 0, timeout_s: float = 30.0, answer_budget_s: Optional[float] = None):
+        """``timeout_s`` is ``llm.timeout``.  ``answer_budget_s`` (default: timeout_s): the time a
+        synchronous answer may take - the server sets it below its write timeout
+        (``answer_budget``) so the engine ends the generation at the deadline with
+        finish_reason "deadline" and the caller gets the answer generated so far, instead of a 504
+        while the GPU keeps generating for a client that has gone."""
         from ..engine import SamplingParams
 
         self.svc = service
         self.model = service.engine.model_cfg.name
         self.default = SamplingParams(max_tokens=max_tokens, temperature=temperature, top_p=top_p, top_k=top_k)
         self.timeout_s = timeout_s
+        self.answer_budget_s = answer_budget_s if answer_budget_s is not None else (timeout_s if timeout_s > 0 else None)
         self.tokenizer = service.engine.tokenizer
 
     def count_tokens(self, text: str) -> int:
@@ -62,8 +69,15 @@ class LocalEngineBackend:
         p = SamplingParams(max_tokens=max_tokens or d.max_tokens,
                            temperature=d.temperature if temperature is None else temperature,
                            top_k=d.top_k, top_p=d.top_p, ignore_eos=ignore_eos)
-        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id)
-        text, seq = fut.result(timeout=self.timeout_s if self.timeout_s > 0 else None)
+        budget = self.answer_budget_s
+        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id,
+                              deadline=time.perf_counter() + budget if budget else None)
+        try:
+            # the engine stops the sequence at the deadline; the grace covers the last step + detokenize
+            text, seq = fut.result(timeout=budget + 2.0 if budget else None)
+        except FutTimeout:
+            self.svc.cancel(fut)  # free the KV blocks: nobody waits for this answer any more
+            raise TimeoutError("answer not ready within the answer budget") from None
         t = seq.timings()
         return GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason, **t)
 
@@ -82,7 +96,8 @@ class LocalEngineBackend:
                            temperature=d.temperature if temperature is None else temperature,
                            top_k=d.top_k, top_p=d.top_p, ignore_eos=ignore_eos)
         q: queue.SimpleQueue = queue.SimpleQueue()
-        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id, on_tokens=q.put)
+        fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id, on_tokens=q.put,
+                              deadline=time.perf_counter() + self.timeout_s if self.timeout_s > 0 else None)
         det = IncrementalDetokenizer(self.tokenizer)
         deadline = time.monotonic() + self.timeout_s if self.timeout_s > 0 else None
         try:
@@ -278,11 +293,15 @@ class AnalysisService:
     # ------------------------------------------------------------------ entry points
     def _respond(self, rid: str, kind: str, prompt: str, extra: dict, max_tokens: Optional[int] = None,
                  ignore_eos: bool = False) -> AnalysisResponse:
+        from ..engine import EngineOverloaded, EngineUnavailable
+
         try:
             g = self.backend.generate(prompt, max_tokens=max_tokens or self.max_tokens, request_id=rid,
                                       ignore_eos=ignore_eos)
             result = {"type": kind, "answer": g.pop("text"), **g, **extra}
             resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
+        except (EngineOverloaded, EngineUnavailable):
+            raise  # admission refused: the HTTP layer answers 503 (nothing to record)
         except Exception as e:  # noqa: BLE001 - an engine failure becomes an error record, not a 500
             log.error("analysis %s failed: %s", rid, e)
             resp = AnalysisResponse(request_id=rid, status="error", result={"type": kind, **extra},

@@ -56,6 +56,12 @@ class AttnMeta:
     block_tables: Optional[torch.Tensor] = None  # [B, W] int32
     seq_lens: Optional[torch.Tensor] = None  # [B] int32 (including the token being decoded)
     decode_ws: Optional[tuple] = None  # paged_decode partial buffers
+    # mixed prefill+decode step (is_prefill): the first num_decode rows are single decode tokens
+    # attending their paged context through paged_decode; cu_seqlens / qb_* / ctx_start /
+    # block_tables then describe the prefill rows that follow
+    num_decode: int = 0
+    dec_block_tables: Optional[torch.Tensor] = None  # [num_decode, W] int32
+    dec_seq_lens: Optional[torch.Tensor] = None  # [num_decode] int32 (including the decoded token)
 
 
 def _seed_for(name: str, seed: int) -> int:
@@ -258,8 +264,18 @@ class CausalLM:
             paged = None
             if meta.ctx_start is not None:  # some prompts start with cached prefix blocks
                 paged = (meta.ctx_start, k_cache, v_cache, meta.block_tables)
-            o = ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb,
-                                  paged=paged)
+            nd = meta.num_decode
+            if nd == 0:
+                return ops.flash_prefill(qkv, meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb,
+                                         paged=paged)
+            # mixed step: decode rows through paged_decode, prefill rows through flash prefill
+            o = torch.empty(qkv.shape[0], self.hq * self.D, dtype=qkv.dtype, device=qkv.device)
+            ops.paged_decode(qkv[:nd], k_cache, v_cache, meta.dec_block_tables, meta.dec_seq_lens, self.hq,
+                             self.hkv, self.D, self.scale, workspace=meta.decode_ws, out=o[:nd])
+            op = ops.flash_prefill(qkv[nd:], meta.cu_seqlens, self.hq, self.hkv, self.D, self.scale, qblocks=qb,
+                                   paged=paged, out=o[nd:])
+            if op.data_ptr() != o[nd:].data_ptr():  # CPU reference paths return a fresh tensor
+                o[nd:] = op
         else:
             out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device) if slabs is not None else None
             o = ops.paged_decode(qkv, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.hq, self.hkv,

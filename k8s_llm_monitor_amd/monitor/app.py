@@ -145,15 +145,20 @@ def build_monitor(cfg: Config, backend=None, start_manager: bool = True, llm: bo
                                  max_context_events=cfg.analysis.max_context_events,
                                  token_budget=cfg.analysis.prompt_token_budget, max_tokens=cfg.llm.max_tokens)
     m.app = MonitorApp(m.client, m.manager, m.analysis, m.engine_service, llm_timeout_s=float(cfg.llm.timeout))
+    if hasattr(backend_llm, "answer_budget_s"):  # the engine stops generations before the write timeout
+        backend_llm.answer_budget_s = m.app.answer_budget_s()
     m.analysis.analyzer = m.app.analyzer if analyzer is None else analyzer
     return m
 
 
 # --------------------------------------------------------------------------- bench helpers
 
-def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0):
+def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0, write_timeout_s: float = 600.0,
+                        llm_timeout_s: float = 600.0):
     """An HTTP server in this process whose /api/v1/query is served by ``engine_service``
-    (FakeCluster behind it, metrics collected once).  Returns (server, port)."""
+    (FakeCluster behind it, metrics collected once).  Returns (server, port).  The default
+    timeouts are the bench's (long waves); ``write_timeout_s=15, llm_timeout_s=30`` is the
+    production server's (reference cmd/server/main.go:147-148, config.go:141-145)."""
     from ..llm.service import AnalysisService, LocalEngineBackend
     from .cluster.fake import FakeCluster
     from .cluster.client import K8sClient
@@ -166,9 +171,11 @@ def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0):
     client = K8sClient(fake, cfg.k8s)
     mgr = MetricsManager(fake, ManagerConfig(namespaces=["default", "kube-system"]))
     mgr.collect()
-    backend = LocalEngineBackend(engine_service, max_tokens=2000, temperature=0.1, timeout_s=600.0)
+    backend = LocalEngineBackend(engine_service, max_tokens=2000, temperature=0.1, timeout_s=llm_timeout_s)
     analysis = AnalysisService(backend, manager=mgr, client=client)
-    app = MonitorApp(client, mgr, analysis, engine_service, write_timeout_s=600.0, llm_timeout_s=600.0)
+    app = MonitorApp(client, mgr, analysis, engine_service, write_timeout_s=write_timeout_s,
+                     llm_timeout_s=llm_timeout_s)
+    backend.answer_budget_s = app.answer_budget_s()
     analysis.analyzer = app.analyzer
     srv = make_server(app, host, port)
     threading.Thread(target=srv.serve_forever, name="bench-http", daemon=True).start()

@@ -35,6 +35,18 @@ from ..utils import gojson
 from ..utils.gojson import utcnow
 from .types import AnalysisRequest, AnalysisResponse, UAVReport
 
+
+def _busy_types() -> tuple:
+    try:
+        from ..engine.engine import EngineOverloaded, EngineUnavailable
+
+        return (EngineOverloaded, EngineUnavailable)
+    except Exception:  # noqa: BLE001 - no torch: nothing can be busy
+        return (type("_NeverRaised", (Exception,), {}),)
+
+
+_BUSY = _busy_types()
+
 log = logging.getLogger("server")
 WEB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "web")
 VERSION = "1.0.0"
@@ -150,6 +162,13 @@ class MonitorApp:
 
     # ------------------------------------------------------------------ reference routes
     def health(self, method, body, q) -> Reply:
+        """Reference contract (always healthy), except that a configured in-process engine which
+        has gone unhealthy (EngineService: repeated step failures / dead engine thread) answers 503
+        so a Kubernetes liveness probe restarts the pod."""
+        svc = self.engine_service
+        if svc is not None and not getattr(svc, "healthy", True):
+            return json_reply({"status": "unhealthy", "error": "LLM engine failed", "timestamp": utcnow(),
+                               "version": VERSION}, 503)
         return json_reply({"status": "healthy", "timestamp": utcnow(), "version": VERSION})
 
     def cluster_status(self, method, body, q) -> Reply:
@@ -204,6 +223,8 @@ class MonitorApp:
                 resp["llm"] = rec
             except FutTimeout:
                 resp["llm"] = {"status": "error", "error": "llm timeout"}
+            except _BUSY as e:
+                resp["llm"] = {"status": "error", "error": f"llm overloaded: {e}"}
         return json_reply(resp)
 
     def _mgr(self):
@@ -315,11 +336,23 @@ class MonitorApp:
 
         return self.analysis is not None and not isinstance(self.analysis.backend, RuleBackend)
 
+    def answer_budget_s(self) -> float:
+        """Time an engine generation may take so the answer still beats the write timeout: the
+        engine ends the sequence at this deadline (finish_reason "deadline") - a truncated answer
+        instead of a 504 (LocalEngineBackend.answer_budget_s)."""
+        return max(0.5, min(self.llm_timeout_s, self.write_timeout_s) - 1.25)
+
     def _bounded(self, fn):
         """Run fn within the write timeout (leave 0.5 s to write the answer).  One shared pool (no
-        thread spawned per request); a timed-out call keeps its worker until the engine answers."""
+        thread spawned per request).  The engine itself stops at answer_budget_s (0.75 s earlier),
+        so this limit is a backstop; the backend cancels the engine request if it ever fires."""
         limit = max(0.5, min(self.llm_timeout_s, self.write_timeout_s) - 0.5)
         return _bounded_pool().submit(fn).result(timeout=limit)
+
+    @staticmethod
+    def _busy_reply(e: Exception) -> Reply:
+        return json_reply(AnalysisResponse(request_id="", status="error", error=f"engine busy: {e}",
+                                           timestamp=utcnow()), 503)
 
     def query(self, method, body, q) -> Reply:
         _only(method, "POST")
@@ -356,6 +389,8 @@ class MonitorApp:
             resp = self._bounded(lambda: self.analysis.query(question, max_tokens=mt,
                                                              ignore_eos=bool(d.get("ignore_eos", False)),
                                                              context_text=ctx_text))
+        except _BUSY as e:
+            return self._busy_reply(e)
         except FutTimeout:
             resp = AnalysisResponse(request_id="", status="error", result={"question": question},
                                     error="answer not ready within the server write timeout", timestamp=utcnow())
@@ -373,6 +408,8 @@ class MonitorApp:
                               context=d.get("context") or {})
         try:
             resp = self._bounded(lambda: self.analysis.analyze(req))
+        except _BUSY as e:
+            return self._busy_reply(e)
         except ValueError as e:
             raise http_error(400, str(e))
         except FutTimeout:

@@ -110,6 +110,18 @@ class BlockPool {
     return n;
   }
 
+  // Of the leading cached hashes, how many map to blocks with no reference (parked in the LRU):
+  // matching those takes them out of the free pool, so admission must count them as consumed.
+  int peek_idle(const std::vector<uint64_t>& hashes) const {
+    int n = 0;
+    for (uint64_t h : hashes) {
+      auto it = map_.find(h);
+      if (it == map_.end()) break;
+      if (ref_[it->second] == 0) ++n;
+    }
+    return n;
+  }
+
   // Longest cached prefix; takes one reference on every returned block.
   std::vector<int> match(const std::vector<uint64_t>& hashes) {
     std::vector<int> out;
@@ -424,6 +436,7 @@ PYBIND11_MODULE(_k8sllm_runtime, m) {
   py::class_<BlockPool>(m, "BlockPool")
       .def(py::init<int>())
       .def("peek", &BlockPool::peek)
+      .def("peek_idle", &BlockPool::peek_idle)
       .def("match", &BlockPool::match)
       .def("allocate", &BlockPool::allocate)
       .def("publish", &BlockPool::publish)
