@@ -2,26 +2,42 @@
 """Headline benchmark: diagnostic queries/sec + p50 answer latency, Llama-3-8B TP=1, on the
 ``/api/v1/query`` path (BASELINE.json "metric").
 
-One process per GPU (torchrun launches N ranks); each rank is an independent TP=1 engine replica
-(data-parallel serving, weak scaling: per-GPU work is fixed).  One *step* = one wave of
-``--batch`` concurrent diagnostic queries per GPU, each a synthetic cluster-state prompt in the
-reference's prompt format answered with up to ``--max-new-tokens`` tokens through the
-continuous-batching engine (prefill + hipGraph decode + sampling).  With ``--path http`` (default)
-every query is a real ``POST /api/v1/query`` to the in-process REST server, sent by a child
-load-generator process (``--client process``, default: remote clients do not share the serving
-process's interpreter lock; ``--client thread`` keeps them in-process); ``--path engine``
-submits to the engine queue directly (same engine, no HTTP).
+Process model: one process per GPU.  ``python bench.py --gpus N`` launches N rank processes by
+itself (before anything touches a GPU) when it is not already running under torchrun; under
+``torch.distributed.run`` (the driver's multi-GPU command) each process is one rank.  Ranks form
+``N / tp`` engine replicas (data parallel, weak scaling: per-replica work is fixed) of ``--tp``
+GPUs each (tensor parallel over RCCL / the one-shot IPC all-reduce).  The TP leader of each
+replica serves HTTP; its TP workers mirror its steps (parallel/step_bus.py).
 
-Timing: W untimed warmup waves, then a barrier + device sync, K timed waves, a device sync + barrier;
-the elapsed time is the MAX over ranks.  ``value`` = total queries answered by all ranks / that
-time.  Weights are random-init (no checkpoints offline), prompts are synthetic (``data``).
+Modes (``--mode``):
+* ``wave`` (default, the headline) - one step = one closed-loop wave of ``--batch`` concurrent
+  diagnostic queries per replica, each a synthetic cluster-state prompt in the reference's prompt
+  format answered with ``--max-new-tokens`` tokens through the continuous-batching engine.
+* ``poisson`` - open loop: ``--steps x --batch`` queries per replica arriving as a Poisson process
+  at ``--rate`` queries/s; reports TTFT / TPOT / latency percentiles (mixed prefill+decode steps
+  at work).
+* ``latency`` - batch 1: one query at a time; a step = one query.
+``--production``: the server runs with the reference's timeouts (15 s write, 30 s llm.timeout)
+instead of the bench's 600 s; answers that reach the deadline come back truncated
+(finish_reason "deadline") and overload as 503 - both are counted in the JSON line.
+
+With ``--path http`` (default) every query is a real ``POST /api/v1/query`` to the in-process REST
+server, sent by a child load-generator process (``--client process``); ``--path engine`` submits
+to the engine queue directly; ``--path podcomm`` posts /api/v1/analyze/pod-communication.
+
+Timing: W untimed warmup steps, then a barrier + device sync, K timed steps, a device sync +
+barrier; the elapsed time is the MAX over ranks.  ``value`` = total queries answered by all
+replicas / that time.  Weights are random-init (no checkpoints offline), prompts are synthetic.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import random
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -29,17 +45,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+_MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "mixtral-8x7b": "Mixtral-8x7B",
+                "gpt2-small": "GPT-2-small"}
 
-def main() -> None:
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) of this node")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree of one engine replica")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
+    ap.add_argument("--batch", type=int, default=64, help="concurrent queries per replica per step")
     ap.add_argument("--max-new-tokens", type=int, default=256)
+    ap.add_argument("--mode", choices=["wave", "poisson", "latency"], default="wave")
+    ap.add_argument("--rate", type=float, default=16.0, help="poisson: arrivals per second per replica")
+    ap.add_argument("--production", action="store_true",
+                    help="reference server timeouts (15 s write / 30 s llm): deadline truncation + 503s")
     ap.add_argument("--kv-cache-gb", type=float, default=48.0)
     ap.add_argument("--max-prefill-tokens", type=int, default=16384, help="token budget of one prefill step")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=None,
+                    help="prefill budget of a mixed prefill+decode step (0: prefill stalls decodes)")
     ap.add_argument("--chunked-prefill", type=int, default=1, choices=[0, 1])
     ap.add_argument("--admit-gap-ms", type=float, default=None, help="engine admission coalescing gap (0 disables)")
     ap.add_argument("--admit-window-ms", type=float, default=None)
@@ -52,140 +78,275 @@ def main() -> None:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.mode == "latency":
+        a.batch = 1
+    if a.gpus < 1 or a.tp < 1 or a.gpus % a.tp:
+        ap.error(f"--tp {a.tp} must divide --gpus {a.gpus}")
+    return a
 
+
+# --------------------------------------------------------------------------- launcher
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list, timeout_s: float = 0.0) -> int:
+    """Run this script as ``n`` rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
+    GPU each) and return the first non-zero exit code (0 when all succeed).  Called before this
+    process touches any GPU; rank 0's stdout (the JSON line) is this process's stdout.  A rank that
+    fails takes the others down (they would otherwise wait in a collective forever)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      start_new_session=True))
+    t0 = time.time()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout_s and time.time() - t0 > timeout_s:
+                rc = 124
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, 15)
+                except ProcessLookupError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, 9)
+                p.wait()
+    return rc
+
+
+# --------------------------------------------------------------------------- one rank
+
+def _pct(xs: list, q: float):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return round(xs[min(len(xs) - 1, int(len(xs) * q))], 2)
+
+
+def run_rank(a) -> None:
+    env_rank = int(os.environ.get("RANK", "0"))
+    leader = env_rank % a.tp == 0
     loadgen = None
-    if a.path in ("http", "podcomm") and a.client == "process":
+    if leader and a.path in ("http", "podcomm") and a.client == "process":
         # started before this process initialises the GPU (the child never touches it)
         from k8s_llm_monitor_amd.monitor.loadgen import LoadGen
 
         loadgen = LoadGen(ROOT)
 
     import torch
+    import torch.distributed as dist
 
     from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
     from k8s_llm_monitor_amd.llm.synthetic import synthetic_cluster_prompt, synthetic_context
     from k8s_llm_monitor_amd.parallel import comm
-    from k8s_llm_monitor_amd.parallel.state import barrier_all, init_parallel
+    from k8s_llm_monitor_amd.parallel.state import init_parallel
 
-    ps = init_parallel(tp_size=1)
+    ps = init_parallel(tp_size=a.tp)
     rank, world = ps.rank, ps.world_size
-    if a.gpus != world and world > 1:
+    if a.gpus != world:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dp = world // a.tp
     on_gpu = ps.device.type == "cuda"
     if on_gpu:
         from k8s_llm_monitor_amd import ops
-        ops.native()  # fail loudly if the HIP kernels are missing
 
-    admit = {k: v for k, v in (("admit_gap_ms", a.admit_gap_ms), ("admit_window_ms", a.admit_window_ms))
-             if v is not None}
-    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, max_model_len=8192, **admit,
-                                 max_prefill_tokens=a.max_prefill_tokens, chunked_prefill=bool(a.chunked_prefill),
+        ops.native()  # fail loudly if the HIP kernels are missing
+    # the replicas' leaders synchronise the timed region among themselves (workers are inside
+    # worker_loop); every rank creates the group, in the same order
+    leaders_group = None
+    if world > 1:
+        leaders_group = dist.new_group(list(range(0, world, a.tp)), backend="gloo")
+
+    def leaders_barrier() -> None:
+        if leaders_group is not None:
+            dist.barrier(group=leaders_group)
+
+    admit = {k: v for k, v in (("admit_gap_ms", a.admit_gap_ms), ("admit_window_ms", a.admit_window_ms),
+                               ("mixed_prefill_tokens", a.mixed_prefill_tokens)) if v is not None}
+    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=max(a.batch, 8) if a.mode == "latency" else a.batch,
+                                 max_model_len=8192, max_prefill_tokens=a.max_prefill_tokens,
+                                 chunked_prefill=bool(a.chunked_prefill), tp_size=a.tp,
                                  kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
-                                 seed=a.seed + rank), pstate=ps)
+                                 seed=a.seed + ps.dp_rank, **admit), pstate=ps)
     eng.warmup()
-    svc = EngineService(eng)
-    server = None
+    devices = [str(ps.device)] * world
+    if world > 1:
+        dist.all_gather_object(devices, str(ps.device))
+
+    if not ps.tp_leader:  # TP worker: mirror the leader's steps, then join the final reductions
+        eng.worker_loop()
+        _finish(a, ps, comm, 0.0, 0, 0, 0, [], {}, devices, eng, on_gpu)
+        return
+
+    svc = EngineService(eng, max_queue=max(4 * a.batch, 256))
+    server = port = None
     if a.path in ("http", "podcomm"):
         from k8s_llm_monitor_amd.monitor.app import build_app_for_bench
 
-        server, port = build_app_for_bench(svc)
+        tmo = dict(write_timeout_s=15.0, llm_timeout_s=30.0) if a.production else {}
+        server, port = build_app_for_bench(svc, **tmo)
     params = SamplingParams(max_tokens=a.max_new_tokens, temperature=0.1, ignore_eos=True)
+    rng = random.Random(1234 + ps.dp_rank)
 
-    def wave(w: int) -> tuple[list[float], int, int]:
-        seeds = [rank * 1_000_003 + w * a.batch + i for i in range(a.batch)]
+    def post(items, offsets=None):
+        from k8s_llm_monitor_amd.monitor.app import post_queries
+
+        kw = dict(offsets_s=offsets, allow_errors=a.production or a.mode == "poisson")
+        return (loadgen.post_queries if loadgen else post_queries)(port, items, a.max_new_tokens, **kw)
+
+    def step(w: int) -> list[dict]:
+        """One bench step; per-request result dicts (http_status, latency_ms, ttft_ms, tokens)."""
+        n = a.batch
+        seeds = [ps.dp_rank * 1_000_003 + w * n + i for i in range(n)]
         if a.path == "http":
-            from k8s_llm_monitor_amd.monitor.app import post_queries
-
             items = [synthetic_context(s)[::-1] for s in seeds]  # (question, cluster context)
-            res = (loadgen.post_queries if loadgen else post_queries)(port, items, a.max_new_tokens)
-            lat = [r["http_latency_ms"] for r in res]
-            ptok = sum(r["prompt_tokens"] for r in res)
-            gtok = sum(r["completion_tokens"] for r in res)
-        elif a.path == "podcomm":
+            if a.mode == "poisson":
+                t, offs = 0.0, []
+                for _ in items:
+                    t += rng.expovariate(a.rate)
+                    offs.append(t)
+                return post(items, offs)
+            return post(items)
+        if a.path == "podcomm":
             from k8s_llm_monitor_amd.monitor.app import bench_pod_pairs, post_pod_communication
 
-            pairs = bench_pod_pairs(a.batch * (w + 1))[a.batch * w:]
-            res = (loadgen.post_pod_communication if loadgen else post_pod_communication)(port, pairs,
+            pairs = bench_pod_pairs(n * (w + 1))[n * w:]
+            return (loadgen.post_pod_communication if loadgen else post_pod_communication)(port, pairs,
                                                                                           a.max_new_tokens)
-            lat = [r["http_latency_ms"] for r in res]
-            ptok = sum(r["prompt_tokens"] for r in res)
-            gtok = sum(r["completion_tokens"] for r in res)
-        else:
-            futs = [svc.submit(synthetic_cluster_prompt(s), params) for s in seeds]
-            outs = [f.result() for f in futs]
-            lat = [s.timings()["latency_ms"] for _, s in outs]
-            ptok = sum(len(s.prompt_ids) for _, s in outs)
-            gtok = sum(len(s.output_ids) for _, s in outs)
-        return lat, ptok, gtok
+        futs = [svc.submit(synthetic_cluster_prompt(s), params) for s in seeds]
+        out = []
+        for f in futs:
+            _, s = f.result()
+            d = s.timings()
+            d.update(http_status=200, http_latency_ms=d["latency_ms"], finish_reason=s.finish_reason)
+            out.append(d)
+        return out
 
     for w in range(a.warmup):
-        wave(w)
-    barrier_all()
+        step(w)
+    leaders_barrier()
     if on_gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lats, ptoks, gtoks = [], 0, 0
+    res: list[dict] = []
     for k in range(a.steps):
-        lat, p, g = wave(a.warmup + k)
-        lats += lat
-        ptoks += p
-        gtoks += g
+        res += step(a.warmup + k)
     if on_gpu:
         torch.cuda.synchronize()
-    barrier_all()
+    leaders_barrier()
     elapsed = time.perf_counter() - t0
-    t_max = comm.all_reduce_max_scalar(elapsed)
-    total_q = comm.all_reduce_sum_scalar(float(a.batch * a.steps))
-    total_gen = comm.all_reduce_sum_scalar(float(gtoks))
-    p50_local = statistics.median(lats)
-    p50 = comm.all_reduce_max_scalar(p50_local)
+    ok = [r for r in res if r.get("http_status", 200) == 200]
     stats = svc.stats()
     if eng.trace is not None and rank == 0:
         _print_trace(eng.trace, t0)
-    svc.close()
+    svc.close()  # stops this replica's TP workers
     if server is not None:
         server.shutdown()
     if loadgen is not None:
         loadgen.close()
-    if rank == 0:
-        qps = total_q / t_max
-        name = _MODEL_NAMES.get(a.model, a.model)
-        metric = (f"pod-communication analyses/sec ({name} TP=1, /api/v1/analyze/pod-communication)"
-                  if a.path == "podcomm" else f"diagnostic queries/sec ({name} TP=1, /api/v1/query)")
-        res = {
-            "metric": metric,
-            "value": round(qps, 4),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(t_max / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
-            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": 8192,
-                       "parallelism": f"dp{world}" if world > 1 else "tp1",
-                       "prompt_tokens_mean": round(ptoks / max(1, a.batch * a.steps), 1),
-                       "max_new_tokens": a.max_new_tokens, "path": a.path,
-                       "client": a.client if a.path != "engine" else None},
-            "p50_latency_ms": round(p50, 2),
-            "p99_latency_ms": round(sorted(lats)[min(len(lats) - 1, int(len(lats) * 0.99))], 2),
-            "generated_tokens_per_s": round(total_gen / t_max, 1),
-            "decode_steps": stats.get("decode_steps"),
-            "prefill_steps": stats.get("prefill_steps"),
-        }
-        line = json.dumps(res)
-        print(line, flush=True)
-        if a.out:
-            with open(a.out, "w") as f:
-                f.write(line + "\n")
+    ptoks = sum(r.get("prompt_tokens", 0) for r in ok)
+    gtoks = sum(r.get("completion_tokens", 0) for r in ok)
+    _finish(a, ps, comm, elapsed, len(ok), ptoks, gtoks, res, stats, devices, eng, on_gpu)
 
 
-_MODEL_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B", "mixtral-8x7b": "Mixtral-8x7B",
-                "gpt2-small": "GPT-2-small"}
+def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, on_gpu) -> None:
+    world = ps.world_size
+    t_max = comm.all_reduce_max_scalar(elapsed)
+    total_q = comm.all_reduce_sum_scalar(float(n_ok))
+    total_gen = comm.all_reduce_sum_scalar(float(gtoks))
+    total_p = comm.all_reduce_sum_scalar(float(ptoks))
+    ok = [r for r in res if r.get("http_status", 200) == 200]
+    lats = [r["http_latency_ms"] for r in ok]
+    p50 = comm.all_reduce_max_scalar(statistics.median(lats) if lats else 0.0)
+    if ps.rank != 0:
+        return
+    dp = world // a.tp
+    name = _MODEL_NAMES.get(a.model, a.model)
+    tp_s = f"TP={a.tp}"
+    metric = (f"pod-communication analyses/sec ({name} {tp_s}, /api/v1/analyze/pod-communication)"
+              if a.path == "podcomm" else f"diagnostic queries/sec ({name} {tp_s}, /api/v1/query)")
+    if world == 1:
+        par = "tp1"
+    elif a.tp == 1:
+        par = f"dp{dp}"
+    elif dp == 1:
+        par = f"tp{a.tp}"
+    else:
+        par = f"dp{dp}tp{a.tp}"
+    out = {
+        "metric": metric,
+        "value": round(total_q / t_max, 4) if t_max > 0 else 0.0,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(t_max / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
+        "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": 8192, "parallelism": par,
+                   "prompt_tokens_mean": round(total_p / max(1.0, total_q), 1),
+                   "max_new_tokens": a.max_new_tokens, "path": a.path, "mode": a.mode,
+                   "client": a.client if a.path != "engine" else None,
+                   "server_timeouts": "production 15s/30s" if a.production else "bench 600s"},
+        "p50_latency_ms": round(p50, 2),
+        "p99_latency_ms": _pct(lats, 0.99),
+        "generated_tokens_per_s": round(total_gen / t_max, 1) if t_max > 0 else 0.0,
+        "decode_steps": stats.get("decode_steps"),
+        "prefill_steps": stats.get("prefill_steps"),
+        "mixed_steps": stats.get("mixed_steps"),
+        "dist": {"world_size": world, "tp": a.tp, "dp": dp, "devices": devices,
+                 "backend": _backend(), "custom_allreduce": ps.custom_ar is not None,
+                 "step_bus": type(eng.bus).__name__ if eng.bus is not None else None},
+    }
+    if a.mode != "wave" or a.production:  # rank-0 replica's request-level detail
+        ttft = [r["ttft_ms"] for r in ok if r.get("ttft_ms") is not None]
+        tpot = [(r["latency_ms"] - r["ttft_ms"]) / (r["completion_tokens"] - 1) for r in ok
+                if r.get("ttft_ms") is not None and r.get("completion_tokens", 0) > 1]
+        out["requests"] = {"sent": len(res) * dp, "ok_rank0": len(ok), "rejected_503_rank0":
+                           sum(r.get("http_status") == 503 for r in res),
+                           "timeout_504_rank0": sum(r.get("http_status") == 504 for r in res),
+                           "deadline_truncated_rank0": sum(r.get("finish_reason") == "deadline" for r in ok)}
+        out["ttft_ms"] = {"p50": _pct(ttft, 0.5), "p99": _pct(ttft, 0.99)}
+        out["tpot_ms"] = {"p50": _pct(tpot, 0.5), "p99": _pct(tpot, 0.99)}
+        if a.mode == "poisson":
+            out["config"]["rate_per_replica"] = a.rate
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+
+
+def _backend():
+    import torch.distributed as dist
+
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
 
 
 def _print_trace(trace: list, t0: float) -> None:
@@ -204,10 +365,6 @@ def _print_trace(trace: list, t0: float) -> None:
             cur = []
         cur.append(e)
     waves.append(cur)
-    subs = [e[0] for e in ev if e[1] == "submit"]
-    if subs:
-        print(f"[trace] submits {len(subs)}: " + " ".join(f"{(t - t0) * 1e3:.0f}" for t in subs[:200]), file=sys.stderr)
-        print("[trace] adds: " + " ".join(f"{(e[0] - t0) * 1e3:.0f}" for e in adds[:200]), file=sys.stderr)
     for w in waves:
         gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
         print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"
@@ -218,6 +375,14 @@ def _print_trace(trace: list, t0: float) -> None:
     if dec:
         print(f"[trace] decode steps {len(dec)} first +{(dec[0][0] - t0) * 1e3:.1f} last +{(dec[-1][0] - t0) * 1e3:.1f} ms",
               file=sys.stderr)
+
+
+def main(argv=None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, argv))
+    run_rank(a)
 
 
 if __name__ == "__main__":

@@ -29,8 +29,8 @@ import torch
 from ..models.checkpoint import config_from_hf, load_checkpoint
 from ..models.config import ModelConfig, get_config
 from ..models.llama import CausalLM
-from ..parallel.comm import tp_broadcast_object
 from ..parallel.state import ParallelState, get_state
+from ..parallel.step_bus import KIND_DECODE, KIND_PICKLE, KIND_STOP, bus_slot_bytes, decode_message, make_step_bus
 from .block_manager import BlockManager
 from .runner import ModelRunner, RunnerConfig
 from .scheduler import Scheduler, SchedulerConfig
@@ -70,12 +70,15 @@ class EngineConfig:
 class _View:
     """What the runner needs of a sequence; built on non-leader TP ranks from the broadcast."""
 
-    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params", "num_computed", "chunk")
+    __slots__ = ("all_ids", "num_tokens", "block_table", "last_token", "params", "num_computed", "chunk",
+                 "chunk_ids")
 
-    def __init__(self, all_ids, num_tokens, block_table, last_token, params, num_computed=0, chunk=0):
+    def __init__(self, all_ids, num_tokens, block_table, last_token, params, num_computed=0, chunk=0,
+                 chunk_ids=None):
         self.all_ids, self.num_tokens, self.block_table = all_ids, num_tokens, block_table
         self.last_token, self.params = last_token, params
         self.num_computed, self.chunk = num_computed, chunk
+        self.chunk_ids = chunk_ids
 
 
 class LLMEngine:
@@ -117,6 +120,16 @@ class LLMEngine:
         self._inflight = None  # (seqs, DecodeHandle) of the enqueued, not yet read back decode step
         self.trace: Optional[list] = [] if os.environ.get("K8SLLM_TRACE") else None  # (t, kind, n, tokens)
         self._inflight_rows: dict = {}
+        # TP: the step bus to the workers (shared-memory ring, parallel/step_bus.py) - collective
+        self.bus = make_step_bus(self.ps, bus_slot_bytes(cfg.max_num_seqs, self.runner.max_len,
+                                                         self.runner.max_blocks_per_seq)) if self.ps.tp_size > 1 else None
+        self._publish = self.bus.send_raw if (self.bus is not None and self.is_leader) else None
+        # custom all-reduce health: its error flag is copied back after every decode launch
+        car = self.ps.custom_ar
+        self._car_flag = None
+        if car is not None and self.device.type == "cuda":
+            self._car_flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self.runner.on_launched = lambda: car.error_async(self._car_flag)
 
     # ----------------------------------------------------------------- public API
     def warmup(self) -> None:
@@ -179,10 +192,7 @@ class LLMEngine:
             return done + (self._resolve() if self._inflight is not None else [])
         prev_rows = self._inflight_rows
         src = [prev_rows.get(q.seq_id, -1) for q in seqs]
-        if self.ps.tp_size > 1:
-            tp_broadcast_object((False, [(q.last_token, q.num_tokens, q.block_table, _params_t(q.params))
-                                         for q in seqs], src), ps=self.ps)
-        handle = self.runner.decode_launch(seqs, src)
+        handle = self.runner.decode_launch(seqs, src, publish=self._publish)
         self.counters["decode_steps"] += 1
         if self.trace is not None:
             self.trace.append((time.perf_counter(), "decode", len(seqs), 0))
@@ -204,8 +214,13 @@ class LLMEngine:
         self._inflight_rows = {}
         return self._resolve_step(seqs, handle)
 
+    def _check_collectives(self) -> None:
+        if self._car_flag is not None and int(self._car_flag[0]) != 0:
+            raise RuntimeError("custom all-reduce: a TP peer did not arrive (step output invalid)")
+
     def _resolve_step(self, seqs: list, handle) -> list[Sequence]:
         toks = self.runner.decode_collect(handle)
+        self._check_collectives()
         now = time.perf_counter()
         done = []
         for q, tok in zip(seqs, toks):
@@ -242,8 +257,8 @@ class LLMEngine:
         return self._run_sync(plan)
 
     def _run_sync(self, plan) -> list[Sequence]:
-        if self.ps.tp_size > 1:
-            tp_broadcast_object(self._pack(plan), ps=self.ps)
+        if self.bus is not None and plan.is_prefill:
+            self.bus.send_obj(self._pack(plan))
         if plan.is_prefill:
             toks = self.runner.prefill(plan.seqs, plan.decode)
             self.counters["prefill_steps"] += 1
@@ -255,7 +270,8 @@ class LLMEngine:
             rows = list(plan.decode) + list(plan.seqs)
             nd = len(plan.decode)
         else:
-            toks = self.runner.decode(plan.seqs)
+            toks = self.runner.decode(plan.seqs, publish=self._publish)
+            self._check_collectives()
             self.counters["decode_steps"] += 1
             rows, nd = plan.seqs, len(plan.seqs)
         now = time.perf_counter()
@@ -329,41 +345,40 @@ class LLMEngine:
     # ----------------------------------------------------------------- tensor parallel
     @staticmethod
     def _pack(plan) -> tuple:
-        if plan.is_prefill:
-            return (True, [(s.all_ids, s.block_table, _params_t(s.params), s.num_computed, s.chunk)
-                           for s in plan.seqs],
-                    [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.decode])
-        return (False, [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.seqs])
+        """A prefill / mixed step for the TP workers: each chunk's token ids (not the whole prompt)
+        and block table, and the decode rows of a mixed step."""
+        return ([(s.all_ids[s.num_computed:s.num_computed + s.chunk], s.block_table, _params_t(s.params),
+                  s.num_computed, s.chunk) for s in plan.seqs],
+                [(s.last_token, s.num_tokens, s.block_table, _params_t(s.params)) for s in plan.decode])
 
     def worker_loop(self) -> None:
-        """Non-leader TP ranks: mirror the leader's steps until it broadcasts ``None``."""
+        """Non-leader TP ranks: mirror the leader's steps (step bus) until it sends STOP."""
         pending = None
         while True:
-            msg = tp_broadcast_object(None, ps=self.ps)
-            if msg is None:
-                return
-            is_prefill, items = msg[0], msg[1]
-            if is_prefill:
-                if pending is not None:
-                    self.runner.decode_collect(pending)
-                    pending = None
-                views = [_View(ids, len(ids), bt, ids[-1], SamplingParams(*p), nc, ch)
-                         for ids, bt, p, nc, ch in items]
-                dec = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in msg[2]]
-                self.runner.prefill(views, dec)
-            else:
-                src = msg[2] if len(msg) > 2 else None
-                views = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in items]
-                h = self.runner.decode_launch(views, src)
+            kind, payload = decode_message(self.bus.recv())
+            if kind == KIND_DECODE:
+                h = self.runner.decode_launch_raw(*payload)
                 if pending is not None:  # keep at most two steps enqueued (staging is double-buffered)
                     self.runner.decode_collect(pending)
                 pending = h
+                continue
+            if pending is not None:
+                self.runner.decode_collect(pending)
+                pending = None
+            if kind == KIND_STOP:
+                return
+            if kind == KIND_PICKLE:
+                items, dec = payload
+                views = [_View(None, nc + ch, bt, None, SamplingParams(*p), nc, ch, chunk_ids=ids)
+                         for ids, bt, p, nc, ch in items]
+                dviews = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in dec]
+                self.runner.prefill(views, dviews)
 
     def stop_workers(self) -> None:
         if self._inflight is not None:
             self._resolve()
-        if self.ps.tp_size > 1 and self.is_leader:
-            tp_broadcast_object(None, ps=self.ps)
+        if self.bus is not None and self.is_leader:
+            self.bus.send_stop()
 
 
 def _params_t(p: SamplingParams) -> tuple:

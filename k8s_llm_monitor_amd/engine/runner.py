@@ -84,6 +84,7 @@ class ModelRunner:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.n_steps = {"prefill": 0, "decode": 0}
+        self.on_launched = None  # hook after every decode launch (TP: enqueue the custom-AR error readback)
 
     # --------------------------------------------------------------------- helpers
     def bucket_for(self, n: int) -> int:
@@ -122,7 +123,8 @@ class ModelRunner:
             slots[i] = q.block_table[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
         o = nd
         for s, c, n in zip(seqs, starts, lens):
-            ids[o:o + n] = s.all_ids[c:c + n]
+            ch = getattr(s, "chunk_ids", None)  # TP worker views carry just the chunk
+            ids[o:o + n] = ch if ch is not None else s.all_ids[c:c + n]
             p = np.arange(c, c + n, dtype=np.int32)
             pos[o:o + n] = p
             bt = np.asarray(s.block_table, dtype=np.int32)
@@ -200,15 +202,17 @@ class ModelRunner:
         torch.cuda.synchronize()
         self.rng.copy_(rng_state)
 
-    def decode(self, seqs: list, src_rows: Optional[list] = None) -> list[int]:
+    def decode(self, seqs: list, src_rows: Optional[list] = None, publish=None) -> list[int]:
         """One decode step, synchronous: the sampled token per sequence."""
-        return self.decode_collect(self.decode_launch(seqs, src_rows))
+        return self.decode_collect(self.decode_launch(seqs, src_rows, publish))
 
-    def decode_launch(self, seqs: list, src_rows: Optional[list] = None) -> "DecodeHandle":
+    def decode_launch(self, seqs: list, src_rows: Optional[list] = None, publish=None) -> "DecodeHandle":
         """Enqueue one decode step without waiting for it.  ``src_rows[i] >= 0``: sequence i's input
         token is the one the previous (possibly still running) step sampled in that row; else its
         ``last_token``.  Positions come from ``num_tokens``, so a sequence carrying a not yet
-        resolved token from the in-flight step is already one position further."""
+        resolved token from the in-flight step is already one position further.  ``publish``
+        (TP leader): called with the raw step message (parallel/step_bus.py) after staging and
+        before the launch, so the workers replay the same step."""
         n = len(seqs)
         b = self.bucket_for(n) if self.graphs else n
         st = self.stage[self._stage_i]
@@ -240,6 +244,18 @@ class ModelRunner:
             topk[n:b] = 0
             topp[n:b] = 1
         n_el = _Staging.prefix(self.B, self.max_blocks_per_seq, b)  # the per-row fields + b block-table rows
+        if publish is not None:
+            publish(st.message(n, b, n_el))
+        return self._launch_staged(st, n, b, n_el)
+
+    def decode_launch_raw(self, n: int, b: int, n_el: int, words: np.ndarray) -> "DecodeHandle":
+        """TP worker: launch the decode step the leader staged (its raw staging words)."""
+        st = self.stage[self._stage_i]
+        self._stage_i ^= 1
+        st.raw[:n_el] = words
+        return self._launch_staged(st, n, b, n_el)
+
+    def _launch_staged(self, st: "_Staging", n: int, b: int, n_el: int) -> "DecodeHandle":
         self.d_all[:n_el].copy_(st.h_all[:n_el], non_blocking=True)
         g = self.graphs.get(b)
         if g is not None:
@@ -247,6 +263,8 @@ class ModelRunner:
         else:
             self._decode_body(b)
         self.n_steps["decode"] += 1
+        if self.on_launched is not None:
+            self.on_launched()
         if not self.is_gpu:
             return DecodeHandle(n, None, self.d_out[:n].tolist())
         h = self.h_out[self._out_i]
@@ -299,9 +317,23 @@ class _Staging:
         return (*f, bt)
 
     def __init__(self, B: int, max_blocks: int, pin: bool):
-        self.h_all = torch.zeros(self.size(B, max_blocks), dtype=torch.int32, pin_memory=pin)
+        from ..parallel.step_bus import DECODE_HDR, KIND_DECODE
+
+        # DECODE_HDR leading words hold the step-bus header, so a TP leader publishes
+        # full[:DECODE_HDR + n_el] without a copy (parallel/step_bus.py)
+        self.h_full = torch.zeros(DECODE_HDR + self.size(B, max_blocks), dtype=torch.int32, pin_memory=pin)
+        self.h_all = self.h_full[DECODE_HDR:]
+        self.full = self.h_full.numpy()
+        self.full[0] = KIND_DECODE
+        self.raw = self.full[DECODE_HDR:]
         (self.n_ids, self.n_src, self.n_pos, self.n_slots, self.n_lens, self.n_topk, self.n_temp, self.n_topp,
-         self.n_bt) = self.views(self.h_all.numpy(), B, max_blocks)
+         self.n_bt) = self.views(self.raw, B, max_blocks)
+
+    def message(self, n: int, b: int, n_el: int) -> np.ndarray:
+        from ..parallel.step_bus import DECODE_HDR
+
+        self.full[1:4] = (n, b, n_el)
+        return self.full[:DECODE_HDR + n_el]
 
 
 @dataclass

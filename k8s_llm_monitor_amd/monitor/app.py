@@ -183,14 +183,24 @@ def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0, 
 
 
 def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0.0.1",
-                 concurrency: Optional[int] = None) -> list:
+                 concurrency: Optional[int] = None, offsets_s: Optional[list] = None,
+                 allow_errors: bool = False) -> list:
     """Fire ``items`` = [(question, context_text)] as concurrent POST /api/v1/query; returns the
-    per-request result dicts (answer, timings)."""
+    per-request result dicts (answer, timings, ``http_latency_ms``).  ``offsets_s``: open-loop
+    arrivals - request i is sent ``offsets_s[i]`` seconds after the call starts (``t_send_s``
+    records when it went out).  ``allow_errors``: a non-200 answer becomes
+    ``{"http_status": code, "error": ...}`` instead of raising (overload / admission studies)."""
     import concurrent.futures as cf
     import http.client
 
-    def one(item):
-        q, ctx = item
+    t_start = time.perf_counter()
+
+    def one(i):
+        q, ctx = items[i]
+        if offsets_s is not None:
+            delay = t_start + offsets_s[i] - time.perf_counter()
+            if delay > 0:
+                time.sleep(delay)
         body = json.dumps({"question": q, "max_tokens": max_new_tokens, "ignore_eos": True,
                            "context": {"cluster_state": ctx}}).encode()
         conn = http.client.HTTPConnection(host, port, timeout=900)
@@ -199,14 +209,20 @@ def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0
         r = conn.getresponse()
         data = json.loads(r.read())
         conn.close()
+        lat = (time.perf_counter() - t0) * 1e3
         if r.status != 200 or data.get("status") != "success":
+            if allow_errors:
+                return {"http_status": r.status, "error": data.get("error"), "http_latency_ms": lat,
+                        "t_send_s": t0 - t_start}
             raise RuntimeError(f"query failed: HTTP {r.status}: {data}")
         res = data["result"]
-        res["http_latency_ms"] = (time.perf_counter() - t0) * 1e3
+        res["http_status"] = r.status
+        res["http_latency_ms"] = lat
+        res["t_send_s"] = t0 - t_start
         return res
 
     with cf.ThreadPoolExecutor(max_workers=concurrency or len(items)) as ex:
-        return list(ex.map(one, items))
+        return list(ex.map(one, range(len(items))))
 
 
 def post_pod_communication(port: int, pairs: list, max_new_tokens: int, host: str = "127.0.0.1") -> list:

@@ -8,7 +8,8 @@ the GPU (this module imports no torch and never initialises a device).
 
 Protocol: one JSON request per stdin line, one JSON reply per stdout line.
 
-    {"op": "query", "port": P, "items": [[question, context], ...], "max_new_tokens": N}
+    {"op": "query", "port": P, "items": [[question, context], ...], "max_new_tokens": N,
+     "offsets_s": [...] (optional, open-loop arrival times), "allow_errors": bool (optional)}
     {"op": "podcomm", "port": P, "pairs": [[pod_a, pod_b], ...], "max_new_tokens": N}
     -> {"ok": true, "results": [...]}   (post_queries / post_pod_communication result dicts)
     -> {"ok": false, "error": "..."}
@@ -32,7 +33,8 @@ def serve(stdin=None, stdout=None) -> None:
         try:
             req = json.loads(line)
             if req["op"] == "query":
-                res = post_queries(req["port"], [tuple(x) for x in req["items"]], req["max_new_tokens"])
+                res = post_queries(req["port"], [tuple(x) for x in req["items"]], req["max_new_tokens"],
+                                   offsets_s=req.get("offsets_s"), allow_errors=bool(req.get("allow_errors")))
             elif req["op"] == "podcomm":
                 res = post_pod_communication(req["port"], [tuple(x) for x in req["pairs"]], req["max_new_tokens"])
             else:
@@ -64,9 +66,10 @@ class LoadGen:
             raise RuntimeError(f"load generator: {rep['error']}")
         return rep["results"]
 
-    def post_queries(self, port: int, items: list, max_new_tokens: int) -> list:
+    def post_queries(self, port: int, items: list, max_new_tokens: int, offsets_s: list | None = None,
+                     allow_errors: bool = False) -> list:
         return self._call({"op": "query", "port": port, "items": [list(x) for x in items],
-                           "max_new_tokens": max_new_tokens})
+                           "max_new_tokens": max_new_tokens, "offsets_s": offsets_s, "allow_errors": allow_errors})
 
     def post_pod_communication(self, port: int, pairs: list, max_new_tokens: int) -> list:
         return self._call({"op": "podcomm", "port": port, "pairs": [list(x) for x in pairs],

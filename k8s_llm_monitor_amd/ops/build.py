@@ -126,7 +126,7 @@ def build_runtime(force: bool = False) -> Path:
     tmp = RT_SO.with_suffix(".tmp.so")
     _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-          *map(str, srcs), "-o", str(tmp)])
+          f"-I{RT_SRC}", *map(str, srcs), "-o", str(tmp), "-lrt"])
     os.replace(tmp, RT_SO)
     return RT_SO
 

@@ -60,6 +60,8 @@ int k8sllm_car_handle_size();
 int k8sllm_car_open(void* state, const void* all_handles);
 int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
 int k8sllm_car_error(void* state);
+int k8sllm_car_all_gather(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
+int k8sllm_car_error_async(void* state, void* host_dst, hipStream_t s);
 void k8sllm_car_destroy(void* state);
 }
 
@@ -651,7 +653,21 @@ void car_all_reduce(int64_t state, torch::Tensor in, torch::Tensor out, int64_t 
         "car_all_reduce");
 }
 
+void car_all_gather(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit) {
+  dev_bf16(in, "in"); dev_bf16(out, "out");
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && out.numel() % in.numel() == 0 &&
+                  out.data_ptr() != in.data_ptr(), "car_all_gather layout");
+  check(k8sllm_car_all_gather((void*)(intptr_t)state, in.data_ptr(), out.data_ptr(), (long)in.numel(),
+                              (long)spin_limit, cur()),
+        "car_all_gather");
+}
+
 int64_t car_error(int64_t state) { return k8sllm_car_error((void*)(intptr_t)state); }
+
+void car_error_async(int64_t state, torch::Tensor host) {
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == torch::kInt32 && host.numel() >= 1, "host int32 flag");
+  check(k8sllm_car_error_async((void*)(intptr_t)state, host.data_ptr(), cur()), "car_error_async");
+}
 
 void car_destroy(int64_t state) { k8sllm_car_destroy((void*)(intptr_t)state); }
 
@@ -684,5 +700,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("car_open", &car_open);
   m.def("car_all_reduce", &car_all_reduce);
   m.def("car_error", &car_error);
+  m.def("car_all_gather", &car_all_gather);
+  m.def("car_error_async", &car_error_async);
   m.def("car_destroy", &car_destroy);
 }

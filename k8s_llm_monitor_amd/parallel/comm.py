@@ -40,11 +40,15 @@ def tp_all_gather_last(x: torch.Tensor, ps=None) -> torch.Tensor:
     if st.tp_size == 1:
         return x
     x = x.contiguous()
-    out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    if _rccl(st, x):
-        dist.all_gather_into_tensor(out, x, group=st.tp_group)
-    else:  # gloo has no all_gather_into_tensor
-        dist.all_gather(list(out.unbind(0)), x, group=st.tp_group)
+    car = st.custom_ar
+    if car is not None and car.fits_gather(x):  # one-shot IPC gather (decode logits)
+        out = car.all_gather(x)
+    else:
+        out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        if _rccl(st, x):
+            dist.all_gather_into_tensor(out, x, group=st.tp_group)
+        else:  # gloo has no all_gather_into_tensor
+            dist.all_gather(list(out.unbind(0)), x, group=st.tp_group)
     return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
 
 

@@ -7,9 +7,13 @@ every peer and sums all ranks' slices in rank order - one xGMI hop reading all p
 instead of a ring's 2(W-1) latency-bound hops over one link.  Messages larger than the staging
 buffer (prefill activations) keep RCCL (``parallel/comm.tp_all_reduce`` picks per call).
 
-Enabled with ``K8SLLM_CUSTOM_AR=1`` (``init_parallel(custom_ar=True)``): validated on one MI355X
-with two processes sharing the GPU (tests/test_custom_ar.py); RCCL stays the default until an
-8-GPU node has exercised it.
+The same protocol provides a one-shot all-gather (the vocab-parallel logits, C-4), so a TP decode
+step captured in a hipGraph contains no RCCL call at all.
+
+On by default at TP 2..8 on the GPU (``K8SLLM_CUSTOM_AR=0`` keeps RCCL for everything): validated
+on one MI355X with two processes sharing the GPU (tests/test_custom_ar.py, tests/test_tp_gpu.py).
+A call whose peer never arrives sets the error flag instead of hanging; the engine enqueues a copy
+of the flag after every decode step (``error_async``) and fails the step if it was set.
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-DEFAULT_MAX_BYTES = 8 << 20  # >= 64 rows x 8192 x bf16 (Llama-3-70B decode at TP=8) with headroom
+DEFAULT_MAX_BYTES = 16 << 20  # >= 64 rows x 64128 bf16 (TP=2 logits shard) and 64 x 8192 activations
 DEFAULT_SPIN_LIMIT = 4_000_000  # polls before a missing peer is declared failed (seconds, not forever)
 
 
@@ -45,6 +49,19 @@ class CustomAllReduce:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
                 and 0 < x.numel() <= self.max_elems)
 
+    def fits_gather(self, x: torch.Tensor) -> bool:
+        return self.fits(x)
+
+    def all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """[world, *x.shape]: every rank's x in rank order (x must satisfy ``fits_gather``)."""
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        self._n.car_all_gather(self.state, x, out, self.spin_limit)
+        return out
+
+    def error_async(self, host_flag: torch.Tensor) -> None:
+        """Enqueue a copy of the error flag into ``host_flag`` (pinned int32) on the current stream."""
+        self._n.car_error_async(self.state, host_flag)
+
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         """In-place sum over the group (x must satisfy ``fits``)."""
         self._n.car_all_reduce(self.state, x, x, self.spin_limit)
@@ -66,11 +83,11 @@ class CustomAllReduce:
 
 
 def enabled() -> bool:
-    return os.environ.get("K8SLLM_CUSTOM_AR", "0") == "1"
+    return os.environ.get("K8SLLM_CUSTOM_AR", "1") != "0"
 
 
 def maybe_create(ps) -> Optional[CustomAllReduce]:
-    """Collective over the TP group: a CustomAllReduce when enabled, on GPU, TP 2..8."""
+    """Collective over the TP group: a CustomAllReduce on the GPU at TP 2..8 (unless disabled)."""
     if not (enabled() and ps.tp_size > 1 and ps.tp_size <= 8 and ps.device.type == "cuda"):
         return None
     return CustomAllReduce(ps.tp_rank, ps.tp_size, cpu_group=ps.cpu_group)

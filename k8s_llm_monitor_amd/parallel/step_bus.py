@@ -1,0 +1,150 @@
+"""Step bus: how the tensor-parallel leader hands each engine step to its TP workers (SURVEY.md
+§2.12 C-6).
+
+The leader owns the scheduler; every TP rank runs the identical forward.  Per step the workers need
+the step's inputs:
+
+* decode  - the leader's pinned staging buffer (ids, src rows, positions, slots, lengths, sampling
+            parameters, block-table rows: ``engine/runner._Staging``) sent RAW - no pickling, and
+            the worker copies it straight into its own staging and replays the same hipGraph;
+* prefill / mixed / stop - a pickled plan (prefill steps are tens to hundreds of ms; pickling is
+            noise there).
+
+Transport: ``ShmStepBus`` - the native shared-memory ring (``runtime/csrc/step_channel.cpp``,
+all TP ranks of a group live on one node) - by default; ``GlooStepBus`` - ``broadcast_object_list``
+over the CPU gloo group - when the native runtime is missing or ``K8SLLM_STEP_BUS=gloo``.
+Message framing: int32 kind, then the payload (decode: int32 [n, b, n_el] + n_el staging words).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import struct
+import uuid
+
+import numpy as np
+import torch.distributed as dist
+
+KIND_DECODE = 1
+KIND_PICKLE = 2
+KIND_STOP = 3
+
+DECODE_HDR = 4  # int32 words in front of a raw decode message: kind, n, b, n_el
+
+
+class GlooStepBus:
+    def __init__(self, ps):
+        self.ps = ps
+        self.src = ps.rank - ps.tp_rank
+
+    def _bcast(self, obj):
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=self.src, group=self.ps.cpu_group)
+        return lst[0]
+
+    def send_raw(self, words: np.ndarray) -> None:
+        self._bcast(words.tobytes())
+
+    def send_obj(self, obj) -> None:
+        self._bcast(struct.pack("<i", KIND_PICKLE) + pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL))
+
+    def send_stop(self) -> None:
+        self._bcast(struct.pack("<i", KIND_STOP))
+
+    def recv(self) -> bytes:
+        return self._bcast(None)
+
+    def close(self) -> None:
+        pass
+
+
+class ShmStepBus:
+    """Leader publishes into a native shared-memory ring; worker ``tp_rank - 1`` is reader index
+    ``tp_rank - 1``.  Collective over the TP group's CPU group (name exchange + barrier)."""
+
+    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 600.0):
+        from ..runtime import native_runtime
+
+        rt = native_runtime()
+        if rt is None or not hasattr(rt, "StepChannel"):
+            raise RuntimeError("native StepChannel unavailable")
+        self.ps = ps
+        self.timeout_s = timeout_s
+        src = ps.rank - ps.tp_rank
+        name = [f"/k8sllm_step_{os.getpid()}_{uuid.uuid4().hex[:12]}" if ps.tp_rank == 0 else None]
+        ok = [True]
+        if ps.tp_rank == 0:
+            try:
+                self.ch = rt.StepChannel(name[0], True, nslots, int(slot_bytes), ps.tp_size - 1)
+            except Exception:  # noqa: BLE001 - no /dev/shm: tell the workers to fall back
+                ok[0] = False
+        dist.broadcast_object_list(name, src=src, group=ps.cpu_group)
+        if ps.tp_rank != 0 and ok[0]:
+            try:
+                self.ch = rt.StepChannel(name[0], False)
+            except Exception:  # noqa: BLE001
+                ok[0] = False
+        oks: list = [None] * ps.tp_size  # every rank learns whether every rank has the channel
+        dist.all_gather_object(oks, ok[0], group=ps.cpu_group)
+        if ps.tp_rank == 0 and ok[0]:
+            self.ch.unlink()  # every rank that could map it has: the name is no longer needed
+        if not all(oks):
+            if ok[0]:
+                self.ch.close()
+            raise RuntimeError("shared-memory step channel unavailable on some TP rank")
+        self.reader = ps.tp_rank - 1
+
+    def _publish(self, data) -> None:
+        if not self.ch.publish(data, self.timeout_s):
+            raise TimeoutError("TP worker did not consume the previous step within the step-bus timeout")
+
+    def send_raw(self, words: np.ndarray) -> None:
+        self._publish(words)
+
+    def send_obj(self, obj) -> None:
+        self._publish(struct.pack("<i", KIND_PICKLE) + pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL))
+
+    def send_stop(self) -> None:
+        self._publish(struct.pack("<i", KIND_STOP))
+
+    def recv(self) -> bytes:
+        m = self.ch.recv(self.reader, self.timeout_s)
+        if m is None:
+            raise TimeoutError("no step from the TP leader within the step-bus timeout")
+        return m
+
+    def close(self) -> None:
+        self.ch.close()
+
+
+def make_step_bus(ps, slot_bytes: int):
+    """Collective over the TP group.  None at TP 1."""
+    if ps.tp_size == 1:
+        return None
+    if os.environ.get("K8SLLM_STEP_BUS", "shm") != "gloo":
+        try:
+            return ShmStepBus(ps, slot_bytes)
+        except Exception:  # noqa: BLE001 - every rank takes the same branch (the failure is broadcast)
+            pass
+    return GlooStepBus(ps)
+
+
+def decode_message(buf: bytes) -> tuple:
+    """(kind, payload): KIND_DECODE -> (n, b, n_el, int32 staging words); KIND_PICKLE -> object."""
+    kind = struct.unpack_from("<i", buf, 0)[0]
+    if kind == KIND_DECODE:
+        w = np.frombuffer(buf, dtype=np.int32)
+        n, b, n_el = int(w[1]), int(w[2]), int(w[3])
+        return kind, (n, b, n_el, w[DECODE_HDR:DECODE_HDR + n_el])
+    if kind == KIND_PICKLE:
+        return kind, pickle.loads(buf[4:])
+    return kind, None
+
+
+def bus_slot_bytes(max_num_seqs: int, max_model_len: int, max_blocks: int) -> int:
+    """Enough for the largest message: a raw decode step or a pickled prefill plan (chunk ids +
+    block tables of every sequence)."""
+    raw = 4 * (DECODE_HDR + 8 * max_num_seqs + max_num_seqs * max_blocks)
+    pickled = max_num_seqs * (max_model_len * 6 + max_blocks * 6 + 256) + (1 << 16)
+    return int(max(1 << 20, raw, pickled))
+

@@ -7,6 +7,8 @@
 //                     tokens encode in microseconds, keeping /api/v1/query admission off the GIL.
 //  * pack_decode    - builds the decode-step staging arrays (ids, positions, slot mapping, lengths,
 //                     block-table rows) for a batch in one call.
+//  * StepChannel    - (step_channel.cpp) shared-memory ring carrying each step's inputs from the
+//                     tensor-parallel leader to its workers.
 //
 // The reference has no native code; this replaces its Go process runtime pieces
 // that matter for serving latency.
@@ -22,6 +24,8 @@
 #include <unordered_map>
 #include <vector>
 #include <list>
+
+#include "runtime.h"
 
 namespace py = pybind11;
 
@@ -447,4 +451,5 @@ PYBIND11_MODULE(_k8sllm_runtime, m) {
       .def_property_readonly("num_blocks", &BlockPool::num_blocks)
       .def_property_readonly("num_cached", &BlockPool::num_cached);
   m.def("block_hashes", &block_hashes, py::arg("tokens"), py::arg("block_size") = 16, py::arg("seed") = 0);
+  register_step_channel(m);
 }

@@ -83,3 +83,42 @@ def test_bench_two_ranks_under_torchrun_cpu():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 8
     assert d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0 and d["scaling"] == "weak"
     assert d["config"]["path"] == "http" and d["config"]["client"] == "process"
+
+
+def _bench(args):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", *args], capture_output=True, text=True, timeout=400, cwd=root,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_bench_self_launches_ranks_cpu(tp):
+    """``python bench.py --gpus 2`` with no torchrun: the parent spawns the 2 ranks itself (DP
+    replicas, or one TP=2 replica whose worker mirrors the leader over the shared-memory step bus)."""
+    d = _bench(["--gpus", "2", "--tp", str(tp), "--steps", "1", "--warmup", "1", "--model", "llama-tiny",
+                "--batch", "3", "--max-new-tokens", "3"])
+    assert d["n_gpus"] == 2 and d["dist"]["world_size"] == 2 and d["dist"]["tp"] == tp
+    assert d["config"]["parallelism"] == ("dp2" if tp == 1 else "tp2")
+    assert d["config"]["global_batch"] == (6 if tp == 1 else 3)
+    assert d["value"] > 0 and "TP=%d" % tp in d["metric"]
+    if tp == 2:
+        assert d["dist"]["step_bus"] == "ShmStepBus"
+
+
+def test_bench_open_loop_and_latency_modes_cpu():
+    d = _bench(["--steps", "1", "--warmup", "0", "--model", "llama-tiny", "--mode", "poisson", "--rate", "50",
+                "--batch", "4", "--max-new-tokens", "4", "--production"])
+    assert d["config"]["mode"] == "poisson" and d["requests"]["ok_rank0"] == 4
+    assert d["ttft_ms"]["p50"] is not None and d["config"]["server_timeouts"].startswith("production")
+    d = _bench(["--steps", "2", "--warmup", "0", "--model", "llama-tiny", "--mode", "latency",
+                "--max-new-tokens", "3"])
+    assert d["config"]["global_batch"] == 1 and d["steps"] == 2 and d["p50_latency_ms"] > 0

@@ -32,13 +32,15 @@ def test_tp_all_reduce_routes_small_messages_to_custom_ar():
     assert comm.tp_all_reduce(x, ps) is x and torch.equal(x, torch.full((8,), 2.0)) and car.calls == 1
 
 
-def test_custom_ar_is_opt_in(monkeypatch):
+def test_custom_ar_gate(monkeypatch):
     from k8s_llm_monitor_amd.parallel import custom_ar
 
-    monkeypatch.delenv("K8SLLM_CUSTOM_AR", raising=False)
+    monkeypatch.setenv("K8SLLM_CUSTOM_AR", "0")
     assert custom_ar.maybe_create(ParallelState(tp_size=2, device=torch.device("cuda", 0))) is None
-    monkeypatch.setenv("K8SLLM_CUSTOM_AR", "1")
+    monkeypatch.delenv("K8SLLM_CUSTOM_AR", raising=False)
+    assert custom_ar.enabled()  # default on
     assert custom_ar.maybe_create(ParallelState(tp_size=2)) is None  # CPU: RCCL/gloo only
+    assert custom_ar.maybe_create(ParallelState(tp_size=1, device=torch.device("cuda", 0))) is None
 
 
 def _free_port() -> int:
@@ -77,6 +79,22 @@ def _rank_main(rank: int, world: int, port: int, q) -> None:
             car.all_reduce_(x)
             if not torch.equal(x.cpu(), ref):
                 bad.append(("in-place", n))
+        # consecutive calls of different sizes (decode buckets, prefill chunks): ADVICE r1 - the
+        # buffer half is per call, so a slow peer never reads a slice overwritten by a smaller call
+        for it, n in enumerate([64 * 4096, 8, 4096, 64 * 4096, 16, 200 * 8, 64 * 4096, 8] * 3):
+            xc = torch.randn(n, generator=g).bfloat16()
+            out = car.all_reduce(xc.cuda())
+            if not torch.equal(out.cpu(), ref_sum(xc)):
+                bad.append(("alternating", it, n))
+        # one-shot all-gather (vocab-parallel logits), interleaved with all-reduces
+        for n in (8, 64 * 1000, 64 * 16032):
+            xc = torch.randn(n, generator=g).bfloat16()
+            got = car.all_gather(xc.cuda()).cpu()
+            parts = [torch.empty_like(xc) for _ in range(world)]
+            dist.all_gather(parts, xc)
+            if not torch.equal(got, torch.stack(parts)):
+                bad.append(("gather", n))
+            car.all_reduce(xc[:8].cuda())
         # hipGraph: three captured calls per replay, fresh inputs every replay
         n = 64 * 4096
         sin = torch.empty(n, dtype=torch.bfloat16, device="cuda")

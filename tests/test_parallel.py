@@ -18,9 +18,21 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, model, q):
+def _drive(eng, SamplingParams):
+    """Two prompts, then a third arriving while they decode (mixed prefill+decode steps)."""
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    seqs = [eng.add_request(p, sp) for p in ("node NotReady", "pod crashloop")]
+    for _ in range(2):
+        eng.step()
+    seqs.append(eng.add_request("why is coredns failing " * 3, sp))
+    while eng.has_work():
+        eng.step()
+    return [s.output_ids for s in seqs], eng.counters["mixed_steps"]
+
+
+def _worker(rank, world, port, model, q, bus="shm"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), K8SLLM_STEP_BUS=bus)
     torch.set_num_threads(2)
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
@@ -43,17 +55,17 @@ def _worker(rank, world, port, model, q):
         ecfg = EngineConfig(model=model, max_num_seqs=4, max_model_len=128, num_blocks=64, use_graphs=False, seed=5,
                             dtype="float32")  # fp32: TP vs TP=1 rounding must not flip greedy ties
         eng = LLMEngine(ecfg, device="cpu", pstate=ps)
+        assert type(eng.bus).__name__ == ("ShmStepBus" if bus == "shm" else "GlooStepBus")
         toks = None
         if ps.tp_rank == 0:
-            seqs = eng.generate(["node NotReady", "pod crashloop"], SamplingParams(max_tokens=5, temperature=0.0,
-                                                                                  ignore_eos=True))
-            toks = [s.output_ids for s in seqs]
+            toks, mixed = _drive(eng, SamplingParams)
+            assert mixed > 0
             eng.stop_workers()
         else:
             eng.worker_loop()
+        eng.bus.close()
         single = LLMEngine(ecfg, device="cpu", pstate=ParallelState())
-        ref = [s.output_ids for s in single.generate(["node NotReady", "pod crashloop"],
-                                                       SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True))]
+        ref, _ = _drive(single, SamplingParams)
         q.put((rank, err, a.shape[-1], toks, ref))
         destroy()
     except Exception as e:  # noqa: BLE001
@@ -62,14 +74,15 @@ def _worker(rank, world, port, model, q):
         q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("model,world", [("llama-tiny", 2), ("mixtral-tiny", 2), ("gpt2-tiny", 2),
-                                         # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
-                                         ("llama-tiny", 4), ("mixtral-tiny", 4)])
-def test_tp_matches_tp1(model, world):
+@pytest.mark.parametrize("model,world,bus", [("llama-tiny", 2, "shm"), ("mixtral-tiny", 2, "shm"),
+                                             ("gpt2-tiny", 2, "shm"), ("llama-tiny", 2, "gloo"),
+                                             # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
+                                             ("llama-tiny", 4, "shm"), ("mixtral-tiny", 4, "shm")])
+def test_tp_matches_tp1(model, world, bus):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, bus)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
