@@ -46,7 +46,7 @@ class EngineConfig:
     max_prefill_tokens: int = 16384
     chunked_prefill: bool = True  # prompts beyond a step's token budget prefill in chunks (scheduler.py)
     # prefill budget of a mixed prefill+decode step (scheduler.py); 0 = prefill steps stall decodes
-    mixed_prefill_tokens: int = 8192
+    mixed_prefill_tokens: int = 16384
     kv_cache_gb: float = 32.0
     num_blocks: Optional[int] = None
     use_graphs: bool = True

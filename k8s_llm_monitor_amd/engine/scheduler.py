@@ -37,7 +37,7 @@ class SchedulerConfig:
     # step's activation memory and on how long running decodes wait behind a long prompt
     chunked_prefill: bool = True
     # mixed prefill+decode steps (see the module docstring); 0 = prefill steps stall decodes
-    mixed_prefill_tokens: int = 8192
+    mixed_prefill_tokens: int = 16384
 
 
 @dataclass
