@@ -12,6 +12,7 @@
 #include <fcntl.h>
 #include <pybind11/pybind11.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -79,6 +80,7 @@ class StepChannel {
     }
     base_ = (uint8_t*)p;
     hdr_ = reinterpret_cast<ChanHeader*>(base_);
+    prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // idle back-off sleeps wake within microseconds
     if (create) {
       new (hdr_) ChanHeader();
       hdr_->nslots = (uint64_t)nslots;
@@ -163,22 +165,25 @@ class StepChannel {
         timeout_s);
   }
 
-  // Spin briefly (decode steps arrive every few ms), then back off to short sleeps so an idle
-  // worker does not hold a core; bounded by timeout_s (< 0: forever).
+  // Busy-poll for up to kSpinS (decode steps arrive every few ms: a sleeping reader would pay the
+  // scheduler's wake-up latency, ~60 us with the default 50 us timer slack, on every step), then
+  // back off to 20 us sleeps (timer slack lowered to 1 us) so an idle worker does not hold a core;
+  // bounded by timeout_s (< 0: forever).
+  static constexpr double kSpinS = 0.05;
   template <class F>
   static bool spin_until(F ready, double timeout_s) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     for (long i = 0;; ++i) {
       if (ready()) return true;
-      if (i < 20000) {
+      if ((i & 255) != 0) {
         cpu_relax();
         continue;
       }
-      if ((i & 63) == 0 && timeout_s >= 0 &&
-          std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
-        return false;
-      std::this_thread::sleep_for(std::chrono::microseconds(i < 200000 ? 5 : 200));
+      const double el = std::chrono::duration<double>(clk::now() - t0).count();
+      if (timeout_s >= 0 && el > timeout_s) return false;
+      if (el < kSpinS) continue;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
 

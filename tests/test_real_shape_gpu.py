@@ -1,0 +1,85 @@
+"""Real-shape GPU parity (VERDICT r1 'do this' #9): the full engine path - paged prefill, the skinny
+MFMA decode GEMMs over fragment-packed weights inside hipGraphs, HIP attention / RoPE / norms and
+the sampler - at Llama-3-8B dimensions (d 4096, 32/8 heads, ff 14336, vocab 128256, theta 5e5; two
+layers) and at Llama-3-70B dimensions (d 8192, 64/8 heads, ff 28672; one layer), against an fp32
+CPU reference model holding the SAME weights (copied from the GPU model).
+
+Checks: (1) prefill logits of the bf16 GPU forward vs the fp32 reference: max-abs error bounded
+relative to the logit scale; (2) 16 greedy decode steps through the engine: every generated token
+is the fp32 reference's argmax on the teacher-forced sequence, or a provable near-tie (its logit
+within twice the measured bf16 logit error of the max)."""
+import pytest
+import torch
+
+
+def _fp32_reference(gpu_model):
+    from k8s_llm_monitor_amd.models import CausalLM
+    from k8s_llm_monitor_amd.parallel.state import ParallelState
+
+    import os
+
+    old = os.environ.get("K8SLLM_SKINNY")
+    os.environ["K8SLLM_SKINNY"] = "0"  # the reference runs the plain row-major path only
+    try:
+        ref = CausalLM(gpu_model.cfg, device="cpu", dtype=torch.float32, pstate=ParallelState(), init="empty")
+    finally:
+        if old is None:
+            os.environ.pop("K8SLLM_SKINNY", None)
+        else:
+            os.environ["K8SLLM_SKINNY"] = old
+    ref.embed.copy_(gpu_model.embed.float().cpu())
+    if ref.lm_head is not ref.embed:
+        ref.lm_head.copy_(gpu_model.lm_head.float().cpu())
+    ref.final_norm.copy_(gpu_model.final_norm.float().cpu())
+    for Lr, Lg in zip(ref.layers, gpu_model.layers):
+        for k, v in Lr.items():
+            if not k.endswith("_p") and not k.endswith("_pg"):
+                v.copy_(Lg[k].float().cpu())
+    return ref
+
+
+def _logits(model, ids, rows, device):
+    from k8s_llm_monitor_amd.models import AttnMeta
+
+    n = len(ids)
+    t = torch.tensor(ids, dtype=torch.int32, device=device)
+    meta = AttnMeta(is_prefill=True, positions=torch.arange(n, dtype=torch.int32, device=device),
+                    slot_mapping=torch.full((n,), -1, dtype=torch.int32, device=device),
+                    cu_seqlens=torch.tensor([0, n], dtype=torch.int32, device=device),
+                    logits_idx=torch.tensor(rows, device=device))
+    return model.forward(t, meta, None).float().cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,layers", [("llama-3-8b", 2), ("llama-3-70b", 1)])
+def test_gpu_real_shape_engine_matches_fp32_reference(model, layers):
+    from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+
+    torch.set_num_threads(16)
+    eng = LLMEngine(EngineConfig(model=model, model_overrides={"n_layers": layers}, max_num_seqs=8,
+                                 max_model_len=2048, kv_cache_gb=1.0, seed=21), device="cuda")
+    eng.warmup()
+    assert eng.runner.graphs and "wqkv_p" in eng.model.layers[0], "skinny decode path not active"
+    prompts = ["集群状态概览: node-001 CPU=93.1% [资源压力] MEM=88% 为什么我的pod频繁重启？ " * 3,
+               "Why is pod default/api-gateway not ready? kube-system coredns CrashLoopBackOff " * 2,
+               "node-007 NotReady, payments-api OOMKilled x12"]
+    n_new = 16
+    seqs = eng.generate(prompts, SamplingParams(max_tokens=n_new, temperature=0.0, ignore_eos=True))
+    ref = _fp32_reference(eng.model)
+    for s in seqs:
+        assert len(s.output_ids) == n_new
+        ids = s.prompt_ids + s.output_ids
+        p = len(s.prompt_ids)
+        rows = list(range(p - 1, p - 1 + n_new))
+        lr = _logits(ref, ids, rows, "cpu")  # [16, V] fp32 reference, teacher-forced
+        lg = _logits(eng.model, ids, rows, "cuda")  # the bf16 GPU prefill path on the same rows
+        scale = float(lr.abs().max())
+        err = float((lg - lr).abs().max())
+        assert err < 0.03 * scale, f"{model}: prefill logits max-abs err {err:.4f} vs scale {scale:.3f}"
+        for t in range(n_new):
+            top = float(lr[t].max())
+            got = float(lr[t, s.output_ids[t]])
+            assert top - got <= 2 * err + 1e-6, (
+                f"{model} step {t}: token {s.output_ids[t]} logit {got:.4f} vs max {top:.4f} (bf16 err {err:.4f})")
+    del eng
+    torch.cuda.empty_cache()

@@ -117,8 +117,10 @@ class Smoke:
                    "timestamp": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
                    "state": {"uav_id": "UAV-smoke-node", "node_name": "smoke-node",
                              "battery": {"remaining_percent": 77.0, "voltage": 15.8},
-                             "gps": {"latitude": 39.9, "longitude": 116.4, "altitude": 50.0, "satellites": 12,
-                                     "fix_type": 3}},
+                             "gps": {"latitude": 39.9, "longitude": 116.4, "altitude": 50.0, "satellite_count": 12,
+                                     "fix_type": 3},
+                             "flight": {"mode": "LOITER", "armed": True},
+                             "health": {"system_status": "OK"}},
                    "heartbeat_interval_seconds": 10}
             c, j, _ = self.req("POST", "/api/v1/uav/report", rep)
             return None if c == 200 else f"{c} {j}"
@@ -136,12 +138,69 @@ class Smoke:
             c, j, _ = self.req("GET", "/api/v1/crd/uav")
             return None if c in (200, 503) else f"{c} {j}"
 
+        def states() -> dict:
+            c, j, _ = self.req("GET", "/api/v1/metrics/uav")
+            data = (j or {}).get("data") or {}
+            return {k: (v.get("state") or v) if isinstance(v, dict) else {} for k, v in data.items()}
+
+        def single_from_list():  # reference test_get_single_uav: the first listed node
+            st = states()
+            if not st:
+                return "no UAV listed"
+            node = sorted(st)[0]
+            c, j, _ = self.req("GET", f"/api/v1/metrics/uav/{node}")
+            return None if c == 200 and (j or {}).get("status") == "success" else f"{node}: {c} {j}"
+
+        def integrity():  # reference test_data_integrity: the five fields of the first entry
+            st = states()
+            if not st:
+                return "no UAV listed"
+            first = st[sorted(st)[0]]
+            missing = [f for f in ("uav_id", "gps", "battery", "flight", "health") if first.get(f) is None]
+            return f"missing fields {missing}" if missing else None
+
+        def monitor(label, pred, fmt):
+            """Reference low-battery / GPS / health monitors: list the offenders (a warning, as in
+            the reference, not a failure)."""
+            def run():
+                bad = [fmt(k, v) for k, v in sorted(states().items()) if pred(v)]
+                print(f"    {label}: " + ("none" if not bad else "; ".join(bad)))
+                return None
+            return run
+
+        def latency():  # reference test_performance: average of 10 GETs, < 1000 ms good, > 3 s slow
+            ts = []
+            for _ in range(10):
+                t0 = time.perf_counter()
+                self.req("GET", "/api/v1/metrics/uav")
+                ts.append((time.perf_counter() - t0) * 1e3)
+            avg = sum(ts) / len(ts)
+            grade = "good (<1s)" if avg < 1000 else ("fair (1-3s)" if avg < 3000 else "slow (>3s)")
+            print(f"    average response {avg:.1f} ms: {grade}")
+            return None if avg < 3000 else f"average {avg:.0f} ms"
+
         self.check("UAV metrics list", uav_list)
         if push:
             self.check("UAV report push", uav_push)
             self.check("UAV metrics by node", uav_node)
             self.check("UAV battery + GPS present", battery_gps)
+        self.check("UAV single lookup (first listed node)", single_from_list)
+        self.check("UAV data integrity (uav_id/gps/battery/flight/health)", integrity)
+        self.check("low battery monitor (<20%)", monitor(
+            "low battery", lambda v: float((v.get("battery") or {}).get("remaining_percent", 100)) < 20,
+            lambda k, v: f"{k}: {v['battery']['remaining_percent']}%"))
+        self.check("GPS monitor (<10 satellites)", monitor(
+            "weak GPS", lambda v: int((v.get("gps") or {}).get("satellite_count", 99)) < 10,
+            lambda k, v: f"{k}: {v['gps'].get('satellite_count')} satellites"))
+        self.check("health monitor (system_status != OK)", monitor(
+            "unhealthy", lambda v: (v.get("health") or {}).get("system_status", "OK") != "OK",
+            lambda k, v: f"{k}: {v['health'].get('system_status')}"))
+        self.check("collection latency (10 GETs)", latency)
         self.check("UAVMetric CRD list", crds)
+        for k, v in sorted(states().items()):  # reference generate_report
+            print(f"    {k}: battery {(v.get('battery') or {}).get('remaining_percent')}%, "
+                  f"GPS {(v.get('gps') or {}).get('satellite_count')} sats, mode {(v.get('flight') or {}).get('mode')}, "
+                  f"status {(v.get('health') or {}).get('system_status')}")
 
 
 def main(argv=None) -> int:
