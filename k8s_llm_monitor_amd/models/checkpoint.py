@@ -224,7 +224,8 @@ def load_checkpoint(model, path: PathLike, strict: bool = True) -> list[str]:
     unused = [k for k in unused if k not in rope_buffers]
     if strict and unused:
         raise ValueError(f"checkpoint tensors not consumed by {c.name}: {unused[:8]}{' ...' if len(unused) > 8 else ''}")
-    model._init_skinny()  # re-pack the decode-layout copies from the loaded weights
+    model._w13_il = False  # w13 was just loaded as [gate; up]
+    model._init_skinny()  # interleave w13, (re)build the decode-path views from the loaded weights
     return unused
 
 
@@ -295,16 +296,23 @@ def hf_state_dict(model) -> Iterator[tuple[str, torch.Tensor]]:
         yield p + "input_layernorm.weight", L["attn_norm"]
         yield p + "post_attention_layernorm.weight", L["mlp_norm"]
         F = c.ffn_dim
+        from .. import ops
+
+        def canon(w):  # the resident w13 is gate/up-interleaved per 128 rows (CausalLM._init_skinny)
+            return ops.deinterleave_gate_up(w) if model._w13_il else w
+
         if c.is_moe:
             m = p + "block_sparse_moe."
             yield m + "gate.weight", L["router"]
             for e in range(c.n_experts):
-                yield f"{m}experts.{e}.w1.weight", L["w13"][e][:F]
-                yield f"{m}experts.{e}.w3.weight", L["w13"][e][F:]
+                w13 = canon(L["w13"][e])
+                yield f"{m}experts.{e}.w1.weight", w13[:F]
+                yield f"{m}experts.{e}.w3.weight", w13[F:]
                 yield f"{m}experts.{e}.w2.weight", L["w2"][e]
         else:
-            yield p + "mlp.gate_proj.weight", L["w13"][:F]
-            yield p + "mlp.up_proj.weight", L["w13"][F:]
+            w13 = canon(L["w13"])
+            yield p + "mlp.gate_proj.weight", w13[:F]
+            yield p + "mlp.up_proj.weight", w13[F:]
             yield p + "mlp.down_proj.weight", L["w2"]
 
 

@@ -11,14 +11,14 @@ hipGraph:
   -> flash_prefill | paged_decode (HIP MFMA) -> o_proj GEMM (+ RCCL all-reduce at TP>1)
   -> fused_add_rms_norm (HIP) -> gate_up GEMM -> silu_mul (HIP) -> down GEMM (+ all-reduce)
 
-Dense decode at TP=1 runs all four projections through the skinny MFMA GEMM over
-fragment-packed weights (ops/csrc/gemm_skinny.hip; ``_init_skinny``): split-K slabs reduced by
-the next kernel (rope_and_cache, reduce_add_rms_norm) and SwiGLU in the gate_up epilogue -
-7 launches per layer instead of 9.
+Dense decode runs all four projections through the skinny MFMA GEMM over the same row-major
+weights prefill uses (ops/csrc/gemm_skinny.hip, LDS-DMA whole-line staging; ``_init_skinny``):
+split-K slabs reduced by the next kernel (paged_decode_fused, add_norm_partial) and SwiGLU in the
+gate_up epilogue.
 
 Weights are stored fused and pre-sharded: ``wqkv`` [(Hq+2Hkv)/tp * D, d] (column-parallel),
-``wo`` [d, Hq/tp * D] (row-parallel), ``w13`` [2F/tp, d] (gate rows then up rows of this rank's
-shard), ``w2`` [d, F/tp].  Random init is seeded per tensor name, and every rank generates the
+``wo`` [d, Hq/tp * D] (row-parallel), ``w13`` [2F/tp, d] (this rank's gate and up rows, stored
+interleaved per 128 rows as [64 gate | 64 up] - see _init_skinny), ``w2`` [d, F/tp].  Random init is seeded per tensor name, and every rank generates the
 full tensor then keeps its shard, so any TP degree reproduces the TP=1 model exactly.
 """
 from __future__ import annotations
@@ -101,6 +101,8 @@ class CausalLM:
             self.e_lo, self.e_hi = shard_range(cfg.n_experts, tp, r)
         self.moe_comm = os.environ.get("K8SLLM_MOE_COMM", "a2a")  # "a2a" (prefill all-to-all EP) | "allreduce"
         self.layers: list[dict] = []
+        self._w13_il = False  # w13 gate/up-interleaved per 128 rows (set by _init_skinny)
+        self.skinny_layout = None
         self._build()
         self._init_skinny()
         self.cos_sin = None
@@ -237,7 +239,7 @@ class CausalLM:
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
         if slabs is not None and self._fuse_rope:
             # qkv GEMM + RoPE + KV-cache write in one launch (gemm_skinny ROPE epilogue)
-            qkv = torch.empty(T, L["wqkv_p"].shape[0] * 16, dtype=self.dtype, device=self.device)
+            qkv = torch.empty(T, ops.skinny_wdims(L["wqkv_p"])[0], dtype=self.dtype, device=self.device)
             ops.skinny_qkv_rope(x, L["wqkv_p"], qkv, meta.positions, cs, k_cache, v_cache,
                                 meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, rows=T,
                                 apply_rope=c.arch == "llama", rownorm=rownorm, workspace=slabs[0],
@@ -252,7 +254,7 @@ class CausalLM:
                                               meta.block_tables, meta.seq_lens, self.hq, self.hkv, self.D, self.scale,
                                               workspace=meta.decode_ws, out=out)
             partial = ws
-            qkv = torch.empty(T, L["wqkv_p"].shape[0] * 16, dtype=self.dtype, device=self.device)
+            qkv = torch.empty(T, ops.skinny_wdims(L["wqkv_p"])[0], dtype=self.dtype, device=self.device)
         else:
             qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
         if not (slabs is not None and self._fuse_rope):
@@ -294,7 +296,7 @@ class CausalLM:
             if meta.is_prefill and self.tp > 1 and self.moe_comm == "a2a":
                 return self._moe_a2a(L, x)
             return tp_all_reduce(self._moe(L, x, meta), self.ps)
-        h = ops.silu_mul(F.linear(x, L["w13"]))
+        h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=self._w13_il)
         return tp_all_reduce(F.linear(h, L["w2"]), self.ps)
 
     def _moe(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
@@ -313,7 +315,7 @@ class CausalLM:
             wd.scatter_(1, ids.long(), w)
             out = torch.zeros(T, c.d_model, dtype=torch.float32, device=x.device)
             for j, e in enumerate(range(self.e_lo, self.e_hi)):
-                h = ops.silu_mul(F.linear(x, L["w13"][j]))
+                h = ops.silu_mul(F.linear(x, L["w13"][j]), interleaved=self._w13_il)
                 out += F.linear(h, L["w2"][j]).float() * wd[:, e:e + 1]
             return out.to(x.dtype)
         offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
@@ -323,7 +325,7 @@ class CausalLM:
         for j, e in enumerate(range(self.e_lo, self.e_hi)):
             a, b = off[e], off[e + 1]
             if b > a:
-                h = ops.silu_mul(F.linear(xs[a:b], L["w13"][j]))
+                h = ops.silu_mul(F.linear(xs[a:b], L["w13"][j]), interleaved=self._w13_il)
                 ys[a:b] = F.linear(h, L["w2"][j])
         return ops.moe_combine(ys, inv_idx, w, T)
 
@@ -363,7 +365,7 @@ class CausalLM:
         for j, e in enumerate(range(self.e_lo, self.e_hi)):
             rows = (recv_exp == e).nonzero().flatten()
             if rows.numel():
-                h = ops.silu_mul(F.linear(recv[rows], L["w13"][j]))
+                h = ops.silu_mul(F.linear(recv[rows], L["w13"][j]), interleaved=self._w13_il)
                 y[rows] = F.linear(h, L["w2"][j])
         back = x.new_empty(n * K, c.d_model)
         tp_all_to_all(back, y, send_counts, recv_counts, self.ps)
@@ -428,21 +430,36 @@ class CausalLM:
                 and meta.logits_idx is None and os.environ.get("K8SLLM_SKINNY", "1") != "0")
 
     def _init_skinny(self) -> None:
-        """Decode-path weights: a fragment-packed copy of wqkv / wo / w13 (gate/up interleaved per
-        64-row tile) / w2 for gemm_skinny (ops/csrc/gemm_skinny.hip); prefill keeps hipBLASLt on
-        the row-major tensors.  Costs one extra copy of the layer weights (16 GB for Llama-3-8B on
-        a 288 GB MI355X) and buys whole-line weight streaming for every decode projection.
+        """Decode-path weights.  ONE resident copy of every projection: gemm_skinny_rm_kernel
+        (ops/csrc/gemm_skinny.hip) streams the row-major tensors prefill's hipBLASLt GEMMs read -
+        whole 128-B lines by LDS-DMA - within 1-3 % of the old fragment-packed duplicate at every
+        decode batch (tools/bench_skinny_rm.py, profiles/r02/skinny_rm_vs_packed.jsonl), so
+        Llama-3-8B holds 16 GB of weights, not 32, and 70B fits one GPU on the skinny path.
+        ``K8SLLM_SKINNY_LAYOUT=packed`` (or a shape the row-major kernel does not take: N or K not
+        a multiple of 64) keeps fragment-packed copies instead.
 
-        Per layer at decode (7 launches): qkv skinny (split-K slabs) -> rope_and_cache (reduces
-        the slabs, RoPE, KV write) -> paged_decode -> o skinny (slabs) -> reduce_add_rms_norm
-        (residual add + mlp norm) -> gate_up skinny with the SwiGLU epilogue -> down skinny
-        (slabs) -> reduce_add_rms_norm (residual add + next layer's attn norm).
-        TP>1: the column-parallel qkv / gate_up are unchanged; the row-parallel o / down sum their
-        slabs to bf16 (reduce_slabs), all-reduce over RCCL, then fused_add_rms_norm.
+        w13 is stored gate/up-interleaved per 128 rows ([64 gate | 64 up], the SwiGLU epilogue's
+        pairing): called on canonical [gate; up] tensors (after _build or load_checkpoint), it
+        interleaves them in place and prefill's silu_mul reads the interleaved GEMM output.
+
+        Per layer at decode (5-7 launches): qkv skinny (split-K slabs) -> paged_decode_fused (slab
+        reduce, RoPE, KV write, attention) -> o skinny (slabs) -> add_norm_partial (residual add,
+        deferred mlp norm) -> gate_up skinny with the SwiGLU epilogue -> down skinny (slabs) ->
+        add_norm_partial.  TP>1: the row-parallel o / down sum their slabs to bf16 (reduce_slabs),
+        all-reduce over RCCL / the one-shot IPC all-reduce, then fused_add_rms_norm.
         On the CPU the same ops run as fp32 references with the kernels' split-K slicing, so the
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         c = self.cfg
+        ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
+        if not getattr(self, "_w13_il", False) and c.arch == "llama" and ff % 64 == 0:
+            for L in self.layers:
+                w = L["w13"]
+                L["w13"] = (torch.stack([ops.interleave_gate_up(e) for e in w]) if w.dim() == 3
+                            else ops.interleave_gate_up(w)).contiguous()
+                del w
+            self._w13_il = True
+        self._w13_il = getattr(self, "_w13_il", False)
         # opt-in fused epilogues (K8SLLM_FUSED_EPI=1): RoPE + KV write in the qkv GEMM (head_dim
         # 128, any TP); residual add + norm producer in the o / down GEMMs (TP=1 dense: the
         # row-parallel sums need the all-reduce first), each reduced in-launch by the tile's last
@@ -456,23 +473,25 @@ class CausalLM:
         # GEMM's split-K slabs directly: one launch per layer fewer (K8SLLM_ATTN_ROPE=0 disables)
         self._attn_rope = not self._fuse_rope and self.D == 128 and os.environ.get("K8SLLM_ATTN_ROPE", "1") != "0"
         self._fuse_resnorm = fuse and self.tp == 1 and not c.is_moe and c.d_model % 64 == 0
-        if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0":
+        if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0" or not self._w13_il:
             self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
-        ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
-        if d % 64 or nq % 64 or (self.hq * self.D) % 32 or ff % 64:
+        if d % 64 or nq % 64 or (self.hq * self.D) % 32:
             self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
             return
+        rowmajor = os.environ.get("K8SLLM_SKINNY_LAYOUT", "rowmajor") != "packed" and (self.hq * self.D) % 64 == 0
+        self.skinny_layout = "rowmajor" if rowmajor else "packed"
+        keep = (lambda w: w) if rowmajor else ops.pack_skinny
         for L in self.layers:
-            L["wqkv_p"] = ops.pack_skinny(L["wqkv"])
-            L["wo_p"] = ops.pack_skinny(L["wo"])
+            L["wqkv_p"] = keep(L["wqkv"])
+            L["wo_p"] = keep(L["wo"])
             if c.is_moe:  # stacked per local expert for the grouped (grid.z = expert) launches
-                L["w13_pg"] = torch.stack([ops.pack_skinny(ops.interleave_gate_up(w)) for w in L["w13"]])
-                L["w2_pg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
+                L["w13_pg"] = L["w13"] if rowmajor else torch.stack([keep(w) for w in L["w13"]])
+                L["w2_pg"] = L["w2"] if rowmajor else torch.stack([keep(w) for w in L["w2"]])
             else:
-                L["w13_p"] = ops.pack_skinny(ops.interleave_gate_up(L["w13"]))
-                L["w2_p"] = ops.pack_skinny(L["w2"])
+                L["w13_p"] = keep(L["w13"])
+                L["w2_p"] = keep(L["w2"])
         env = os.environ.get("K8SLLM_SKINNY_SPLITS")
         split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split

@@ -100,6 +100,12 @@ def interleave_gate_up(w13: torch.Tensor) -> torch.Tensor:
     return w13.reshape(2, F // 64, 64, K).permute(1, 0, 2, 3).reshape(F2, K)
 
 
+def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """Inverse of interleave_gate_up: per-128-row [64 gate | 64 up] -> [gate (F rows); up (F rows)]."""
+    F2, K = w.shape
+    return w.reshape(F2 // 128, 2, 64, K).permute(1, 0, 2, 3).reshape(F2, K)
+
+
 def skinny_splits(N: int, K: int, target_wgs: int = 256) -> int:
     """Split-K factor for a slab-epilogue gemm_skinny: (N/64) x S workgroups ~ one per CU, each K
     slice at least 512 deep (tools/bench_skinny.py on MI355X, decode batch 1-64: S = 4 beats 2, 6
@@ -133,8 +139,16 @@ def skinny_nslabs(K: int, S: int) -> int:
 
 # CPU forms of the skinny ops: the same packed layouts, split-K slicing and roundings as the
 # kernels, so the decode control flow (and TP over gloo) is exercised by the CPU test suite.
+def skinny_wdims(wp: torch.Tensor) -> tuple:
+    """(N, K) of a skinny-GEMM weight: fragment-packed [N/16, K/32, 64, 8] or row-major [N, K]
+    (the single resident copy, read by gemm_skinny_rm_kernel)."""
+    if wp.dim() == 4:
+        return wp.shape[0] * 16, wp.shape[1] * 32
+    return wp.shape[0], wp.shape[1]
+
+
 def _cpu_w(wp: torch.Tensor) -> torch.Tensor:
-    return unpack_skinny(wp).float()
+    return (unpack_skinny(wp) if wp.dim() == 4 else wp).float()
 
 
 def _cpu_deinterleave(gu: torch.Tensor) -> tuple:
@@ -211,7 +225,7 @@ def skinny_linear(a: torch.Tensor, wp: torch.Tensor, out: Optional[torch.Tensor]
         sc = _rn_scale(rownorm, M, x.shape[1])
         y = (y * sc if sc is not None else y).to(x.dtype)
         return out.copy_(y) if out is not None else y
-    N = wp.shape[0] * 16
+    N = skinny_wdims(wp)[0]
     if out is None:
         out = torch.empty(M, N, dtype=a.dtype, device=a.device)
     native().gemm_skinny(a, wp, None, out, 1, 1, nt_tiles, M, *_rn_args(rownorm))
@@ -224,7 +238,7 @@ def skinny_swiglu(a: torch.Tensor, wp13: torch.Tensor, out: Optional[torch.Tenso
     """``silu(a @ Wg^T) * (a @ Wu^T)`` over a packed, gate/up-interleaved w13: [M, F], or with
     ``packed_out`` the fragment-packed [ceil(M/16), F/32, 64, 8] (the down projection's A)."""
     M = _rows(a, rows)
-    F = wp13.shape[0] * 8
+    F = skinny_wdims(wp13)[0] // 2
     if not _gpu(a):
         x = _cpu_a(a, rows)
         gu = x.float() @ _cpu_w(wp13).t()
@@ -249,7 +263,7 @@ def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, spl
     M = _rows(a, rows)
     if not _gpu(a):
         x = _cpu_a(a, rows)
-        N, K = wp.shape[0] * 16, wp.shape[1] * 32
+        N, K = skinny_wdims(wp)
         if splits <= 0:
             splits = skinny_auto_splits(M, N, K, a.dim() == 4)
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
@@ -269,7 +283,7 @@ def skinny_grouped_swiglu(a: torch.Tensor, wp13: torch.Tensor, rows: int, out: O
     fragment-packed activation [MT, K/32, 64, 8], ``wp13`` the stacked packed, gate/up-interleaved
     expert weights [E, 2F/16, K/32, 64, 8]; returns the per-expert packed SwiGLU activations
     [E, MT, F/32, 64, 8] (the grouped down projection's A)."""
-    E, F = wp13.shape[0], wp13.shape[1] * 8
+    E, F = wp13.shape[0], skinny_wdims(wp13[0])[0] // 2
     mt = -(-rows // 16)
     if not _gpu(a):
         y = torch.stack([skinny_swiglu(a, wp13[e], rows=rows, packed_out=True) for e in range(E)])
@@ -286,7 +300,7 @@ def skinny_grouped_slabs(act: torch.Tensor, wp2: torch.Tensor, workspace: torch.
     expert e's rows are scaled by its routing weights ``row_w[:, e]`` (0 where not selected), so
     summing all slabs (add_norm_partial / reduce_slabs) IS the weighted expert combine.  Returns
     the slab count E * S'."""
-    E, N, K = wp2.shape[0], wp2.shape[1] * 16, wp2.shape[2] * 32
+    E, (N, K) = wp2.shape[0], skinny_wdims(wp2[0])
     M = rows
     if not _gpu(act):
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
@@ -352,7 +366,7 @@ def skinny_resnorm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, no
     ``residual <- bf16(residual + a @ W^T)``; returns ``(residual * norm_w`` fragment-packed,
     ``ss [M, N/64])`` - per-row sums of squares of each tile - for a consumer skinny GEMM called
     with ``rownorm=(ss, eps)``.  Replaces skinny_slabs + add_norm_partial (one launch fewer)."""
-    M, N = rows, wp.shape[0] * 16
+    M, N = rows, skinny_wdims(wp)[0]
     nc = N // 64
     if ss is None:
         ss = torch.empty(M, nc, dtype=torch.float32, device=residual.device)
@@ -386,7 +400,7 @@ def skinny_qkv_rope(a: torch.Tensor, wp: torch.Tensor, qkv: torch.Tensor, positi
         return qkv
     empty = _empty_i32(qkv.device)
     rn_ss, rn_eps = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
-    N = wp.shape[0] * 16
+    N = skinny_wdims(wp)[0]
     native().gemm_skinny_qkv_rope(a, wp, rows, qkv, positions, cos_sin,
                                   k_cache if k_cache is not None else empty,
                                   v_cache if v_cache is not None else empty,
@@ -438,7 +452,7 @@ def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor,
     ``residual <- residual + a @ W^T``; returns ``rms_norm(residual) * norm_w`` (row-major, or
     fragment-packed with ``packed_out``).  GPU: gemm_skinny (packed ``wp``, split-K fp32 slabs)
     then reduce_add_rms_norm."""
-    M, N, K = _rows(a, rows), wp.shape[0] * 16, wp.shape[1] * 32
+    M, (N, K) = _rows(a, rows), skinny_wdims(wp)
     if splits is None:
         splits = 0  # automatic (launcher)
     if workspace is None:
@@ -470,12 +484,15 @@ def layer_norm(x, w, b, eps):
     return out
 
 
-def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None, interleaved: bool = False) -> torch.Tensor:
+    """silu(gate) * up over [.., 2F] gate_up activations: [F gate | F up], or ``interleaved``
+    [64 gate | 64 up] per 128 columns (the output of the single resident, interleaved w13)."""
     if not _gpu(x):
-        return ref.silu_mul(x)
+        y = ref.silu_mul(x, interleaved)
+        return out.copy_(y) if out is not None else y
     if out is None:
         out = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
-    native().silu_mul(out, x)
+    native().silu_mul(out, x.contiguous(), interleaved)
     return out
 
 

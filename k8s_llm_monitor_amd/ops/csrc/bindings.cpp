@@ -10,7 +10,7 @@ int k8sllm_rmsnorm(void* out, const void* x, void* residual, const void* w, long
                    long x_stride, long out_stride, hipStream_t s);
 int k8sllm_layernorm(void* out, const void* x, const void* w, const void* b, long rows, int d, float eps,
                      hipStream_t s);
-int k8sllm_silu_mul(void* out, const void* x, long rows, int F, hipStream_t s);
+int k8sllm_silu_mul(void* out, const void* x, long rows, int F, int interleaved, hipStream_t s);
 int k8sllm_gelu_tanh(void* out, const void* x, long n, hipStream_t s);
 int k8sllm_embedding(void* out, const int* ids, const void* weight, long T, int d, int vocab_start, int rows,
                      hipStream_t s);
@@ -42,12 +42,12 @@ int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, 
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                        float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
-                       const float* row_w, int row_w_ld, hipStream_t s);
+                       const float* row_w, int row_w_ld, int w_rm, hipStream_t s);
 int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* partial, int splits, int* counters, void* Y,
                              long ldy, int M, int N, int K, int epi, const float* rn_ss, int rn_nc, float rn_eps,
                              int waves, void* residual, const void* norm_w, float* ss_out, const int* positions,
                              const float* cos_sin, void* k_cache, void* v_cache, const int* slot_mapping, int Hq,
-                             int Hkv, int block_size, int apply_rope, hipStream_t s);
+                             int Hkv, int block_size, int apply_rope, int w_rm, hipStream_t s);
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
@@ -112,12 +112,14 @@ void layer_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, torch::Tens
         "layer_norm");
 }
 
-void silu_mul(torch::Tensor out, torch::Tensor x) {
+// interleaved: x columns are [64 gate | 64 up] per 128 (ops.interleave_gate_up) instead of [F | F]
+void silu_mul(torch::Tensor out, torch::Tensor x, bool interleaved) {
   dev_bf16(out, "out"); dev_bf16(x, "x");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "silu_mul: contiguous");
   const int F = (int)out.size(-1);
   TORCH_CHECK(x.size(-1) == 2 * F, "silu_mul: x last dim must be 2*F");
-  check(k8sllm_silu_mul(out.data_ptr(), x.data_ptr(), out.numel() / F, F, cur()), "silu_mul");
+  TORCH_CHECK(!interleaved || F % 64 == 0, "silu_mul: interleaved gate/up needs F % 64 == 0");
+  check(k8sllm_silu_mul(out.data_ptr(), x.data_ptr(), out.numel() / F, F, interleaved ? 1 : 0, cur()), "silu_mul");
 }
 
 void gelu_tanh(torch::Tensor out, torch::Tensor x) {
@@ -357,7 +359,25 @@ static void rownorm_args(const c10::optional<torch::Tensor>& rn_ss, int M, int K
   rn_nc = (int)rn_ss->size(1);
 }
 
-// Skinny decode GEMM over a fragment-packed weight wp [N/16][K/32][64][8] (gemm_skinny.hip).
+// Weight of a skinny GEMM: fragment-packed [N/16, K/32, 64, 8] (a decode-only copy), or the
+// row-major [N, K] tensor itself (gemm_skinny_rm_kernel, the single resident copy prefill's GEMMs
+// read as well).  `lead` = leading (expert) dimensions.  Returns w_rm.
+static int skinny_weight_dims(const torch::Tensor& wp, int lead, int& N, int& K, const char* what) {
+  TORCH_CHECK(wp.is_contiguous(), what, ": weight must be contiguous");
+  if (wp.dim() == lead + 4 && wp.size(lead + 2) == 64 && wp.size(lead + 3) == 8) {
+    N = (int)wp.size(lead) * 16;
+    K = (int)wp.size(lead + 1) * 32;
+    return 0;
+  }
+  TORCH_CHECK(wp.dim() == lead + 2, what, ": weight must be fragment-packed [N/16, K/32, 64, 8] or row-major [N, K]");
+  N = (int)wp.size(lead);
+  K = (int)wp.size(lead + 1);
+  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, what, ": row-major weight needs N % 64 == 0 and K % 64 == 0");
+  return 1;
+}
+
+// Skinny decode GEMM over a fragment-packed weight wp [N/16][K/32][64][8] or the row-major [N][K]
+// weight (gemm_skinny.hip).
 // epi 0: fp32 split-K slabs partial[S'][M][N], returns S'; epi 1: y = bf16(a . W^T);
 // epi 2: y[M, N/2] = silu(gate) * up over a [32 gate | 32 up]-interleaved weight; epi 3: the same
 // written fragment-packed.  Returns the
@@ -366,10 +386,10 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
                     c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows,
                     c10::optional<torch::Tensor> rn_ss, double rn_eps, bool wide, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
-  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
-              "gemm_skinny: wp must be fragment-packed [N/16, K/32, 64, 8]");
-  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32;
+  int N, K;
+  const int w_rm = skinny_weight_dims(wp, 0, N, K, "gemm_skinny");
   const bool a_packed = a.dim() == 4;
+  TORCH_CHECK(!w_rm || a_packed, "gemm_skinny: a row-major weight needs a fragment-packed a");
   int M;
   if (a_packed) {  // fragment-packed activations [ceil(M/16), K/32, 64, 8]; `rows` = valid rows
     TORCH_CHECK(a.is_contiguous() && a.size(1) * 32 == K && a.size(2) == 64 && a.size(3) == 8,
@@ -415,7 +435,7 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   rownorm_args(rn_ss, M, K, rp, rn_nc);
   check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
                            epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, rp, rn_nc, K,
-                           (float)rn_eps, wide ? 1 : 0, (int)waves, 1, 0, 0, 0, nullptr, 0, cur()),
+                           (float)rn_eps, wide ? 1 : 0, (int)waves, 1, 0, 0, 0, nullptr, 0, w_rm, cur()),
         "gemm_skinny");
   return S;
 }
@@ -429,10 +449,10 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
                             c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t rows,
                             c10::optional<torch::Tensor> row_w, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
-  TORCH_CHECK(wp.dim() == 5 && wp.size(3) == 64 && wp.size(4) == 8 && wp.is_contiguous(),
-              "gemm_skinny_grouped: wp must be [E, N/16, K/32, 64, 8]");
+  int N, K;
+  const int w_rm = skinny_weight_dims(wp, 1, N, K, "gemm_skinny_grouped");
   TORCH_CHECK(epi == 0 || epi == 3, "gemm_skinny_grouped: epi must be 0 (slabs) or 3 (packed SwiGLU)");
-  const int E = (int)wp.size(0), N = (int)wp.size(1) * 16, K = (int)wp.size(2) * 32, M = (int)rows;
+  const int E = (int)wp.size(0), M = (int)rows;
   const long w_es = wp[0].numel();
   TORCH_CHECK(M > 0 && M <= 64, "gemm_skinny_grouped: 1..64 rows");
   const int MT = (M + 15) / 16;
@@ -473,7 +493,8 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
     y_es = (*y)[0].numel();
   }
   check(k8sllm_gemm_skinny(a.data_ptr(), 0, wp.data_ptr(), pp, yp, 0, M, N, K, epi == 0 ? (int)splits : 1,
-                           (int)epi, 4, 1, nullptr, 0, K, 0.f, 0, (int)waves, E, w_es, a_es, y_es, rw, E, cur()),
+                           (int)epi, 4, 1, nullptr, 0, K, 0.f, 0, (int)waves, E, w_es, a_es, y_es, rw, E, w_rm,
+                           cur()),
         "gemm_skinny_grouped");
   return epi == 0 ? (int64_t)E * S : 1;
 }
@@ -495,8 +516,9 @@ int64_t gemm_skinny_resnorm(torch::Tensor a, torch::Tensor wp, int64_t rows, tor
                             torch::Tensor counters, int64_t splits, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp"); dev_bf16(residual, "residual"); dev_bf16(norm_w, "norm_w");
   dev_bf16(out, "out");
-  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(), "resnorm: wp layout");
-  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32, M = (int)rows;
+  int N, K;
+  const int w_rm = skinny_weight_dims(wp, 0, N, K, "resnorm");
+  const int M = (int)rows;
   TORCH_CHECK(N % 64 == 0, "resnorm: N % 64 != 0");
   TORCH_CHECK(M > 0 && M <= 64, "resnorm: 1..64 rows");
   TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(0) * 16 >= M && a.size(1) * 32 == K && a.size(2) == 64 &&
@@ -515,7 +537,7 @@ int64_t gemm_skinny_resnorm(torch::Tensor a, torch::Tensor wp, int64_t rows, tor
   check(k8sllm_gemm_skinny_fused(a.data_ptr(), wp.data_ptr(), partial.data_ptr<float>(), (int)splits,
                                  counters.data_ptr<int>(), out.data_ptr(), 0, M, N, K, 4, nullptr, 0, 0.f, (int)waves,
                                  residual.data_ptr(), norm_w.data_ptr(), ss_out.data_ptr<float>(), nullptr, nullptr,
-                                 nullptr, nullptr, nullptr, 0, 0, 0, 0, cur()),
+                                 nullptr, nullptr, nullptr, 0, 0, 0, 0, w_rm, cur()),
         "gemm_skinny_resnorm");
   return S;
 }
@@ -528,8 +550,9 @@ int64_t gemm_skinny_qkv_rope(torch::Tensor a, torch::Tensor wp, int64_t rows, to
                              bool apply_rope, c10::optional<torch::Tensor> rn_ss, double rn_eps,
                              torch::Tensor partial, torch::Tensor counters, int64_t splits, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp"); dev_bf16(qkv, "qkv"); dev_i32(positions, "positions");
-  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(), "qkv_rope: wp layout");
-  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32, M = (int)rows;
+  int N, K;
+  const int w_rm = skinny_weight_dims(wp, 0, N, K, "qkv_rope");
+  const int M = (int)rows;
   TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "qkv_rope: N must be (Hq + 2 Hkv) * 128");
   TORCH_CHECK(M > 0 && M <= 64, "qkv_rope: 1..64 rows");
   TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(0) * 16 >= M && a.size(1) * 32 == K && a.size(2) == 64 &&
@@ -562,7 +585,7 @@ int64_t gemm_skinny_qkv_rope(torch::Tensor a, torch::Tensor wp, int64_t rows, to
                                  cos_sin.data_ptr<float>(), has_cache ? k_cache.data_ptr() : nullptr,
                                  has_cache ? v_cache.data_ptr() : nullptr,
                                  has_cache ? slot_mapping.data_ptr<int>() : nullptr, (int)Hq, (int)Hkv, block_size,
-                                 apply_rope ? 1 : 0, cur()),
+                                 apply_rope ? 1 : 0, w_rm, cur()),
         "gemm_skinny_qkv_rope");
   return S;
 }

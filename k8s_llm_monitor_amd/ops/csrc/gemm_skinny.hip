@@ -218,6 +218,78 @@ __device__ __forceinline__ void skinny_fused_tail(const float* __restrict__ part
   }
 }
 
+// Cross-wave combine of the per-wave accumulators and the epilogue (shared by the packed and the
+// row-major kernels), one m-tile per round.  red: [WAVES][NT][64][4] floats.  s_inv: the A rows'
+// 1/rms (deferred RMSNorm) or nullptr.  C/D layout of the 16x16 tile: col = lane & 15, rows
+// (lane >> 4) * 4 + r.
+template <int MT, int NT, int EPI, int WAVES>
+__device__ __forceinline__ void skinny_epilogue(const f32x4 (&acc)[MT][NT], float* red, const float* s_inv,
+                                                float* __restrict__ partial, bf16_t* __restrict__ Y, long ldy, int M,
+                                                int N, int ntile0, int s, int ex, const SkinnyGroup& grp) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto R = [&](int w, int nt, int l) -> f32x4* {
+    return reinterpret_cast<f32x4*>(red + ((w * NT + nt) * 64 + l) * 4);
+  };
+  constexpr int NOUT = EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED ? NT / 2 : NT;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    if (mt > 0) __syncthreads();  // previous round's reads done
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) *R(wave, nt, lane) = acc[mt][nt];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < NOUT * 64; idx += 64 * WAVES) {
+      const int nt = idx >> 6, l = idx & 63;
+      f32x4 v = *R(0, nt, l);
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) v += *R(w, nt, l);
+      // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms
+      // (s_inv, computed at kernel start) is applied here - linear, so exact for split-K slabs too
+      f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
+      if (s_inv != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rs[r] = s_inv[mt * 16 + (l >> 4) * 4 + r];
+      }
+      v *= rs;
+      if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
+        f32x4 u = *R(0, nt + NT / 2, l);
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) u += *R(w, nt + NT / 2, l);
+        u *= rs;
+        // gate n-tiles 8q + 2h + {0,1} pair with up n-tiles 8q + 4 + 2h + {0,1} (swiglu_tile)
+        const int f = (blockIdx.x >> 1) * 64 + (blockIdx.x & 1) * 32 + nt * 16 + (l & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + (l >> 4) * 4 + r;
+          // the gate and up values are rounded to bf16 first, as the unfused GEMM -> silu_mul does
+          const float g = bf2f(f2bf(v[r]));
+          const float uu = bf2f(f2bf(u[r]));
+          const bf16_t o = f2bf(g * uu / (1.f + __expf(-g)));
+          if constexpr (EPI == EPI_SWIGLU_PACKED) {
+            // fragment-packed activation for the down projection's A operand: [MT][F/32][64][8]
+            const int F = N >> 1;
+            Y[(((long)mt * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 + (row & 15)) * 8 + (f & 7)] = o;
+          } else if (row < M) {
+            Y[(long)row * ldy + f] = o;
+          }
+        }
+      } else {  // SLAB / BF16; the fused epilogues write their split-K slab here too (reduced after)
+        const int col = swiglu_tile<EPI, NT>(ntile0, nt) * 16 + (l & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + (l >> 4) * 4 + r;
+          if (row < M) {
+            const float o = grp.row_w != nullptr ? v[r] * grp.row_w[(long)row * grp.row_w_ld + ex] : v[r];
+            if constexpr (EPI == EPI_BF16)
+              Y[(long)row * ldy + col] = f2bf(o);
+            else
+              partial[((long)(ex * gridDim.y + s) * M + row) * N + col] = o;
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int MT, int NT, int EPI, bool APK, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
@@ -322,66 +394,159 @@ __global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t
     }
   }
 
-  // cross-wave combine, one m-tile per round (keeps LDS at 16 KiB so occupancy is VGPR-bound).
-  // C/D layout of the 16x16 tile: col = lane & 15, rows (lane >> 4) * 4 + r
-  constexpr int NOUT = EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED ? NT / 2 : NT;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    if (mt > 0) __syncthreads();  // previous round's reads done
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(&red[wave][nt][lane][0]) = acc[mt][nt];
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < NOUT * 64; idx += 64 * WAVES) {
-      const int nt = idx >> 6, l = idx & 63;
-      f32x4 v = *reinterpret_cast<const f32x4*>(&red[0][nt][l][0]);
-#pragma unroll
-      for (int w = 1; w < WAVES; ++w) v += *reinterpret_cast<const f32x4*>(&red[w][nt][l][0]);
-      // deferred RMSNorm of the A rows (add_norm_partial): A held x * w, the row's 1/rms
-      // (s_inv, computed at kernel start) is applied here - linear, so exact for split-K slabs too
-      f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
-      if (rn_ss != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rs[r] = s_inv[mt * 16 + (l >> 4) * 4 + r];
-      }
-      v *= rs;
-      if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
-        f32x4 u = *reinterpret_cast<const f32x4*>(&red[0][nt + NT / 2][l][0]);
-#pragma unroll
-        for (int w = 1; w < WAVES; ++w) u += *reinterpret_cast<const f32x4*>(&red[w][nt + NT / 2][l][0]);
-        u *= rs;
-        // gate n-tiles 8q + 2h + {0,1} pair with up n-tiles 8q + 4 + 2h + {0,1} (swiglu_tile)
-        const int f = (blockIdx.x >> 1) * 64 + (blockIdx.x & 1) * 32 + nt * 16 + (l & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + (l >> 4) * 4 + r;
-          // the gate and up values are rounded to bf16 first, as the unfused GEMM -> silu_mul does
-          const float g = bf2f(f2bf(v[r]));
-          const float uu = bf2f(f2bf(u[r]));
-          const bf16_t o = f2bf(g * uu / (1.f + __expf(-g)));
-          if constexpr (EPI == EPI_SWIGLU_PACKED) {
-            // fragment-packed activation for the down projection's A operand: [MT][F/32][64][8]
-            const int F = N >> 1;
-            Y[(((long)mt * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 + (row & 15)) * 8 + (f & 7)] = o;
-          } else if (row < M) {
-            Y[(long)row * ldy + f] = o;
-          }
-        }
-      } else {  // SLAB / BF16; the fused epilogues write their split-K slab here too (reduced below)
-        const int col = swiglu_tile<EPI, NT>(ntile0, nt) * 16 + (l & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + (l >> 4) * 4 + r;
-          if (row < M) {
-            const float o = grp.row_w != nullptr ? v[r] * grp.row_w[(long)row * grp.row_w_ld + ex] : v[r];
-            if constexpr (EPI == EPI_BF16)
-              Y[(long)row * ldy + col] = f2bf(o);
-            else
-              partial[((long)(ex * gridDim.y + s) * M + row) * N + col] = o;
-          }
-        }
-      }
-    }
+  skinny_epilogue<MT, NT, EPI, WAVES>(acc, &red[0][0][0][0], rn_ss != nullptr ? s_inv : nullptr, partial, Y, ldy, M,
+                                      N, ntile0, s, ex, grp);
+  if constexpr (EPI == EPI_RESNORM || EPI == EPI_ROPE) skinny_fused_tail<MT, EPI, WAVES>(partial, Y, ldy, M, N, ep);
+}
+
+// Row-major weights, LDS-DMA staged: the SAME decomposition, epilogues and fragment-packed A as
+// gemm_skinny_kernel, but W is the plain row-major [N][K] tensor that prefill's hipBLASLt GEMMs
+// also read - one resident copy of every projection (no fragment-packed duplicate).
+//
+// Why LDS: an MFMA B fragment (16 rows x 32 k) read straight from a row-major W touches 16 rows x
+// 64 B per wave-instruction; whole-line orders stream 1.5-4x faster (tools/membw.hip).  Here each
+// wave streams its own rows in whole 128-B lines with global_load_lds_dwordx4 (8 rows x 128 B per
+// instruction, non-temporal: weights are read once per step) into a private two-slot LDS ring,
+// and reads the fragments back with conflict-free ds_read_b128: the 16-B chunk c of LDS row r
+// holds global chunk c ^ ((r >> 1) & 7), so the 16 rows of one fragment read hit 16 distinct
+// bank quads (cdna_hip_programming.md T2; the swizzle sits on the per-lane SOURCE address because
+// the DMA writes lane-linear, rule 21).  The fragment-packed A operand is staged the same way
+// (1 KiB contiguous per m-tile and k-step, read lane-linear).  Every load of the main loop is an
+// LDS-DMA, so the waits are explicit counted vmcnt (hipcc drains to vmcnt(0) beside a mix of
+// DMA and register loads, §5 "Projection GEMM" item 4(b)); no barrier - each wave reads only
+// what it loaded itself.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int MT, int NT, int EPI, int WAVES>
+struct SkinnyRmGeom {
+  static constexpr int U = 2;                        // k-steps per stage: 64 k = one 128-B line per row
+  static constexpr int WB = NT * 16 * 128;           // W bytes per stage
+  static constexpr int AB = MT * U * 1024;           // A bytes per stage
+  static constexpr int SB = WB + AB;
+  static constexpr int RING = 2 * SB;                // per wave
+  static constexpr int RED = WAVES * NT * 64 * 16;   // cross-wave combine (aliases the rings)
+  static constexpr int EPI_LDS = RED + MT * 16 * 4;  // + s_inv, written after the main loop
+  static constexpr int LDS = WAVES * RING > EPI_LDS ? WAVES * RING : EPI_LDS;
+  static constexpr int NLOAD = NT * 2 + MT * U;      // DMA instructions per stage
+};
+
+template <int MT, int NT, int EPI, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, long ldw, float* __restrict__ partial,
+    bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
+    float rn_inv_d, float rn_eps, SkinnyGroup grp, SkinnyEpi ep) {
+  using G = SkinnyRmGeom<MT, NT, EPI, WAVES>;
+  constexpr int U = G::U;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  float* s_inv = reinterpret_cast<float*>(smem + G::RED);  // aliases a ring: written after the loop
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int ntile0 = blockIdx.x * NT;
+  const int s = blockIdx.y;
+  const int ex = blockIdx.z;
+  W += ex * grp.w_es;
+  A += ex * grp.a_es;
+  if (Y != nullptr) Y += ex * grp.y_es;
+  const int kbeg = s * kchunk;
+  const int nsteps = (min(K, kbeg + kchunk) - kbeg) >> 5;  // host: 64 | K and 64 | kchunk
+  const int ksteps = K >> 5;
+  const int ngroups = nsteps / U;
+
+  // deferred RMSNorm: this thread's partial sum of squares of one A row, loaded before the first
+  // DMA (its waits then drain nothing of the ring) and held in a register through the main loop
+  float ss = 0.f;
+  if (rn_ss != nullptr && threadIdx.x < MT * 64) {
+    const int row = min((int)(threadIdx.x >> 2), M - 1);
+    for (int c = threadIdx.x & 3; c < rn_nc; c += 4) ss += rn_ss[row * rn_nc + c];
   }
+
+  // per-lane DMA sources at k-step 0 of the slice: W instruction j covers LDS rows 8j..8j+7
+  const bf16_t* wsrc[NT * 2];
+#pragma unroll
+  for (int j = 0; j < NT * 2; ++j) {
+    const int rl = 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((rl >> 1) & 7);
+    const long grow = (long)swiglu_tile<EPI, NT>(ntile0, rl >> 4) * 16 + (rl & 15);
+    wsrc[j] = W + grow * ldw + kbeg + c * 8;
+  }
+  const bf16_t* asrc = A + ((long)(kbeg >> 5) * 64 + lane) * 8;
+  char* ring = smem + wave * G::RING;
+
+  auto issue = [&](int slot, int g) {
+    const int k0 = g * U;  // k-step within the slice
+    char* st = ring + slot * G::SB;
+#pragma unroll
+    for (int j = 0; j < NT * 2; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(wsrc[j] + k0 * 32), (lds_void_t*)(st + j * 1024), 16, 0, 2);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc + ((long)mt * ksteps + k0 + u) * 512),
+                                         (lds_void_t*)(st + G::WB + (mt * U + u) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within a stage)
+  int woff[NT][U];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rl = nt * 16 + (lane & 15);
+      woff[nt][u] = rl * 128 + (((u * 4 + (lane >> 4)) ^ ((rl >> 1) & 7)) << 4);
+    }
+
+  // groups g = wave, wave + WAVES, ... ; two stages in flight per wave
+  const int nmy = wave < ngroups ? (ngroups - wave + WAVES - 1) / WAVES : 0;
+  if (nmy > 0) issue(0, wave);
+  if (nmy > 1) issue(1, wave + WAVES);
+  for (int i = 0; i < nmy; ++i) {
+    const int slot = i & 1;
+    if (i + 1 < nmy)
+      wait_vmcnt<G::NLOAD>();  // stage i landed, stage i + 1 may still fly
+    else
+      wait_vmcnt<0>();
+    const char* st = ring + slot * G::SB;
+    bf16x8 bw[U][NT], ba[U][MT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bw[u][nt] = *reinterpret_cast<const bf16x8*>(st + woff[nt][u]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        ba[u][mt] = *reinterpret_cast<const bf16x8*>(st + G::WB + (mt * U + u) * 1024 + lane * 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers: the slot is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (i + 2 < nmy) issue(slot, wave + (i + 2) * WAVES);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][mt], bw[u][nt], acc[mt][nt], 0, 0, 0);
+  }
+  __syncthreads();  // every wave is done with its ring before the combine buffer aliases it
+  if (rn_ss != nullptr && threadIdx.x < MT * 64) {  // published by the epilogue's first barrier
+    ss += __shfl_xor(ss, 1, kWave);
+    ss += __shfl_xor(ss, 2, kWave);
+    if ((threadIdx.x & 3) == 0) s_inv[threadIdx.x >> 2] = rsqrtf(ss * rn_inv_d + rn_eps);
+  }
+  skinny_epilogue<MT, NT, EPI, WAVES>(acc, reinterpret_cast<float*>(smem), rn_ss != nullptr ? s_inv : nullptr,
+                                      partial, Y, ldy, M, N, ntile0, s, ex, grp);
   if constexpr (EPI == EPI_RESNORM || EPI == EPI_ROPE) skinny_fused_tail<MT, EPI, WAVES>(partial, Y, ldy, M, N, ep);
 }
 
@@ -642,11 +807,12 @@ extern "C" int k8sllm_reduce_slabs(void* out, const float* partial, int S, long 
 
 // kchunk: K split into `S` slices rounded up to whole wave groups (128 k) where that keeps the
 // slice count, else to whole k-steps.
-static int skinny_kchunk(int K, int S) {
+// `gran`: the smallest slice granule (32: one k-step; 64 for the row-major kernel's 64-deep stages).
+static int skinny_kchunk(int K, int S, int gran = 32) {
   int kc = (K + S - 1) / S;
   const int kc128 = (kc + 127) / 128 * 128;
   if ((K + kc128 - 1) / kc128 == S) return kc128;
-  return (kc + 31) / 32 * 32;
+  return (kc + gran - 1) / gran * gran;
 }
 
 extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
@@ -678,15 +844,15 @@ extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed,
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                          float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
-                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, hipStream_t s);
+                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s);
 
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
                                   int rn_nc, int rn_d, float rn_eps, int wide, int waves, int experts, long w_es,
-                                  long a_es, long y_es, const float* row_w, int row_w_ld, hipStream_t s) {
+                                  long a_es, long y_es, const float* row_w, int row_w_ld, int w_rm, hipStream_t s) {
   if (epi == EPI_RESNORM || epi == EPI_ROPE) return -6;  // fused epilogues: k8sllm_gemm_skinny_fused
   return skinny_launch(A, lda, Wp, partial, Y, ldy, M, N, K, S, epi, nt_tiles, a_packed, rn_ss, rn_nc, rn_d, rn_eps,
-                       wide, waves, experts, w_es, a_es, y_es, row_w, row_w_ld, SkinnyEpi{}, s);
+                       wide, waves, experts, w_es, a_es, y_es, row_w, row_w_ld, SkinnyEpi{}, w_rm, s);
 }
 
 // Fused epilogues (A fragment-packed, 64-column tiles, split-K slabs in `partial` reduced by each
@@ -699,7 +865,7 @@ extern "C" int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* pa
                                         int rn_nc, float rn_eps, int waves, void* residual, const void* norm_w,
                                         float* ss_out, const int* positions, const float* cos_sin, void* k_cache,
                                         void* v_cache, const int* slot_mapping, int Hq, int Hkv, int block_size,
-                                        int apply_rope, hipStream_t s) {
+                                        int apply_rope, int w_rm, hipStream_t s) {
   if (partial == nullptr || counters == nullptr || N % 64 != 0) return -7;
   if (epi == EPI_RESNORM) {
     if (residual == nullptr || norm_w == nullptr || ss_out == nullptr) return -7;
@@ -712,20 +878,62 @@ extern "C" int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* pa
   SkinnyEpi ep{(bf16_t*)residual, (const bf16_t*)norm_w, ss_out, positions, cos_sin, (bf16_t*)k_cache,
                (bf16_t*)v_cache, slot_mapping, counters, Hq, Hkv, block_size, apply_rope};
   return skinny_launch(A, 0, Wp, partial, Y, ldy, M, N, K, splits, epi, 4, 1, rn_ss, rn_nc, K, rn_eps, 0, waves, 1,
-                       0, 0, 0, nullptr, 0, ep, s);
+                       0, 0, 0, nullptr, 0, ep, w_rm, s);
 }
 
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                          float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
-                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, hipStream_t s) {
+                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s) {
   if (M <= 0) return 0;
   if (experts < 1) return -5;
-  if (experts > 1) wide = 0;  // grouped launches use the narrow kernel
+  if (experts > 1 || w_rm) wide = 0;  // grouped / row-major launches use the narrow decomposition
   const SkinnyGroup grp{w_es, a_es, y_es, row_w, row_w_ld};
   if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed, wide) : 1;  // fused: caller
-  const int kc = skinny_kchunk(K, S);
+  const int kc = skinny_kchunk(K, S, w_rm ? 64 : 32);
+  if (w_rm) {
+    if (!a_packed || K % 64 != 0 || N % 64 != 0) return -9;  // row-major W: packed A, 64-deep stages, NT = 4
+    const int slabs_rm = (K + kc - 1) / kc;
+    if (epi != EPI_SLAB && epi != EPI_RESNORM && epi != EPI_ROPE && slabs_rm != 1) return -3;
+    const float inv_d_rm = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
+    const int MT = (M + 15) / 16;
+    // 4 waves per workgroup unless the grid then needs more than one round of workgroups: each
+    // wave's ring holds two 16-KiB stages at M = 64, so LDS caps residency (4 waves: 1 workgroup
+    // per CU at MT 2-4); 2-wave workgroups keep e.g. gate_up's 448 tiles co-resident.
+    // waves = 2 or 4 forces one.
+    static const int lds4[5] = {0, SkinnyRmGeom<1, 4, 0, 4>::LDS, SkinnyRmGeom<2, 4, 0, 4>::LDS,
+                                SkinnyRmGeom<3, 4, 0, 4>::LDS, SkinnyRmGeom<4, 4, 0, 4>::LDS};
+    const long nwg = (long)(N / 64) * slabs_rm * experts;
+    int rw = waves == 2 || waves == 4 ? waves : 4;
+    if (waves != 2 && waves != 4 && nwg > 256L * (163840 / lds4[MT])) rw = 2;
+    dim3 grid(N / 64, slabs_rm, experts), blk(64 * rw);
+#define K8S_RM(MTV, EPV)                                                                                             \
+  if (rw == 4)                                                                                                       \
+    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 4, EPV, 4>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep);     \
+  else                                                                                                               \
+    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 4, EPV, 2>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep)
+#define K8S_RM_M(EPV)                  \
+  switch (MT) {                        \
+    case 1: K8S_RM(1, EPV); break;     \
+    case 2: K8S_RM(2, EPV); break;     \
+    case 3: K8S_RM(3, EPV); break;     \
+    default: K8S_RM(4, EPV); break;    \
+  }
+    switch (epi) {
+      case EPI_SLAB: K8S_RM_M(EPI_SLAB) break;
+      case EPI_BF16: K8S_RM_M(EPI_BF16) break;
+      case EPI_SWIGLU: K8S_RM_M(EPI_SWIGLU) break;
+      case EPI_SWIGLU_PACKED: K8S_RM_M(EPI_SWIGLU_PACKED) break;
+      case EPI_RESNORM: K8S_RM_M(EPI_RESNORM) break;
+      default: K8S_RM_M(EPI_ROPE) break;
+    }
+#undef K8S_RM_M
+#undef K8S_RM
+    return (int)hipGetLastError();
+  }
   const int slabs = (K + kc - 1) / kc;
   if (epi != EPI_SLAB && epi != EPI_RESNORM && epi != EPI_ROPE && slabs != 1) return -3;
   if ((epi == EPI_SWIGLU || epi == EPI_SWIGLU_PACKED || epi == EPI_ROPE || epi == EPI_RESNORM) && nt_tiles != 4)

@@ -112,6 +112,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(bf16_t* __restrict__ out
 }
 
 // SwiGLU: x = [gate | up] per row (width 2F), out = silu(gate) * up (width F).
+// IL: gate/up interleaved per 128 columns as [64 gate | 64 up] (the single resident w13 layout,
+// ops.interleave_gate_up, shared with the decode skinny SwiGLU epilogue); else [F gate | F up].
+template <bool IL>
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
                                                        long rows, int F) {
   // grid (ceil(F/8 / 256), min(rows, 65535)): 2-D indexing, no 64-bit division per element
@@ -122,8 +125,10 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
     float g[8], u[8], o[8];
     // the gate_up activations are read exactly once: non-temporal loads
     typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-    const u32x4_t ga = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + c));
-    const u32x4_t ua = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + F + c));
+    const int gc = IL ? ((c >> 6) << 7) + (c & 63) : c;
+    const int uc = IL ? gc + 64 : F + c;
+    const u32x4_t ga = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + gc));
+    const u32x4_t ua = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(xr + uc));
     unpack8(make_uint4(ga.x, ga.y, ga.z, ga.w), g);
     unpack8(make_uint4(ua.x, ua.y, ua.z, ua.w), u);
 #pragma unroll
@@ -223,11 +228,14 @@ int k8sllm_layernorm(void* out, const void* x, const void* w, const void* b, lon
   return (int)hipGetLastError();
 }
 
-int k8sllm_silu_mul(void* out, const void* x, long rows, int F, hipStream_t s) {
-  if (F % 8 != 0) return -1;
+int k8sllm_silu_mul(void* out, const void* x, long rows, int F, int interleaved, hipStream_t s) {
+  if (F % 8 != 0 || (interleaved && F % 64 != 0)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3((F / 8 + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535)), dim3(256), 0,
-                     s, (bf16_t*)out, (const bf16_t*)x, rows, F);
+  const dim3 grid((F / 8 + 255) / 256, (unsigned)(rows < 65535 ? rows : 65535));
+  if (interleaved)
+    hipLaunchKernelGGL(silu_mul_kernel<true>, grid, dim3(256), 0, s, (bf16_t*)out, (const bf16_t*)x, rows, F);
+  else
+    hipLaunchKernelGGL(silu_mul_kernel<false>, grid, dim3(256), 0, s, (bf16_t*)out, (const bf16_t*)x, rows, F);
   return (int)hipGetLastError();
 }
 

@@ -30,9 +30,13 @@ def layer_norm(x, w, b, eps):
     return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
 
 
-def silu_mul(x: torch.Tensor) -> torch.Tensor:
+def silu_mul(x: torch.Tensor, interleaved: bool = False) -> torch.Tensor:
+    """silu(gate) * up; ``interleaved``: columns are [64 gate | 64 up] per 128."""
     f = x.shape[-1] // 2
     xf = x.float()
+    if interleaved:
+        t = xf.reshape(*xf.shape[:-1], f // 64, 2, 64)
+        return (F.silu(t[..., 0, :]) * t[..., 1, :]).reshape(*xf.shape[:-1], f).to(x.dtype)
     return (F.silu(xf[..., :f]) * xf[..., f:]).to(x.dtype)
 
 

@@ -115,7 +115,13 @@ def test_tp_shards_from_checkpoint(tmp_path):
         k = L0["wqkv"][nq:nq + nk].chunk(2)[r]
         v = L0["wqkv"][nq + nk:].chunk(2)[r]
         assert torch.equal(L["wqkv"], torch.cat([q, k, v]))
-        assert torch.equal(L["w13"], torch.cat([L0["w13"][:F].chunk(2)[r], L0["w13"][F:].chunk(2)[r]]))
+        from k8s_llm_monitor_amd import ops
+
+        def canon(model, w):  # resident w13 is gate/up-interleaved per 128 rows when F allows
+            return ops.deinterleave_gate_up(w) if model._w13_il else w
+
+        w0 = canon(full, L0["w13"])
+        assert torch.equal(canon(m, L["w13"]), torch.cat([w0[:F].chunk(2)[r], w0[F:].chunk(2)[r]]))
         assert torch.equal(L["wo"], L0["wo"].chunk(2, dim=1)[r])
         assert torch.equal(m.embed, full.embed.chunk(2)[r])
 

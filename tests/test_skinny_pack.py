@@ -28,6 +28,31 @@ def test_interleave_gate_up():
     assert torch.equal(w[128:192, 0], torch.arange(64, 128, dtype=torch.float32))
 
 
+def test_deinterleave_and_interleaved_silu_mul():
+    """The single resident w13 is gate/up-interleaved: de-interleaving restores [gate; up], and
+    silu_mul over the interleaved GEMM output equals silu_mul over the canonical one."""
+    F, K = 192, 16
+    w = torch.randn(2 * F, K)
+    wi = ops.interleave_gate_up(w)
+    assert torch.equal(ops.deinterleave_gate_up(wi), w)
+    x = torch.randn(5, K)
+    y_can = ops.silu_mul(x @ w.t())
+    y_il = ops.silu_mul(x @ wi.t(), interleaved=True)
+    assert torch.allclose(y_can, y_il, atol=1e-6)
+
+
+def test_model_single_weight_copy_cpu():
+    """Row-major layout: the decode-path weight views ARE the prefill tensors (no second copy)."""
+    from k8s_llm_monitor_amd.models.config import get_config
+    from k8s_llm_monitor_amd.models.llama import CausalLM
+
+    m = CausalLM(get_config("llama-tiny"), device="cpu", dtype=torch.float32, seed=1)
+    if m.skinny_layout != "rowmajor":
+        pytest.skip("tiny config not eligible for the row-major skinny path")
+    L = m.layers[0]
+    assert L["wqkv_p"] is L["wqkv"] and L["wo_p"] is L["wo"] and L["w13_p"] is L["w13"] and L["w2_p"] is L["w2"]
+
+
 def test_skinny_splits_bounds(monkeypatch):
     monkeypatch.delenv("K8SLLM_SKINNY_SPLITS", raising=False)
     assert ops.skinny_splits(4096, 4096) == 4
