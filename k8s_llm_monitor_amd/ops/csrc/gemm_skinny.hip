@@ -423,6 +423,75 @@ __device__ __forceinline__ void wait_vmcnt() {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
 
+// Row-oriented combine + epilogue of the row-major kernel, all m-tiles in one round: every wave
+// parks its accumulators as rows of a padded [WAVES][MT*16][NT*16 + 4] fp32 image (conflict-free
+// ds_write_b32: the 4-float pad moves each 4-row lane group to its own 16 banks), one barrier,
+// then each thread sums 4 consecutive columns of one row over the waves (ds_read_b128, one
+// 256-B row per 16 lanes) and stores them whole: 16-B slab stores (a 64-column tile row = one
+// 256-B segment) and 8-B bf16 stores.  The ablation that motivated it (tools/abl_skinny_rm.py,
+// profiles/r02/skinny_rm_ablation.jsonl): at M = 64 the per-m-tile rounds with 4-byte slab
+// stores cost 2-3.5 us per projection.
+template <int MT, int NT, int EPI, int WAVES>
+__device__ __forceinline__ void skinny_epilogue_rows(const f32x4 (&acc)[MT][NT], float* red, const float* s_inv,
+                                                     float* __restrict__ partial, bf16_t* __restrict__ Y, long ldy,
+                                                     int M, int N, int ntile0, int s, int ex, const SkinnyGroup& grp) {
+  constexpr int LD = NT * 16 + 4, ROWS = MT * 16, NTH = 64 * WAVES;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * ROWS + mt * 16 + (lane >> 4) * 4 + r) * LD + nt * 16 + (lane & 15)] = acc[mt][nt][r];
+  __syncthreads();
+  auto sum4 = [&](int row, int c) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(red + row * LD + c);
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) v += *reinterpret_cast<const f32x4*>(red + (w * ROWS + row) * LD + c);
+    return v;
+  };
+  if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
+    // gate n-tiles (nt 0, 1) pair with up n-tiles (nt 2, 3): column j of the gate half with 32 + j
+    for (int it = threadIdx.x; it < ROWS * 8; it += NTH) {
+      const int row = it >> 3, j = (it & 7) * 4;
+      const float rs = s_inv != nullptr ? s_inv[row] : 1.f;
+      const f32x4 g4 = sum4(row, j) * rs, u4 = sum4(row, 32 + j) * rs;
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // the gate and up values are rounded to bf16 first, as the unfused GEMM -> silu_mul does
+        const float g = bf2f(f2bf(g4[q])), uu = bf2f(f2bf(u4[q]));
+        o[q] = g * uu / (1.f + __expf(-g));
+      }
+      const int f = (blockIdx.x >> 1) * 64 + (blockIdx.x & 1) * 32 + j;
+      if constexpr (EPI == EPI_SWIGLU_PACKED) {  // 4 consecutive f: contiguous in the packed layout
+        const int F = N >> 1;
+        *reinterpret_cast<uint2*>(Y + (((long)(row >> 4) * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 +
+                                       (row & 15)) * 8 + (f & 7)) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      } else if (row < M) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Y[(long)row * ldy + f + q] = f2bf(o[q]);
+      }
+    }
+  } else {
+    for (int it = threadIdx.x; it < ROWS * NT * 4; it += NTH) {
+      const int row = it / (NT * 4), c = (it % (NT * 4)) * 4;
+      if (row >= M) continue;
+      f32x4 v = sum4(row, c);
+      if (s_inv != nullptr) v *= s_inv[row];
+      if (grp.row_w != nullptr) v *= grp.row_w[(long)row * grp.row_w_ld + ex];
+      const int col = swiglu_tile<EPI, NT>(ntile0, c >> 4) * 16 + (c & 15);
+      if constexpr (EPI == EPI_BF16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Y[(long)row * ldy + col + q] = f2bf(v[q]);
+      } else {
+        *reinterpret_cast<f32x4*>(partial + ((long)(ex * gridDim.y + s) * M + row) * N + col) = v;
+      }
+    }
+  }
+}
+
 template <int MT, int NT, int EPI, int WAVES>
 struct SkinnyRmGeom {
   static constexpr int U = 2;                        // k-steps per stage: 64 k = one 128-B line per row
@@ -430,7 +499,8 @@ struct SkinnyRmGeom {
   static constexpr int AB = MT * U * 1024;           // A bytes per stage
   static constexpr int SB = WB + AB;
   static constexpr int RING = 2 * SB;                // per wave
-  static constexpr int RED = WAVES * NT * 64 * 16;   // cross-wave combine (aliases the rings)
+  static constexpr int LDR = NT * 16 + 4;            // combine row pitch (floats): conflict-free
+  static constexpr int RED = WAVES * MT * 16 * LDR * 4;  // cross-wave combine (aliases the rings)
   static constexpr int EPI_LDS = RED + MT * 16 * 4;  // + s_inv, written after the main loop
   static constexpr int LDS = WAVES * RING > EPI_LDS ? WAVES * RING : EPI_LDS;
   static constexpr int NLOAD = NT * 2 + MT * U;      // DMA instructions per stage
@@ -545,8 +615,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     ss += __shfl_xor(ss, 2, kWave);
     if ((threadIdx.x & 3) == 0) s_inv[threadIdx.x >> 2] = rsqrtf(ss * rn_inv_d + rn_eps);
   }
-  skinny_epilogue<MT, NT, EPI, WAVES>(acc, reinterpret_cast<float*>(smem), rn_ss != nullptr ? s_inv : nullptr,
-                                      partial, Y, ldy, M, N, ntile0, s, ex, grp);
+  skinny_epilogue_rows<MT, NT, EPI, WAVES>(acc, reinterpret_cast<float*>(smem), rn_ss != nullptr ? s_inv : nullptr,
+                                           partial, Y, ldy, M, N, ntile0, s, ex, grp);
   if constexpr (EPI == EPI_RESNORM || EPI == EPI_ROPE) skinny_fused_tail<MT, EPI, WAVES>(partial, Y, ldy, M, N, ep);
 }
 
