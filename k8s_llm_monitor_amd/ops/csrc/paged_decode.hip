@@ -25,14 +25,15 @@
 //    measured 2.3x slower at batch 64 x 1.8k context: every workgroup paid the L2 write-back).
 // Everything is static-shaped so the decode step can be captured in a hipGraph.
 #include "common.h"
+#include <stdlib.h>
 
 namespace k8sllm {
 
 constexpr int kBS = 16;   // tokens per KV-cache block
-constexpr int kCH = 256;  // tokens per chunk (4 waves x 64)
 
-__device__ __forceinline__ void split_range(int seq_len, int S, int split, int* c0, int* c1, int* nvalid) {
-  const int nch = (seq_len + kCH - 1) / kCH;
+// kch: tokens per chunk (4 waves x TW tokens)
+__device__ __forceinline__ void split_range(int seq_len, int S, int split, int kch, int* c0, int* c1, int* nvalid) {
+  const int nch = (seq_len + kch - 1) / kch;
   const int per = (nch + S - 1) / S;
   *c0 = split * per;
   *c1 = min(nch, *c0 + per);
@@ -56,8 +57,12 @@ struct DecodeFuse {
   bf16_t* v_cache;
 };
 
-template <int D, int G, bool FQ>
-__global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ out, long out_stride,
+// TW: tokens per wave per chunk.  TW = 32: two chunk buffers per wave (double-buffered loads,
+// ~240 VGPRs: 2 waves per SIMD) for grids that fill the chip (batch 64: 512 workgroups);
+// TW = 64: one buffer of 64 tokens (~120 VGPRs: up to 4 workgroups per CU) for small, split
+// grids, where residency, not the per-wave pipeline, hides the memory latency.
+template <int D, int G, bool FQ, int TW>
+__global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf16_t* __restrict__ out, long out_stride,
                                                            float* __restrict__ part_out,  // [B][Hq][S][D]
                                                            float* __restrict__ part_ml,   // [B][Hq][S][2]
                                                            const bf16_t* __restrict__ q, long q_stride,
@@ -82,7 +87,11 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
     return;
   }
   int c0, c1, nvalid;
-  split_range(seq_len, S, split, &c0, &c1, &nvalid);
+  constexpr int kTW = TW, kCH = 4 * TW;
+  constexpr int kNI = kTW / 16;  // 16-token K tiles (QK MFMAs) per wave and chunk
+  constexpr int kNS = kTW / 32;  // 32-token PV k-steps per wave and chunk
+  constexpr bool DB = TW == 32;  // double-buffered chunk loads
+  split_range(seq_len, S, split, kCH, &c0, &c1, &nvalid);
   if (c0 >= c1) return;  // uniform over the workgroup
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int col = lane & 15, kg = lane >> 4;
@@ -94,40 +103,48 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   const int n_cached = FQ ? seq_len - 1 : seq_len;
   const bool owns_new = FQ && c1 == (seq_len + kCH - 1) / kCH;
 
-  // ---- every K and V load of a wave's 64 tokens of chunk c, issued up front (32 KiB per wave)
-  bf16x8 kf[4][KS];
-  uint2 vlo[2][DT], vhi[2][DT];
-  auto issue = [&](int c) {
-    const int wtok0 = c * kCH + wave * 64;
-    int phys[4];
+  // ---- every K and V load of a wave's kTW tokens of chunk c, issued up front (16 KiB per wave),
+  // two chunk buffers per wave: chunk c + 1's loads fly while chunk c is multiplied (and the first
+  // two chunks' loads fly through the FQ prologue), so a wave never sits out a memory round trip
+  // between chunks.  (The single-buffered 64-token form measured 82 us per layer in the engine at
+  // batch 64, ctx ~1.7k, against 75 us in isolation: the prologue and each chunk's round trip
+  // were exposed.)
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  typedef bf16x8 KF[kNI][KS];
+  typedef u32x2_t VF[kNS][DT];  // ext vectors, not uint2 structs: SROA keeps them in registers
+  auto issue = [&](KF& kf, VF& vlo, VF& vhi, int c) {
+    const int wtok0 = c * kCH + wave * kTW;
+    int phys[kNI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kNI; ++i) {
       const int bi = (wtok0 >> 4) + i;
       phys[i] = bi < nblk ? bt[bi] : first_blk;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kNI; ++i) {
       const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         kf[i][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8));
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kNS; ++s) {
       const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
       const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-        const u32x2_t a2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(va + 16 * dt * kBS));
-        const u32x2_t b2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + 16 * dt * kBS));
-        vlo[s][dt] = make_uint2(a2.x, a2.y);
-        vhi[s][dt] = make_uint2(b2.x, b2.y);
+        vlo[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(va + 16 * dt * kBS));
+        vhi[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + 16 * dt * kBS));
       }
     }
   };
-  // the first chunk's K/V loads fly while q is loaded (FQ: reduced from the slabs and rotated)
-  issue(c0);
+  KF kf0, kf1;
+  VF vlo0, vhi0, vlo1, vhi1;
+  // the first chunks' K/V loads fly while q is loaded (FQ: reduced from the slabs and rotated)
+  issue(kf0, vlo0, vhi0, c0);
+  if constexpr (DB) {
+    if (c0 + 1 < c1) issue(kf1, vlo1, vhi1, c0 + 1);
+  }
 
   bf16x8 qf[KS];
   if constexpr (FQ) {
@@ -186,15 +203,13 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c = c0; c < c1; ++c) {
-    const int wtok0 = c * kCH + wave * 64;
-    if (c != c0) issue(c);  // chunk c0's loads were issued before the q prologue
-    __builtin_amdgcn_sched_barrier(0);  // keep every load above: none may wait behind an MFMA
+  auto compute = [&](const KF& kf, const VF& vlo, const VF& vhi, int c) {
+    const int wtok0 = c * kCH + wave * kTW;
 
     // ---- scores, online softmax (per lane: head `col`)
-    f32x4 sacc[4];
+    f32x4 sacc[kNI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kNI; ++i) {
       sacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -202,7 +217,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kNI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = wtok0 + 16 * i + 4 * kg + r;
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
     const float alpha = exp2f(m - mnew);
     float ls = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kNI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = exp2f(sacc[i][r] - mnew);
@@ -231,7 +246,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kNS; ++s) {
       bf16x8 pb;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -241,9 +256,26 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16x8 a =
-            __builtin_bit_cast(bf16x8, make_uint4(vlo[s][dt].x, vlo[s][dt].y, vhi[s][dt].x, vhi[s][dt].y));
+            __builtin_bit_cast(bf16x8, make_uint4(vlo[s][dt][0], vlo[s][dt][1], vhi[s][dt][0], vhi[s][dt][1]));
         oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[dt], 0, 0, 0);
       }
+    }
+  };
+  if constexpr (DB) {
+    for (int c = c0; c < c1; c += 2) {
+      compute(kf0, vlo0, vhi0, c);
+      if (c + 2 < c1) issue(kf0, vlo0, vhi0, c + 2);
+      __builtin_amdgcn_sched_barrier(0);  // chunk c + 2's loads go out before chunk c + 1's MFMAs
+      if (c + 1 >= c1) break;
+      compute(kf1, vlo1, vhi1, c + 1);
+      if (c + 3 < c1) issue(kf1, vlo1, vhi1, c + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    for (int c = c0; c < c1; ++c) {
+      if (c != c0) issue(kf0, vlo0, vhi0, c);  // chunk c0's loads were issued before the q prologue
+      __builtin_amdgcn_sched_barrier(0);  // keep every load above: none may wait behind an MFMA
+      compute(kf0, vlo0, vhi0, c);
     }
   }
 
@@ -312,13 +344,14 @@ template <int D, int G>
 __global__ __launch_bounds__(256) void paged_decode_reduce_kernel(bf16_t* __restrict__ out, long out_stride,
                                                                   const float* __restrict__ part_out,
                                                                   const float* __restrict__ part_ml,
-                                                                  const int* __restrict__ seq_lens, int Hq, int S) {
+                                                                  const int* __restrict__ seq_lens, int Hq, int S,
+                                                                  int kch) {
   __shared__ float s_w[G][64];
   const int kvh = blockIdx.x, b = blockIdx.y;
   const int seq_len = seq_lens[b];
   if (seq_len <= 0) return;
   int c0, c1, nvalid;
-  split_range(seq_len, S, 0, &c0, &c1, &nvalid);
+  split_range(seq_len, S, 0, kch, &c0, &c1, &nvalid);
   if (nvalid <= 1) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int h = wave; h < G; h += 4) {
@@ -362,6 +395,15 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
                                          const int* block_tables, int bt_stride, const int* seq_lens, int B, int Hq,
                                          int Hkv, int D, int S, float scale, hipStream_t s);
 
+// Tokens per wave per chunk: the double-buffered 32-token form once the grid fills the chip
+// (>= 384 workgroups, e.g. batch 64 x 8 kv heads), else the single-buffered 64-token form (small
+// batches, split grids: higher residency).  K8SLLM_DECODE_TW = 32 / 64 forces one.
+static int decode_tw(int S, int Hkv, int B) {
+  static const int forced = getenv("K8SLLM_DECODE_TW") ? atoi(getenv("K8SLLM_DECODE_TW")) : 0;
+  if (forced == 32 || forced == 64) return forced;
+  return (long)S * Hkv * B >= 384 ? 32 : 64;
+}
+
 extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q,
                                    long q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                                    int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int S,
@@ -371,14 +413,17 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
   const int G = Hq / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
   const DecodeFuse fz{};
+  const int tw = decode_tw(S, Hkv, B);
   dim3 grid(S, Hkv, B), blk(256);
-#define K8S_DEC(DD, GG)                                                                                              \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, false>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out,      \
+#define K8S_DEC_T(DD, GG, TWV)                                                                                       \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, GG, false, TWV>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, \
                      part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,            \
-                     block_tables, bt_stride, seq_lens, Hq, Hkv, S, sl2, fz);                                        \
+                     block_tables, bt_stride, seq_lens, Hq, Hkv, S, sl2, fz)
+#define K8S_DEC(DD, GG)                                                                                              \
+  if (tw == 32) K8S_DEC_T(DD, GG, 32); else K8S_DEC_T(DD, GG, 64);                                                  \
   if (S > 1)                                                                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,      \
-                       part_out, part_ml, seq_lens, Hq, S);
+                       part_out, part_ml, seq_lens, Hq, S, 4 * tw);
   if (D == 128) {
     switch (G) {
       case 1: K8S_DEC(128, 1); break;
@@ -400,6 +445,7 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
     return -1;
   }
 #undef K8S_DEC
+#undef K8S_DEC_T
   return (int)hipGetLastError();
 }
 
@@ -414,14 +460,17 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
   const int G = Hq / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
   const DecodeFuse fz{slabs, nslabs, positions, cos_sin, slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache};
+  const int tw = decode_tw(S, Hkv, B);
   dim3 grid(S, Hkv, B), blk(256);
-#define K8S_DECF(GG)                                                                                                 \
-  hipLaunchKernelGGL((paged_decode_kernel<128, GG, true>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out,      \
+#define K8S_DECF_T(GG, TWV)                                                                                          \
+  hipLaunchKernelGGL((paged_decode_kernel<128, GG, true, TWV>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, \
                      part_ml, nullptr, 0, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride,   \
-                     seq_lens, Hq, Hkv, S, sl2, fz);                                                                 \
+                     seq_lens, Hq, Hkv, S, sl2, fz)
+#define K8S_DECF(GG)                                                                                                 \
+  if (tw == 32) K8S_DECF_T(GG, 32); else K8S_DECF_T(GG, 64);                                                        \
   if (S > 1)                                                                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<128, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,     \
-                       part_out, part_ml, seq_lens, Hq, S);
+                       part_out, part_ml, seq_lens, Hq, S, 4 * tw);
   switch (G) {
     case 1: K8S_DECF(1); break;
     case 2: K8S_DECF(2); break;
@@ -430,5 +479,6 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
     default: return -1;
   }
 #undef K8S_DECF
+#undef K8S_DECF_T
   return (int)hipGetLastError();
 }
