@@ -60,6 +60,15 @@ __device__ __forceinline__ long act_index(int row, int col, long stride) {
   return (((long)(row >> 4) * (-stride) + (col >> 5)) * 64 + ((col >> 3) & 3) * 16 + (row & 15)) * 8 + (col & 7);
 }
 
+// V-cache token order inside each 16-token block (v_cache [NB][Hkv][D][BS], a dim's 16 tokens
+// in 32 contiguous bytes): token t sits at position v_perm(t), an involution that swaps bits 2
+// and 3 - tokens 0-3, 8-11 fill the first 16-byte chunk of a dim row, 4-7, 12-15 the second.  That
+// is exactly the k order of a v_mfma_f32_32x32x16_bf16 operand that sums over the row index of a
+// 32x32 accumulator (lane half h, element j <-> row 8(j>>2) + 4h + (j&3); cdna_hip_programming.md
+// §3): flash prefill's PV A-fragment is one ds_read_b128 of a cache block staged verbatim by
+// LDS-DMA.  Paged decode reads 4-token groups, which v_perm keeps contiguous.
+__device__ __forceinline__ int v_perm(int t) { return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

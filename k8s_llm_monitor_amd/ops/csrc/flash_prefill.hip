@@ -17,10 +17,18 @@
 // causal offsets differ: keys of the new tokens stage from the qkv rows exactly as in the plain
 // kernel; only cached keys (position < ctx_start) are read from the paged cache.
 #include "common.h"
+#include <stdlib.h>
 
 namespace k8sllm {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_fp() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 template <int D, bool PAGED>
 __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restrict__ out, long out_stride,
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
         } else if (kr < cst) {
           const long blk = bt[kr >> 4];
           kv = *reinterpret_cast<const uint4*>(k_cache + (((blk * Hkv + kvh) * CH + ch) * 16 + (kr & 15)) * 8);
-          const bf16_t* vp = v_cache + ((blk * Hkv + kvh) * D + ch * 8) * 16 + (kr & 15);
+          const bf16_t* vp = v_cache + ((blk * Hkv + kvh) * D + ch * 8) * 16 + v_perm(kr & 15);
           uint32_t w[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) w[j] = (uint32_t)vp[(2 * j) * 16] | ((uint32_t)vp[(2 * j + 1) * 16] << 16);
@@ -239,6 +247,225 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Paged prefill v2: every key / value tile is staged VERBATIM from the paged cache by LDS-DMA
+// (rope_and_cache has already written the new tokens), shared by all G query heads of a kv head.
+//
+//  * workgroup = one kv head x QR = 256 / G query rows x all G heads: 8 waves, each 32 rows of
+//    one head (G = 4: 64 rows; grid z splits the host's 128-row q-blocks).  One 64-key tile
+//    (4 cache blocks: K 16 KiB + V 16 KiB) feeds 8 waves instead of 4: half the staging per MFMA
+//    of the v1 kernel (one head per workgroup), and no staging registers: 4 global_load_lds_dwordx4
+//    per wave per tile.
+//  * four-slot LDS ring (128 KiB), ONE barrier per tile, two tiles in flight across it (counted
+//    vmcnt; cdna_hip_programming.md §5 "Pipelining across barriers": raw s_barrier, never
+//    __syncthreads with a DMA in flight); see the pipeline comment at the main loop.
+//  * fragments: K as cached ([piece of 8 dims][16 tokens][8]) is read lane-linear per 16 tokens -
+//    conflict-free ds_read_b128; V as cached ([dim][16 tokens], v_perm token order, common.h) gives
+//    the PV A-operand of a 32x32x16 MFMA in one ds_read_b128 per lane, the dim row's two 16-B
+//    chunks XOR-swapped by bit 3 of the dim (applied to the DMA source address) so the 16 lanes of
+//    a read group hit 16 distinct bank quads.  v1 gathered the cached V with 2-byte loads.
+//  * products as v1: S^T = K Q^T (A = K, B = Q^T from registers), O^T += V^T P^T (B = the score
+//    accumulator converted in place), online softmax lane-local (query = lane).
+//  * heads are remapped nowhere: blockIdx.x = kv head, so all workgroups of one kv head share an
+//    XCD (dispatch round-robin over 8 XCDs) and its L2 serves the head's K/V to every q-block.
+template <int G>
+__global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
+    bf16_t* __restrict__ out, long out_stride, const bf16_t* __restrict__ qkv, long qkv_stride,
+    const int* __restrict__ cu_seqlens, const int* __restrict__ qb_seq, const int* __restrict__ qb_start, int Hq,
+    int Hkv, float scale_log2, const int* __restrict__ ctx_start, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride) {
+  constexpr int D = 128, KS = D / 16, DT = D / 32;
+  constexpr int WPH = 8 / G;      // waves per head
+  constexpr int QR = 32 * WPH;    // query rows per workgroup
+  constexpr int TILE = 32768;     // K (16 KiB) + V (16 KiB) of 64 keys
+  constexpr int NBUF = 4;
+  constexpr int MAXB = 2048;      // block ids per sequence staged in LDS (32k tokens)
+  __shared__ __attribute__((aligned(16))) char fp2_smem[NBUF * TILE + MAXB * 4];  // ring + block ids
+  int* s_blk = reinterpret_cast<int*>(fp2_smem + NBUF * TILE);
+
+  const int kvh = blockIdx.x, qb = blockIdx.y;
+  const int seq = qb_seq[qb];
+  const int qs = qb_start[qb] + blockIdx.z * QR;  // first query row (new-token index) of the workgroup
+  const int s0 = cu_seqlens[seq];
+  const int L = cu_seqlens[seq + 1] - s0;
+  if (qs >= L) return;  // uniform: the last q-block's upper part
+  const int cst = ctx_start[seq];
+  const int LK = cst + L;
+  const int nblk = (LK + 15) / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wave / WPH, sub = wave % WPH;
+  const int hq = kvh * G + g;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int myq = qs + sub * 32 + r32;
+  const int wave_q0 = cst + qs + sub * 32;  // absolute position of the wave's first query
+  const int kv_end = min(LK, cst + qs + QR);
+  const int ntiles = (kv_end + 63) >> 6;
+
+  // the sequence's block ids (the tiles' DMA sources) and this wave's q fragments, loaded with
+  // plain loads and retired before the first DMA: no register load is outstanding beside one
+  const int* bt = block_tables + (long)seq * bt_stride;
+  for (int i = tid; i < ntiles * 4; i += 512) s_blk[i] = i < nblk ? bt[i] : bt[0];
+  bf16x8 qf[KS];
+  {
+    const int qrow = min(myq, L - 1);
+    const bf16_t* qp = qkv + (long)(s0 + qrow) * qkv_stride + hq * D + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+  // consume q here, so the compiler's own wait for these loads sits before the loop; otherwise
+  // hipcc re-waits vmcnt(0) at the first MFMA of EVERY tile, draining the DMAs in flight
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[ks]));
+  __syncthreads();
+
+  // 32 x 1 KiB DMA pieces per tile: wave w issues pieces 4w .. 4w + 3 (waves 0-3 K, 4-7 V)
+  const int kind = wave >> 2, bsel = wave & 3;
+  const bf16_t* cache = kind ? v_cache : k_cache;
+  int src_chunk[4];
+#pragma unroll
+  for (int part = 0; part < 4; ++part) {
+    const int c = part * 64 + lane;  // 16-B chunk of the 4 KiB block image, in LDS order
+    src_chunk[part] = kind ? (((c >> 1) << 1) | ((c & 1) ^ ((c >> 4) & 1))) : c;  // V: dim = c >> 1
+  }
+  auto issue = [&](int t, int buf) {
+    const long phys = s_blk[t * 4 + bsel];
+    const bf16_t* base = cache + (phys * Hkv + kvh) * (D * 16);
+    char* dst = fp2_smem + buf * TILE + kind * 16384 + bsel * 4096;
+#pragma unroll
+    for (int part = 0; part < 4; ++part)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + src_chunk[part] * 8), (lds_void_t*)(dst + part * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  // QK of one tile: S^T[64 keys][32 queries] as two 32-key accumulators
+  auto qk = [&](int t, f32x16 (&sa)[2]) {
+    const char* kt = fp2_smem + (t % NBUF) * TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sa[i][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // key 32 i + r32: block 2 i + (r32 >> 4), token r32 & 15; dims 16 ks + 8 hh = piece 2 ks + hh
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(
+            kt + (2 * i + (r32 >> 4)) * 4096 + ((2 * ks + hh) * 16 + (r32 & 15)) * 16);
+        sa[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sa[i], 0, 0, 0);
+      }
+  };
+  // causal / end-of-sequence mask of one tile's scores: only the diagonal tile and the
+  // sequence's last tile - a uniform scalar branch, kept OUT of the compute block below
+  auto mask = [&](int t, f32x16 (&sa)[2]) {
+    const int k0 = t * 64;
+    if (__builtin_amdgcn_readfirstlane((k0 + 63 > wave_q0) || (k0 + 64 > LK))) {
+      const int lim = min(cst + myq, LK - 1) - k0 - 4 * hh;  // last visible key, relative
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (32 * i + (r & 3) + 8 * (r >> 2) > lim) sa[i][r] = -1e30f;
+    }
+  };
+  // online softmax of one tile's scores (in place -> probabilities), then O += V^T P^T
+  auto softmax_pv = [&](int t, f32x16 (&sa)[2]) {
+    float mx = sa[0][0];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[i][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx * scale_log2);
+    const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i][r], scale_log2, -mnew));
+        sa[i][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    const bool grew = __builtin_amdgcn_ballot_w64(mnew > m) != 0;  // lazy rescale: O only when a max moved
+    m = mnew;
+    if (grew) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    const char* vt = fp2_smem + (t % NBUF) * TILE + 16384;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sa[i][8 * s + j];
+        const char* vb = vt + (2 * i + s) * 4096;  // block 2 i + s: keys 32 i + 16 s ..
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int d = 32 * dt + r32;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(vb + (d * 2 + (hh ^ ((d >> 3) & 1))) * 16);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[dt], 0, 0, 0);
+        }
+      }
+  };
+
+  // Main loop: ONE barrier per tile; tiles t + 1 and t + 2 are in flight while tile t is
+  // computed (4-slot ring).  At tile t's barrier every wave has finished tile t - 1, whose slot
+  // (t + 3) % 4 is refilled right after it.  (A software-pipelined variant that put tile t + 1's
+  // QK beside tile t's softmax measured no faster and spilled once the two phases shared a
+  // basic block.)  The wave computes only its first nt_w tiles (later ones are in the future of
+  // all its rows) but joins every barrier and issues its DMA pieces for every tile.
+  const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD"
+  // item 4): waves w and w + 4 share a SIMD, and the younger half loses every arbitration
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
+  if (ntiles > 2) issue(2, 2);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 2 < ntiles)
+      wait_vmcnt_fp<8>();  // this wave's pieces of tile t landed; t + 1, t + 2 may still fly
+    else if (t + 1 < ntiles)
+      wait_vmcnt_fp<4>();
+    else
+      wait_vmcnt_fp<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t landed; tile t - 1 reads done
+    if (t + 3 < ntiles) issue(t + 3, (t + 3) % NBUF);
+    if (t >= nt_w) continue;
+    f32x16 sa[2];
+    qk(t, sa);
+    mask(t, sa);
+    softmax_pv(t, sa);
+  }
+
+  if (myq < L) {
+    const float inv = 1.f / l;
+    bf16_t* op = out + (long)(s0 + myq) * out_stride + (long)hq * D + 4 * hh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 v;
+        v.x = pack2(o[dt][4 * k] * inv, o[dt][4 * k + 1] * inv);
+        v.y = pack2(o[dt][4 * k + 2] * inv, o[dt][4 * k + 3] * inv);
+        *reinterpret_cast<uint2*>(op + 32 * dt + 8 * k) = v;
+      }
+  }
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
@@ -250,6 +477,24 @@ extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv,
   if (n_qblocks <= 0) return 0;
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
+  const int G = Hq / Hkv;
+  const bool v1_only = getenv("K8SLLM_PREFILL_V1") != nullptr && atoi(getenv("K8SLLM_PREFILL_V1")) == 1;
+  // bt_stride = the block-table width = most blocks a sequence can hold: <= 2048 - 3 fit the LDS copy
+  if (ctx_start != nullptr && !v1_only && (G == 2 || G == 4 || G == 8) && bt_stride <= 2045) {
+    // v2: q-blocks of 128 rows split into 128 / QR workgroups (QR = 256 / G rows each)
+    const int z = 128 / (256 / G);
+#define K8S_FP2(GG)                                                                                                 \
+  hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG>), dim3(Hkv, n_qblocks, z), dim3(512), 0, s, (bf16_t*)out,   \
+                     out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,       \
+                     ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride)
+    switch (G) {
+      case 2: K8S_FP2(2); break;
+      case 4: K8S_FP2(4); break;
+      default: K8S_FP2(8); break;
+    }
+#undef K8S_FP2
+    return (int)hipGetLastError();
+  }
   if (ctx_start != nullptr) {
     hipLaunchKernelGGL((flash_prefill_kernel<128, true>), dim3(Hq, n_qblocks), dim3(256), 0, s, (bf16_t*)out,
                        out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,

@@ -204,7 +204,7 @@ __device__ __forceinline__ void skinny_fused_tail(const float* __restrict__ part
           *reinterpret_cast<uint2*>(kb + ((p >> 3) * bs + off) * 8 + (p & 7)) = lo;
           *reinterpret_cast<uint2*>(kb + (((p + 64) >> 3) * bs + off) * 8 + (p & 7)) = hi;
         } else {  // value: V^T per block, [dim][token]
-          bf16_t* vb = ep.v_cache + ((long)blk * ep.Hkv + (h - ep.Hq - ep.Hkv)) * (128 * bs) + off;
+          bf16_t* vb = ep.v_cache + ((long)blk * ep.Hkv + (h - ep.Hq - ep.Hkv)) * (128 * bs) + v_perm(off);
           const uint32_t w[4] = {lo.x, lo.y, hi.x, hi.y};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {

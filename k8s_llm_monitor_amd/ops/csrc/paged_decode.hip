@@ -129,8 +129,9 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
     }
 #pragma unroll
     for (int s = 0; s < kNS; ++s) {
-      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
-      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + 4 * kg + col * kBS;
+      // tokens 4kg .. 4kg + 3 of each block: contiguous at position v_perm(4kg) (common.h)
+      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + v_perm(4 * kg) + col * kBS;
+      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + v_perm(4 * kg) + col * kBS;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         vlo[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(va + 16 * dt * kBS));
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
     if (owns_new && slot >= 0 && threadIdx.x < D) {  // the new token's k / v for the next steps
       const int blk = slot / kBS, off = slot - blk * kBS, d = threadIdx.x;
       fz.k_cache[(((long)blk * Hkv + kvh) * (D / 8) + (d >> 3)) * (kBS * 8) + off * 8 + (d & 7)] = s_kv[0][d];
-      fz.v_cache[(((long)blk * Hkv + kvh) * D + d) * kBS + off] = s_kv[1][d];
+      fz.v_cache[(((long)blk * Hkv + kvh) * D + d) * kBS + v_perm(off)] = s_kv[1][d];
     }
   } else {
     const int hc = col < G ? col : 0;

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(128) void rope_cache_kernel(bf16_t* __restrict__ qk
       const uint4 v = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + vh) * D + c);
       wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
     }
-    bf16_t* vb = v_cache + ((long)blk * Hkv + vh) * (D * block_size) + off;
+    bf16_t* vb = v_cache + ((long)blk * Hkv + vh) * (D * block_size) + v_perm(off);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       vb[(long)(c + 2 * j) * block_size] = (bf16_t)(wv[j] & 0xffff);
@@ -167,18 +167,21 @@ __global__ __launch_bounds__(256) void kv_cache_write_kernel(const bf16_t* __res
                                     reinterpret_cast<u32x4_t*>(kb + ((long)c * BS + off0 + j) * 8));
       }
     }
-    bf16_t* vb = v_cache + (blk * Hkv + h) * (long)(D * BS);  // [D][BS]
+    bf16_t* vb = v_cache + (blk * Hkv + h) * (long)(D * BS);  // [D][BS], tokens in v_perm order
     for (int e = tid; e < D * 2; e += 256) {
-      const int d = e >> 1, o0 = (e & 1) * 8;  // block offsets o0 .. o0 + 7 of dim d
-      if (off0 + len <= o0 || off0 >= o0 + 8) continue;
+      const int d = e >> 1, o0 = (e & 1) * 8;  // block positions o0 .. o0 + 7 of dim d
       bf16_t v[8];
+      int have = 0;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int j = o0 + q - off0;
-        v[q] = (j >= 0 && j < len) ? qkv[(long)(ts + j) * qkv_stride + voff + d] : (bf16_t)0;
+        const int j = v_perm(o0 + q) - off0;  // token of this position, relative to the run
+        const bool in = j >= 0 && j < len;
+        have += in;
+        v[q] = in ? qkv[(long)(ts + j) * qkv_stride + voff + d] : (bf16_t)0;
       }
+      if (have == 0) continue;
       bf16_t* dst = vb + (long)d * BS + o0;
-      if (off0 <= o0 && off0 + len >= o0 + 8) {
+      if (have == 8) {
         typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
         u32x4_t w;
         w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(256) void kv_cache_write_kernel(const bf16_t* __res
       } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int j = o0 + q - off0;
+          const int j = v_perm(o0 + q) - off0;
           if (j >= 0 && j < len) dst[q] = v[q];
         }
       }

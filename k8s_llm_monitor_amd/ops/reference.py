@@ -5,7 +5,7 @@ are the execution path for CPU tensors (unit tests, the GPT-2 CPU plumbing confi
 KV-cache layouts (see ``csrc/rope_cache.hip``):
 
 * ``k_cache`` ``[num_blocks, Hkv, D // 8, block_size, 8]``
-* ``v_cache`` ``[num_blocks, Hkv, D, block_size]``
+* ``v_cache`` ``[num_blocks, Hkv, D, block_size]``, each block's tokens at positions ``v_perm(t)``
 """
 from __future__ import annotations
 
@@ -98,6 +98,11 @@ def rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, Hq, 
         write_kv_cache(k, v, k_cache, v_cache, slot_mapping)
 
 
+def v_perm(t):
+    """V-cache position of block token t (common.h v_perm): bits 2 and 3 swapped, an involution."""
+    return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1)
+
+
 def write_kv_cache(k, v, k_cache, v_cache, slot_mapping):
     bs = k_cache.shape[3]
     D = v_cache.shape[2]
@@ -107,7 +112,7 @@ def write_kv_cache(k, v, k_cache, v_cache, slot_mapping):
     blk, off = sm // bs, sm % bs
     kk = k.view(k.shape[0], k.shape[1], D // 8, 8)
     k_cache[blk, :, :, off, :] = kk
-    v_cache[blk, :, :, off] = v
+    v_cache[blk, :, :, v_perm(off)] = v
 
 
 def gather_kv(k_cache, v_cache, block_table: torch.Tensor, seq_len: int):
@@ -118,7 +123,8 @@ def gather_kv(k_cache, v_cache, block_table: torch.Tensor, seq_len: int):
     kb = k_cache[blocks]  # [nb, Hkv, D/8, bs, 8]
     nbk, hkv, p, _, _ = kb.shape
     k = kb.permute(0, 3, 1, 2, 4).reshape(nbk * bs, hkv, p * 8)[:seq_len]
-    vb = v_cache[blocks]  # [nb, Hkv, D, bs]
+    vb = v_cache[blocks]  # [nb, Hkv, D, bs], tokens at positions v_perm(t)
+    vb = vb[..., v_perm(torch.arange(bs, device=vb.device))]
     v = vb.permute(0, 3, 1, 2).reshape(nbk * bs, hkv, -1)[:seq_len]
     return k, v
 

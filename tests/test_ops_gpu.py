@@ -465,6 +465,58 @@ def test_gemm_skinny_wide_variant(M, monkeypatch):
     _close(ops.unpack_skinny(actp)[:M].cpu(), ref.silu_mul(gu), atol=3e-2, rtol=2e-2, what="wide swiglu")
 
 
+def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):
+    S = len(new)
+    tot = [c + n for c, n in zip(cached, new)]
+    nblk = [(t + bs - 1) // bs for t in tot]
+    NB = sum(nblk) + 3
+    kc = torch.randn(NB, hkv, D // 8, bs, 8, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(NB, hkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    perm = torch.randperm(NB, device=DEV).to(torch.int32)
+    W = max(nblk) + 5  # wider than needed, as an engine block table is
+    bt = torch.zeros(S, W, dtype=torch.int32, device=DEV)
+    o = 0
+    for i, n in enumerate(nblk):
+        bt[i, :n] = perm[o:o + n]
+        o += n
+    T = sum(new)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16)
+    if spike:  # one query row against one key row: the running max jumps late in the sequence
+        qkv[T - 1, :D] = 8.0
+        qkv[T - 3, (hq) * D:(hq) * D + D] = 8.0
+    cu = torch.tensor([0] + list(torch.tensor(new).cumsum(0).tolist()), dtype=torch.int32, device=DEV)
+    cs = torch.tensor(cached, dtype=torch.int32, device=DEV)
+    pos = torch.cat([torch.arange(c, c + n) for c, n in zip(cached, new)]).to(DEV, torch.int32)
+    seq_of = torch.cat([torch.full((n,), i) for i, n in enumerate(new)]).to(DEV)
+    slots = (bt[seq_of, (pos // bs).long()] * bs + pos % bs).to(torch.int32)
+    ops.rope_and_cache(qkv, pos, torch.zeros(1, D, device=DEV), kc, vc, slots, hq, hkv, D, apply_rope=False)
+    return qkv, cu, cs, kc, vc, bt
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 8), (64, 8)])
+@pytest.mark.parametrize("cached,new", [([0, 0, 0], [1609, 7, 300]), ([48, 160, 1023], [1, 130, 129]), ([5000], [64])])
+def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new, monkeypatch):
+    """The LDS-DMA paged prefill kernel (v2: tiles staged verbatim from the cache, GQA-shared) ==
+    the fp32 reference and == the v1 kernel, for G = 2, 4, 8 and cached prefixes."""
+    D = 128
+    qkv, cu, cs, kc, vc, bt = _paged_prefill_case(cached, new, hq, hkv, D)
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
+    _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what=f"paged prefill v2 G={hq // hkv}")
+    monkeypatch.setenv("K8SLLM_PREFILL_V1", "1")
+    out1 = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    _close(out.cpu(), out1.cpu(), atol=2e-2, rtol=2e-2, what="v2 vs v1")
+
+
+def test_flash_prefill_paged_v2_softmax_spike():
+    """A late running-max jump (forced by one spiked q/k pair) is rescaled correctly."""
+    hq, hkv, D = 32, 8, 128
+    qkv, cu, cs, kc, vc, bt = _paged_prefill_case([100], [700], hq, hkv, D, spike=True)
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
+    _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what="paged prefill v2 spike")
+
+
 @pytest.mark.parametrize("cached,new", [([0, 32], [40, 7]), ([48, 160, 16], [1, 130, 64]), ([1008], [300])])
 def test_flash_prefill_paged(cached, new):
     """Prefill of new tokens attending a cached prefix in the paged cache == the fp32 reference."""

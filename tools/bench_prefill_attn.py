@@ -23,6 +23,7 @@ def main() -> None:
     ap.add_argument("--seqs", type=int, default=10)
     ap.add_argument("--len", type=int, default=1609)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", choices=["all", "v1", "v2"], default="all", help="paged kernel(s) to time (PMC runs)")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     T = a.seqs * a.len
@@ -31,18 +32,53 @@ def main() -> None:
     qs, st = ops.prefill_qblocks(cu.tolist())
     qb = (torch.tensor(qs, dtype=torch.int32, device="cuda"), torch.tensor(st, dtype=torch.int32, device="cuda"))
     out = torch.empty(T, Hq * D, device="cuda", dtype=torch.bfloat16)
-    for _ in range(3):
-        ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out)
-    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.iters):
-        ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out)
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / a.iters * 1e3
     flops = 4 * D * Hq * a.seqs * a.len * a.len / 2
-    print(json.dumps({"seqs": a.seqs, "len": a.len, "us": round(us, 1), "PFps": round(flops / us / 1e9, 3)}))
+    if a.only == "all":
+        for _ in range(3):
+            ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.iters):
+            ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        print(json.dumps({"seqs": a.seqs, "len": a.len, "kernel": "plain", "us": round(us, 1),
+                          "PFps": round(flops / us / 1e9, 3)}))
+    # paged (the engine's path): keys / values from a block-permuted cache, v1 vs v2 interleaved
+    bs = 16
+    nb = a.seqs * ((a.len + bs - 1) // bs)
+    kc = torch.zeros(nb + 4, Hkv, D // 8, bs, 8, device="cuda", dtype=torch.bfloat16)
+    vc = torch.zeros(nb + 4, Hkv, D, bs, device="cuda", dtype=torch.bfloat16)
+    per = (a.len + bs - 1) // bs
+    bt = torch.randperm(nb, device="cuda").to(torch.int32).view(a.seqs, per)
+    bt = torch.cat([bt, torch.zeros(a.seqs, 8, dtype=torch.int32, device="cuda")], 1).contiguous()
+    pos = torch.arange(a.len, device="cuda").repeat(a.seqs).to(torch.int32)
+    seq_of = torch.arange(a.seqs, device="cuda").repeat_interleave(a.len)
+    slots = (bt[seq_of, (pos // bs).long()] * bs + pos % bs).to(torch.int32)
+    ops.rope_and_cache(qkv, pos, torch.zeros(1, D, device="cuda"), kc, vc, slots, Hq, Hkv, D, apply_rope=False)
+    cst = torch.zeros(a.seqs, dtype=torch.int32, device="cuda")
+    res: dict = {}
+    for _ in range(3):
+        for tag, v1 in (("paged_v1", "1"), ("paged_v2", "0")):
+            if a.only != "all" and not tag.endswith(a.only):
+                continue
+            os.environ["K8SLLM_PREFILL_V1"] = v1
+            for _ in range(3):
+                ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out, paged=(cst, kc, vc, bt))
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.iters):
+                ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out, paged=(cst, kc, vc, bt))
+            e1.record()
+            torch.cuda.synchronize()
+            res.setdefault(tag, []).append(e0.elapsed_time(e1) / a.iters * 1e3)
+    os.environ.pop("K8SLLM_PREFILL_V1", None)
+    for tag, ts in res.items():
+        us = min(ts)
+        print(json.dumps({"seqs": a.seqs, "len": a.len, "kernel": tag, "us": round(us, 1),
+                          "PFps": round(flops / us / 1e9, 3)}))
 
 
 if __name__ == "__main__":
