@@ -100,6 +100,14 @@ class CausalLM:
                 raise ValueError("n_experts must be divisible by tp for expert parallelism")
             self.e_lo, self.e_hi = shard_range(cfg.n_experts, tp, r)
         self.moe_comm = os.environ.get("K8SLLM_MOE_COMM", "a2a")  # "a2a" (prefill all-to-all EP) | "allreduce"
+        # MoE prefill GEMMs: "grouped" = one launch per projection over all local experts
+        # (moe_gemm.hip, zero host syncs); "loop" = one hipBLASLt GEMM per expert after a host
+        # sync of the expert offsets
+        self._moe_grouped = os.environ.get("K8SLLM_MOE_PREFILL", "loop") == "grouped"
+        # MoE decode at TP>1: "allreduce" = every rank runs its experts on every (replicated)
+        # token, dense-masked, then one all-reduce; "a2a" = expert-parallel dispatch / combine with
+        # static-capacity all-to-alls (_moe_a2a_decode, graph-capturable)
+        self.moe_decode = os.environ.get("K8SLLM_MOE_DECODE", "allreduce")
         self.layers: list[dict] = []
         self._w13_il = False  # w13 gate/up-interleaved per 128 rows (set by _init_skinny)
         self.skinny_layout = None
@@ -295,6 +303,8 @@ class CausalLM:
         if c.is_moe:
             if meta.is_prefill and self.tp > 1 and self.moe_comm == "a2a":
                 return self._moe_a2a(L, x)
+            if not meta.is_prefill and self.tp > 1 and self.moe_decode == "a2a":
+                return self._moe_a2a_decode(L, x)
             return tp_all_reduce(self._moe(L, x, meta), self.ps)
         h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=self._w13_il)
         return tp_all_reduce(F.linear(h, L["w2"]), self.ps)
@@ -320,8 +330,19 @@ class CausalLM:
             return out.to(x.dtype)
         offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
         xs = ops.gather_rows(x, sorted_idx, K)
+        if self._moe_grouped and x.is_cuda:
+            # every local expert in ONE grouped launch per projection, driven by the device-side
+            # offsets (ops/csrc/moe_gemm.hip): no host sync, no per-expert loop
+            offl = offsets[self.e_lo:self.e_hi + 1]
+            part = self.tp > 1  # other ranks' experts' rows stay zero
+            if self._w13_il:
+                h = ops.moe_grouped_gemm(xs, L["w13"], offl, swiglu=True, zero_fill=part)
+            else:
+                h = ops.silu_mul(ops.moe_grouped_gemm(xs, L["w13"], offl, zero_fill=part))
+            ys = ops.moe_grouped_gemm(h, L["w2"], offl, zero_fill=part)
+            return ops.moe_combine(ys, inv_idx, w, T)
         ys = torch.zeros_like(xs)
-        off = offsets.tolist()  # one host sync per MoE layer in prefill
+        off = offsets.tolist()  # one host sync per MoE layer (the per-expert hipBLASLt loop)
         for j, e in enumerate(range(self.e_lo, self.e_hi)):
             a, b = off[e], off[e + 1]
             if b > a:
@@ -373,6 +394,49 @@ class CausalLM:
         if n < chunk:  # equal-size blocks for the all-gather
             out = torch.cat([out, out.new_zeros(chunk - n, c.d_model)])
         return tp_all_gather_rows(out, self.ps)[:T]
+
+    def _moe_a2a_decode(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+        """Expert-parallel MoE for DECODE steps with static shapes, so the
+        step stays capturable in a hipGraph: rank r routes its ceil(M/P) slice of the (replicated)
+        rows; every (token, slot) pair is sent to the rank owning its expert through a fixed-
+        capacity all-to-all (cap = slice x top-k rows per rank pair, zero rows where a pair goes
+        elsewhere); each rank runs its local experts over what it received (masked per expert),
+        the results return by the reverse all-to-all, are weighted and summed per token, and the
+        slices are all-gathered.  Compared with the replicated form (every rank runs its experts on
+        every token, then ONE all-reduce of [M, d]) it computes only routed pairs but moves two
+        all-to-alls plus an all-gather; at decode batch sizes both stream every local expert's
+        weights once (profiles/r02/README.md has the measured comparison)."""
+        c = self.cfg
+        P, r, K, d = self.tp, self.rank, c.top_k_experts, c.d_model
+        epr = c.n_experts // P
+        M = x.shape[0]
+        cap = -(-M // P)
+        if M < P * cap:
+            x = torch.cat([x, x.new_zeros(P * cap - M, d)])
+        xs = x[r * cap:(r + 1) * cap]
+        ids, w = ops.moe_route(F.linear(xs, L["router"]).float(), K, True)  # [cap, K]
+        ids = ids.long()
+        npair = cap * K
+        pair_x = xs.repeat_interleave(K, dim=0)  # [cap*K, d], pair j = (token j // K, slot j % K)
+        dest = (ids // epr).view(-1)  # [cap*K]
+        sel = dest.unsqueeze(0) == torch.arange(P, device=x.device).unsqueeze(1)  # [P, cap*K]
+        send = pair_x.unsqueeze(0) * sel.unsqueeze(-1).to(x.dtype)
+        send_e = torch.where(sel, (ids.view(-1) % epr).unsqueeze(0), torch.full_like(sel, -1, dtype=torch.long))
+        recv = torch.empty_like(send)
+        recv_e = torch.empty_like(send_e)
+        tp_all_to_all(recv.view(P * npair, d), send.view(P * npair, d), [npair] * P, [npair] * P, self.ps)
+        tp_all_to_all(recv_e.view(-1), send_e.view(-1), [npair] * P, [npair] * P, self.ps)
+        rows = recv.view(P * npair, d)
+        re = recv_e.view(-1, 1)
+        y = torch.zeros(P * npair, d, dtype=torch.float32, device=x.device)
+        for j in range(epr):
+            h = ops.silu_mul(F.linear(rows, L["w13"][j]), interleaved=self._w13_il)
+            y += F.linear(h, L["w2"][j]).float() * (re == j).float()
+        back = torch.empty(P * npair, d, dtype=x.dtype, device=x.device)
+        tp_all_to_all(back, y.to(x.dtype), [npair] * P, [npair] * P, self.ps)
+        res = back.view(P, npair, d)[dest, torch.arange(npair, device=x.device)]  # [cap*K, d]
+        z = (res.view(cap, K, d).float() * w.unsqueeze(-1)).sum(1).to(x.dtype)
+        return tp_all_gather_rows(z, self.ps)[:M]
 
     def _norm(self, x: torch.Tensor, w) -> torch.Tensor:
         if isinstance(w, tuple):
@@ -527,6 +591,18 @@ class CausalLM:
                 rn = (ss, eps)
                 continue
             ns = ops.skinny_slabs(op, L["wo_p"], ws, self._split_o, rows=M)
+            if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
+                # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated
+                # MLP output comes back from _moe_a2a_decode
+                y = self._row_parallel_sum(ws, ns, M, residual)
+                xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], eps)
+                z = self._moe_a2a_decode(L, xn)
+                nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
+                xr = ops.fused_add_rms_norm(z, residual, nw, eps)
+                if i + 1 < n:
+                    xw, rn = ops.pack_activation(xr), None
+                    continue
+                return self._logits(xr)
             if c.is_moe:
                 ns = self._moe_skinny(L, residual, ws, ns, M)
             else:

@@ -739,6 +739,29 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor, div: int = 1) -> torch.Tenso
     return out
 
 
+def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, swiglu: bool = False,
+                     out: Optional[torch.Tensor] = None, zero_fill: bool = True) -> torch.Tensor:
+    """All experts' GEMMs in one launch over expert-sorted rows: ``x`` [rows, K], ``w`` [E, N, K],
+    ``offsets`` [E + 1] int32 absolute row offsets of the experts' rows in ``x`` (moe_align, may be
+    a slice for this rank's experts).  ``swiglu``: ``w`` is gate/up-interleaved and the result is
+    silu(gate) * up [rows, N / 2].  Rows of other experts are left as in ``out`` (zeros when
+    allocated here).  GPU: no host synchronisation (moe_gemm.hip)."""
+    E, N, K = w.shape
+    if out is None:  # zero_fill=False when ``offsets`` covers every row (all experts are local)
+        alloc = torch.zeros if zero_fill else torch.empty
+        out = alloc(x.shape[0], N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if not _gpu(x):
+        off = offsets.tolist()
+        for e in range(E):
+            a, b = off[e], off[e + 1]
+            if b > a:
+                y = torch.nn.functional.linear(x[a:b].float(), w[e].float()).to(x.dtype)
+                out[a:b] = silu_mul(y, interleaved=True) if swiglu else y
+        return out
+    native().moe_grouped_gemm(out, x.contiguous(), w, offsets.contiguous(), swiglu)
+    return out
+
+
 def moe_combine(y: torch.Tensor, inv_idx: torch.Tensor, w: torch.Tensor, T: int) -> torch.Tensor:
     if not _gpu(y):
         return ref.moe_combine(y, inv_idx, w, T)

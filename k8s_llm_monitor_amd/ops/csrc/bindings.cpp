@@ -39,6 +39,8 @@ int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, in
 int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
+int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* offsets, int E, long rows, int N, int K,
+                            long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                        float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
@@ -336,6 +338,24 @@ void moe_combine(torch::Tensor out, torch::Tensor expert_out, torch::Tensor inv_
   check(k8sllm_moe_combine(out.data_ptr(), expert_out.data_ptr(), inv_idx.data_ptr<int>(), topk_w.data_ptr<float>(),
                            out.size(0), (int)topk_w.size(1), d, cur()),
         "moe_combine");
+}
+
+// Grouped expert GEMM over expert-sorted rows (moe_gemm.hip): x [rows, K], w [E, N, K], offsets
+// [E + 1] int32 absolute row offsets of the experts in x (device, from moe_align; no host sync).
+// swiglu: w gate/up-interleaved per 128 rows, y [rows, N / 2] = silu(gate) * up; else y [rows, N].
+// Rows outside [offsets[0], offsets[E]) are not written.
+void moe_grouped_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, torch::Tensor offsets, bool swiglu) {
+  dev_bf16(y, "y"); dev_bf16(x, "x"); dev_bf16(w, "w"); dev_i32(offsets, "offsets");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.dim() == 3 && w.is_contiguous() && y.is_contiguous(),
+              "moe_grouped_gemm: x [rows, K], w [E, N, K] contiguous");
+  const int E = (int)w.size(0), N = (int)w.size(1), K = (int)w.size(2);
+  TORCH_CHECK(x.size(1) == K, "moe_grouped_gemm: K mismatch");
+  TORCH_CHECK(offsets.numel() == E + 1, "moe_grouped_gemm: offsets must hold E + 1 entries");
+  TORCH_CHECK(N % 128 == 0 && K % 64 == 0, "moe_grouped_gemm: N % 128 == 0 and K % 64 == 0");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == (swiglu ? N / 2 : N), "moe_grouped_gemm: y shape");
+  check(k8sllm_moe_grouped_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), offsets.data_ptr<int>(), E, x.size(0), N, K,
+                                (long)N * K, swiglu ? 1 : 0, cur()),
+        "moe_grouped_gemm");
 }
 
 void gather_rows(torch::Tensor out, torch::Tensor x, torch::Tensor idx, int64_t div) {
@@ -700,6 +720,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
   m.def("layer_norm", &layer_norm);
   m.def("silu_mul", &silu_mul);
+  m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("embedding", &embedding);
   m.def("resolve_ids", &resolve_ids);

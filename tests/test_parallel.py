@@ -30,9 +30,9 @@ def _drive(eng, SamplingParams):
     return [s.output_ids for s in seqs], eng.counters["mixed_steps"]
 
 
-def _worker(rank, world, port, model, q, bus="shm"):
+def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), K8SLLM_STEP_BUS=bus)
+                      LOCAL_RANK=str(rank), K8SLLM_STEP_BUS=bus, K8SLLM_MOE_DECODE=moe_decode)
     torch.set_num_threads(2)
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
@@ -74,15 +74,18 @@ def _worker(rank, world, port, model, q, bus="shm"):
         q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("model,world,bus", [("llama-tiny", 2, "shm"), ("mixtral-tiny", 2, "shm"),
-                                             ("gpt2-tiny", 2, "shm"), ("llama-tiny", 2, "gloo"),
-                                             # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
-                                             ("llama-tiny", 4, "shm"), ("mixtral-tiny", 4, "shm")])
-def test_tp_matches_tp1(model, world, bus):
+@pytest.mark.parametrize("model,world,bus,moe_decode", [
+    ("llama-tiny", 2, "shm", "allreduce"), ("mixtral-tiny", 2, "shm", "allreduce"),
+    ("gpt2-tiny", 2, "shm", "allreduce"), ("llama-tiny", 2, "gloo", "allreduce"),
+    # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
+    ("llama-tiny", 4, "shm", "allreduce"), ("mixtral-tiny", 4, "shm", "allreduce"),
+    # expert-parallel all-to-all MoE decode (static-capacity dispatch / combine)
+    ("mixtral-tiny", 2, "shm", "a2a"), ("mixtral-tiny", 4, "shm", "a2a")])
+def test_tp_matches_tp1(model, world, bus, moe_decode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, bus)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, bus, moe_decode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]

@@ -106,3 +106,20 @@ def test_decode_skinny_path_matches_generic_cpu(monkeypatch, model, fused):
     monkeypatch.setenv("K8SLLM_SKINNY", "0")
     b = m.forward(ids, meta, kv)
     assert (a - b).abs().max().item() < 1e-4
+
+
+def test_moe_grouped_gemm_cpu_path():
+    """CPU form of the grouped expert GEMM: per-expert row blocks from the offsets, SwiGLU over the
+    interleaved w13, rows outside the offset range untouched (zero)."""
+    counts = [3, 0, 5]
+    x = torch.randn(sum(counts) + 2, 64)
+    w = torch.randn(3, 128, 64)
+    off = torch.tensor([2, 5, 5, 10], dtype=torch.int32)  # rows 0-1 belong to another rank
+    y = ops.moe_grouped_gemm(x, w, off)
+    assert torch.equal(y[:2], torch.zeros(2, 128))
+    assert torch.allclose(y[2:5], x[2:5] @ w[0].t(), atol=1e-5)
+    assert torch.allclose(y[5:10], x[5:10] @ w[2].t(), atol=1e-5)
+    wi = torch.stack([ops.interleave_gate_up(e) for e in w])
+    ys = ops.moe_grouped_gemm(x, wi, off, swiglu=True)
+    g, u = (x[5:10] @ w[2].t()).chunk(2, dim=1)
+    assert torch.allclose(ys[5:10], torch.nn.functional.silu(g) * u, atol=1e-4)
