@@ -762,6 +762,37 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
     return out
 
 
+def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] = None, swiglu: bool = False,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Prefill-sized ``x @ w^T`` on the 256 x 256 MFMA tile kernel (csrc/gemm_tile.hip).
+
+    Dense: ``w`` [N, K].  Grouped: ``w`` [E, N, K] and ``offsets`` [E + 1] int32 device offsets of
+    each expert's rows in the expert-sorted ``x`` (moe_align; a slice for this rank's experts) - no
+    host synchronisation.  ``swiglu``: ``w`` is gate/up-interleaved (interleave_gate_up) and the
+    result is silu(gate) * up [M, N / 2].  Grouped rows outside the offsets are left as in ``out``
+    (zeros when allocated here)."""
+    M = x.shape[0]
+    N = w.shape[-2]
+    if out is None:
+        alloc = torch.zeros if offsets is not None else torch.empty
+        out = alloc(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if not _gpu(x):
+        def one(xr, wr):
+            y = torch.nn.functional.linear(xr.float(), wr.float()).to(x.dtype)
+            return silu_mul(y, interleaved=True) if swiglu else y
+        if offsets is None:
+            out.copy_(one(x, w))
+        else:
+            off = offsets.tolist()
+            for e in range(w.shape[0]):
+                a, b = off[e], off[e + 1]
+                if b > a:
+                    out[a:b] = one(x[a:b], w[e])
+        return out
+    native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None, swiglu)
+    return out
+
+
 def moe_combine(y: torch.Tensor, inv_idx: torch.Tensor, w: torch.Tensor, T: int) -> torch.Tensor:
     if not _gpu(y):
         return ref.moe_combine(y, inv_idx, w, T)

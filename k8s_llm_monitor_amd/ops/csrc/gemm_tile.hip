@@ -1,0 +1,332 @@
+// 256 x 256 MFMA GEMM for prefill-sized projections, dense or grouped
+// over experts, with the SwiGLU activation fused into the epilogue.
+//
+//   Y[r][n] = sum_k X[r][k] * W[n][k]        (both operands K-contiguous: X [rows][K], W [N][K])
+//
+// Dense:   one weight, rows 0 .. M-1.
+// Grouped: W [E][N][K]; expert e owns rows offsets[e] .. offsets[e+1]-1 of the expert-sorted X
+//          (moe_align); each workgroup finds its (expert, m-tile) from the device offsets, so a
+//          MoE layer needs no host synchronisation.
+// EPI_SWIGLU: W is gate/up-interleaved per 128 rows ([64 gate | 64 up], ops.interleave_gate_up),
+//          Y = silu(gate) * up [rows][N / 2] - the separate silu_mul pass over the [rows][N]
+//          intermediate disappears.
+//
+// Structure (cdna_hip_programming.md §5, "The 256² 8-phase template"; own schedule):
+//  * workgroup = 8 waves, 256 x 256 output, K in 64-deep tiles.  LDS: two buffers x (A 256 x 128 B
+//    + B 256 x 128 B) = 128 KiB, ONE __shared__ array (a second one makes hipcc drain vmcnt).
+//  * every tile is split into four half-tiles A0 A1 B0 B1 (128 rows x 128 B = 16 KiB, two
+//    global_load_lds_dwordx4 per thread); the tile's output is computed as four 128 x 128
+//    quadrants (qm, qn) in the order (0,0) (0,1) (1,1) (1,0), one per phase.  Per quadrant a wave
+//    owns 64 rows x 32 columns (16 v_mfma_f32_16x16x32_bf16: 4 m-fragments x 2 n-fragments x 2
+//    k-steps); its two n-fragments sit 64 columns apart, so a SwiGLU tile's gate and up values of
+//    one output element are in the same lane and register index.
+//  * operand fragments live in four register sets xa0 xa1 (X, quadrant row halves) and wf0 wf1
+//    (W, column halves); the quadrant order alternates with the tile's parity so each phase's
+//    ds_reads fill a set only a LATER phase uses - no fragment read is waited for synchronously.
+//  * one half-tile DMA refill per phase, issued as single pieces between the MFMA k-steps, one
+//    raw s_barrier per two phases (32 MFMAs per wave) preceded by `s_waitcnt vmcnt(8)`: 4 younger
+//    half-tiles stay in flight across it - never __syncthreads() while a DMA is pending.
+//  * LDS rows are 128 B; chunk c of row r is stored at c ^ ((r >> 1) & 7) (swizzle applied to the
+//    DMA source address, the LDS side stays lane-linear), so every ds_read_b128 16-lane group hits
+//    16 distinct bank quads.
+//  * XCD-aware tile order: workgroup ids are remapped so each XCD runs a contiguous range of
+//    logical tiles, ordered in groups of 8 m-tiles (neighbours share A or B through that XCD's L2).
+#include <type_traits>
+
+#include "common.h"
+
+namespace k8sllm {
+
+namespace {
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+}  // namespace
+
+enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1 };
+
+template <int EPI, bool GROUPED>
+__global__ __launch_bounds__(512, 1) void gemm_tile256_kernel(const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                              const int* __restrict__ offsets, int E, int M, int N,
+                                                              int K, long w_es, int n_mt, int n_nt) {
+  constexpr int BUF = 65536, BOFF = 32768, HALF = 16384;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- logical tile of this workgroup: XCD remap (bijective) then groups of 8 m-tiles ----
+  const int nwg = n_mt * n_nt;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = lid / (GM * n_nt), first_m = grp * GM;
+  const int gsz = min(n_mt - first_m, GM);
+  const int in_g = lid - grp * GM * n_nt;
+  const int mt = first_m + in_g % gsz, nt = in_g / gsz;
+
+  int row0, mrows;
+  const bf16_t* Wt = W;
+  if constexpr (GROUPED) {
+    int e = -1, acc_t = 0;
+    row0 = 0;
+    mrows = 0;
+    for (int x = 0; x < E; ++x) {
+      const int o0 = offsets[x], o1 = offsets[x + 1];
+      const int tiles = (o1 - o0 + 255) >> 8;
+      if (e < 0 && mt < acc_t + tiles) {
+        e = x;
+        row0 = o0 + (mt - acc_t) * 256;
+        mrows = min(256, o1 - row0);
+      }
+      acc_t += tiles;
+    }
+    if (e < 0) return;  // uniform: past the last expert's tiles
+    Wt = W + (long)e * w_es;
+  } else {
+    row0 = mt * 256;
+    mrows = min(256, M - row0);
+  }
+  const int n0 = nt * 256;
+
+  // ---- DMA sources: half h (0 A0, 1 A1, 2 B0, 3 B1), piece j (0, 1) -> LDS rows of the half
+  // (j * 8 + wave) * 8 .. + 7; lane -> row + (lane >> 3), 16-B slot lane & 7 ----
+  uint32_t soff[4][2];
+  const char* xb = reinterpret_cast<const char*>(X);
+  const char* wb_ = reinterpret_cast<const char*>(Wt);
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rl = (h & 1) * 128 + (j * 8 + wave) * 8 + (lane >> 3);  // row within the A or B tile
+      const int c = (lane & 7) ^ ((rl >> 1) & 7);
+      if (h < 2) {
+        const int r = row0 + min(rl, mrows - 1);  // rows past the end: clamped, never stored
+        soff[h][j] = (uint32_t)(((long)r * K + c * 8) * 2 - (long)row0 * K * 2);
+      } else {
+        soff[h][j] = (uint32_t)(((long)(n0 + rl) * K + c * 8) * 2);
+      }
+    }
+  const char* xbase = xb + (long)row0 * K * 2;
+  const int nk = K >> 6;
+
+  // issue half-tile h of K-tile kt into buffer kt & 1
+  auto issue = [&](int h, int kt) {
+    char* dst = smem + (kt & 1) * BUF + (h >> 1) * BOFF + (h & 1) * HALF;
+    const char* base = (h < 2 ? xbase : wb_) + kt * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + soff[h][j]), (lds_void_t*)(dst + (j * 8 + wave) * 1024),
+                                       16, 0, 0);
+  };
+
+  // fragment reads: lane row = lane & 15, 16-B chunk 4 ks + (lane >> 4), swizzle (lane >> 1) & 7
+  const int swz = (lane >> 1) & 7;
+  const int rd_row = (lane & 15) * 128;
+  int chk[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) chk[ks] = ((4 * ks + (lane >> 4)) ^ swz) << 4;
+  // X set qm: rows qm*128 + wm*64 + i*16 ; W set qn: rows qn*128 + jj*64 + wn*16
+  auto read_x = [&](bf16x8 (&f)[4][2], int kt, int qm) {
+    const char* b = smem + (kt & 1) * BUF + (qm * 128 + wm * 64) * 128 + rd_row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) f[i][ks] = *reinterpret_cast<const bf16x8*>(b + i * 2048 + chk[ks]);
+  };
+  auto read_w = [&](bf16x8 (&f)[2][2], int kt, int qn) {
+    const char* b = smem + (kt & 1) * BUF + BOFF + (qn * 128 + wn * 16) * 128 + rd_row;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) f[jj][ks] = *reinterpret_cast<const bf16x8*>(b + jj * 8192 + chk[ks]);
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[a][b][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one k-step (8 MFMAs) of quadrant (qm, qn)
+  auto mma = [&](int qm, int qn, const bf16x8 (&xa)[4][2], const bf16x8 (&wf)[2][2], int ks) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[qm][qn][i][jj] = mfma16(wf[jj][ks], xa[i][ks], acc[qm][qn][i][jj]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one DMA piece (1 KiB per wave) between MFMA k-steps: the texture path streams the next tiles
+  // while the matrix cores run, instead of every wave queueing 4 DMAs at once at a barrier
+  auto piece = [&](bool on, int h, int kt, int j) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (on) {
+      char* dst = smem + (kt & 1) * BUF + (h >> 1) * BOFF + (h & 1) * HALF;
+      const char* base = (h < 2 ? xbase : wb_) + kt * 128;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + soff[h][j]), (lds_void_t*)(dst + (j * 8 + wave) * 1024),
+                                       16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  bf16x8 xa0[4][2], xa1[4][2], wf0[2][2], wf1[2][2];
+
+  // ---- quadrant order alternates with the tile's parity P so that no fragment set is read
+  // synchronously: P = 0: (0,0) (0,1) (1,1) (1,0); P = 1: (0,1) (0,0) (1,0) (1,1).  The last
+  // quadrant of a tile and the first of the next differ in both coordinates, so both sets the
+  // next tile starts with are free one phase early.  Fragment reads (one phase ahead of use):
+  //   ph1: W half 1-P of tile t     ph2: X half 1 of t     ph3: X half 0 of t+1
+  //   ph4: W half 1-P of t+1 (= the first W half of tile t+1, whose parity is 1-P)
+  // Barriers: one per two phases (S1 = ph1+ph2, S2 = ph3+ph4; 32 MFMAs per wave between
+  // barriers).  S1(t) reads W_(1-P)(t), A1(t); S2(t) reads A0(t+1), W_(1-P)(t+1).  A region is
+  // refilled for tile t+2 in the half-phase after the barrier that retires its read:
+  //   S1(t) issues A0(t+2), W_P(t+2)        S2(t) issues W_(1-P)(t+2), A1(t+2)
+  // which is 3 half-phases before tile t+2 reads it; each half-phase ends with lgkmcnt(0),
+  // vmcnt(8) (4 younger half-tiles in flight) and one raw s_barrier. ----
+
+  // prologue: tile 0 (parity 0) is preceded by the reads of A0(0) and W0(0) ("S2(-1)");
+  // halves in issue order: A0(0) B0(0) B1(0) A1(0) | A0(1) B1(1) B0(1) A1(1)
+  issue(0, 0);
+  issue(2, 0);
+  issue(3, 0);
+  issue(1, 0);
+  if (nk > 1) {
+    issue(0, 1);
+    issue(3, 1);
+    issue(2, 1);
+    issue(1, 1);
+    vm_wait<12>();  // A0(0), B0(0) landed
+  } else {
+    vm_wait<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  read_x(xa0, 0, 0);
+  read_w(wf0, 0, 0);
+  lgkm_wait0();
+  if (nk > 1) vm_wait<8>(); else vm_wait<0>();  // B1(0), A1(0) landed
+  __builtin_amdgcn_s_barrier();
+
+  auto tile = [&](int t, auto par) {
+    constexpr int P = decltype(par)::value;
+    const bool full = t + 2 < nk;  // every DMA counted by this tile's waits is real
+    auto end_half = [&]() {
+      lgkm_wait0();
+      if (full) vm_wait<8>(); else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+    };
+    // S1: phase 1 + phase 2 (DMA: A0(t+2), W_P(t+2), one piece per MFMA k-step)
+    const bool ld = t + 2 < nk;
+    if constexpr (P == 0) read_w(wf1, t, 1); else read_w(wf0, t, 0);
+    if constexpr (P == 0) {
+      mma(0, 0, xa0, wf0, 0); piece(ld, 0, t + 2, 0); mma(0, 0, xa0, wf0, 1); piece(ld, 0, t + 2, 1);
+    } else {
+      mma(0, 1, xa0, wf1, 0); piece(ld, 0, t + 2, 0); mma(0, 1, xa0, wf1, 1); piece(ld, 0, t + 2, 1);
+    }
+    read_x(xa1, t, 1);
+    if constexpr (P == 0) {
+      mma(0, 1, xa0, wf1, 0); piece(ld, 2 + P, t + 2, 0); mma(0, 1, xa0, wf1, 1); piece(ld, 2 + P, t + 2, 1);
+    } else {
+      mma(0, 0, xa0, wf0, 0); piece(ld, 2 + P, t + 2, 0); mma(0, 0, xa0, wf0, 1); piece(ld, 2 + P, t + 2, 1);
+    }
+    end_half();
+    // S2: phase 3 + phase 4 (DMA: W_(1-P)(t+2), A1(t+2))
+    if (t + 1 < nk) read_x(xa0, t + 1, 0);
+    if constexpr (P == 0) {
+      mma(1, 1, xa1, wf1, 0); piece(ld, 3 - P, t + 2, 0); mma(1, 1, xa1, wf1, 1); piece(ld, 3 - P, t + 2, 1);
+    } else {
+      mma(1, 0, xa1, wf0, 0); piece(ld, 3 - P, t + 2, 0); mma(1, 0, xa1, wf0, 1); piece(ld, 3 - P, t + 2, 1);
+    }
+    if (t + 1 < nk) {
+      if constexpr (P == 0) read_w(wf1, t + 1, 1); else read_w(wf0, t + 1, 0);
+    }
+    if constexpr (P == 0) {
+      mma(1, 0, xa1, wf0, 0); piece(ld, 1, t + 2, 0); mma(1, 0, xa1, wf0, 1); piece(ld, 1, t + 2, 1);
+    } else {
+      mma(1, 1, xa1, wf1, 0); piece(ld, 1, t + 2, 0); mma(1, 1, xa1, wf1, 1); piece(ld, 1, t + 2, 1);
+    }
+    end_half();
+  };
+  for (int t = 0; t < nk; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < nk) tile(t + 1, std::integral_constant<int, 1>{});
+  }
+
+  // ---- epilogue: acc[qm][qn][i][jj][r] = Y[m][n] with m = qm*128 + wm*64 + i*16 + (lane & 15),
+  // n = qn*128 + jj*64 + wn*16 + 4 (lane >> 4) + r (the MFMA took W as its A operand) ----
+  const int ml = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = qm * 128 + wm * 64 + i * 16 + ml;
+      if (m >= mrows) continue;
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) {
+        if constexpr (EPI == TILE_EPI_SWIGLU) {
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float g = bf2f(f2bf(acc[qm][qn][i][0][r])), u = bf2f(f2bf(acc[qm][qn][i][1][r]));
+            o[r] = g * u / (1.f + __expf(-g));
+          }
+          bf16_t* yp = Y + (long)(row0 + m) * (N >> 1) + ((n0 + qn * 128) >> 1) + wn * 16 + nq;
+          *reinterpret_cast<uint2*>(yp) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x4 v = acc[qm][qn][i][jj];
+            bf16_t* yp = Y + (long)(row0 + m) * N + n0 + qn * 128 + jj * 64 + wn * 16 + nq;
+            *reinterpret_cast<uint2*>(yp) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+          }
+        }
+      }
+    }
+}
+
+}  // namespace k8sllm
+
+using namespace k8sllm;
+
+// Dense (offsets == nullptr): Y [M][N] (SwiGLU: [M][N / 2]) = X [M][K] . W[N][K]^T.
+// Grouped: W [E][N][K] with expert stride w_es elements; M = total expert-sorted rows (the grid
+// bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
+extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
+                                long w_es, int epi, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (N % 256 != 0 || K % 64 != 0 || K < 64) return -1;
+  const bool grouped = offsets != nullptr;
+  if (grouped && (E < 1 || E > 256)) return -1;
+  // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert)
+  if ((long)N * K * 2 >= (1L << 31)) return -3;
+  const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = N / 256;
+  const long nwg = (long)n_mt * n_nt;
+  if (nwg > (1L << 30)) return -2;
+  dim3 grid((unsigned)nwg), blk(512);
+#define K8_TILE_LAUNCH(EPI_, G_)                                                                                  \
+  hipLaunchKernelGGL((gemm_tile256_kernel<EPI_, G_>), grid, blk, 0, s, (const bf16_t*)X, (const bf16_t*)W,      \
+                     (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+  if (grouped) {
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true);
+    else K8_TILE_LAUNCH(TILE_EPI_BF16, true);
+  } else {
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false);
+    else K8_TILE_LAUNCH(TILE_EPI_BF16, false);
+  }
+#undef K8_TILE_LAUNCH
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,108 @@
+"""Prefill GEMMs on MI355X: the 256 x 256 MFMA tile kernel (ops/csrc/gemm_tile.hip) against
+hipBLASLt (torch F.linear), at the Llama-3-8B prefill-chunk shapes (16384 tokens) and the
+Mixtral-8x7B grouped expert shapes (top-2 of 8).  Random operands, interleaved rounds, hipGraph
+replay of back-to-back calls; the SwiGLU rows compare the fused epilogue with F.linear + silu_mul.
+
+    python tools/bench_gemm_tile.py [--tokens 16384] [--rounds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from k8s_llm_monitor_amd import ops  # noqa: E402
+from tools.bench_skinny import timeit  # noqa: E402
+
+F_ = torch.nn.functional
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=16)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--impl", default="", help="comma list of implementations to time (default all)")
+    a = ap.parse_args()
+    dev = "cuda"
+    T = a.tokens
+    torch.manual_seed(0)
+    cases = []
+    d, F = 4096, 14336
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    xf = torch.randn(T, F, device=dev, dtype=torch.bfloat16)
+    for name, N, K in (("qkv", 6144, d), ("o", d, d), ("down", d, F)):
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+        xin = xf if K == F else x
+        y = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
+        cases.append((name, 2 * T * N * K, {
+            "tile": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y)),
+            "hipblaslt": (lambda i, xin=xin, w=w, y=y: torch.matmul(xin, w.t(), out=y)),
+        }))
+    w13 = ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02).contiguous()
+    gu = torch.empty(T, 2 * F, device=dev, dtype=torch.bfloat16)
+    act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
+    cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
+        "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act)),
+        "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
+        "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
+    }))
+    # Mixtral grouped experts: T tokens x top-2 over 8 experts (balanced-ish random routing)
+    E = 8
+    ids, _ = ops.moe_route(torch.randn(T, E, device=dev), 2, True)
+    offsets, _, _ = ops.moe_align(ids, E)
+    rows = 2 * T
+    off = offsets.tolist()
+    xs = torch.randn(rows, d, device=dev, dtype=torch.bfloat16)
+    hs = torch.randn(rows, F, device=dev, dtype=torch.bfloat16)
+    we13 = torch.stack([ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02)
+                        for _ in range(E)]).contiguous()
+    we2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.02
+    ha = torch.empty(rows, F, device=dev, dtype=torch.bfloat16)
+    ys = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+
+    def loop13(i):
+        for e in range(E):
+            lo, hi = off[e], off[e + 1]
+            if hi > lo:
+                ops.silu_mul(F_.linear(xs[lo:hi], we13[e]), out=ha[lo:hi], interleaved=True)
+
+    def loop2(i):
+        for e in range(E):
+            lo, hi = off[e], off[e + 1]
+            if hi > lo:
+                torch.matmul(hs[lo:hi], we2[e].t(), out=ys[lo:hi])
+
+    cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
+        "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha)),
+        "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
+        "hipblaslt_loop": loop13,
+    }))
+    cases.append(("moe_w2", 2 * rows * d * F, {
+        "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys)),
+        "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
+        "hipblaslt_loop": loop2,
+    }))
+    for name, flops, impls in cases:
+        if a.only and name not in a.only.split(","):
+            continue
+        res: dict = {}
+        for _ in range(a.rounds):
+            for tag, fn in impls.items():
+                if a.impl and tag not in a.impl.split(","):
+                    continue
+                res.setdefault(tag, []).append(timeit(fn, a.iters, per_graph=4))
+        for tag, ts in res.items():
+            t = min(ts)
+            print(json.dumps({"op": name, "tokens": T, "impl": tag, "us": round(t, 1),
+                              "us_all": [round(v, 1) for v in ts], "PFps": round(flops / t / 1e9, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
