@@ -745,7 +745,8 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
     ``offsets`` [E + 1] int32 absolute row offsets of the experts' rows in ``x`` (moe_align, may be
     a slice for this rank's experts).  ``swiglu``: ``w`` is gate/up-interleaved and the result is
     silu(gate) * up [rows, N / 2].  Rows of other experts are left as in ``out`` (zeros when
-    allocated here).  GPU: no host synchronisation (moe_gemm.hip)."""
+    allocated here).  GPU: no host synchronisation (gemm_tile.hip 256 x 256 tiles where N % 256 == 0,
+    else moe_gemm.hip)."""
     E, N, K = w.shape
     if out is None:  # zero_fill=False when ``offsets`` covers every row (all experts are local)
         alloc = torch.zeros if zero_fill else torch.empty
@@ -758,7 +759,12 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
                 y = torch.nn.functional.linear(x[a:b].float(), w[e].float()).to(x.dtype)
                 out[a:b] = silu_mul(y, interleaved=True) if swiglu else y
         return out
-    native().moe_grouped_gemm(out, x.contiguous(), w, offsets.contiguous(), swiglu)
+    if N % 256 == 0 and K % 64 == 0 and N * K * 2 < (1 << 31):
+        # the 256 x 256 tile kernel (gemm_tile.hip): 1.12-1.15 PF/s on Mixtral's expert shapes
+        # against 0.86-0.94 for the 128-tile kernel below (profiles/r02/gemm_tile_vs_hipblaslt.jsonl)
+        native().gemm_tile(out, x.contiguous(), w, offsets.contiguous(), swiglu)
+    else:
+        native().moe_grouped_gemm(out, x.contiguous(), w, offsets.contiguous(), swiglu)
     return out
 
 
