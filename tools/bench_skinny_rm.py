@@ -26,13 +26,15 @@ def main() -> None:
     ap.add_argument("--ms", default="1,16,64")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ops", default="qkv,o,gate_up,down")
+    ap.add_argument("--ncopy", type=int, default=0, help="weight copies rotated (0: enough for > 512 MiB)")
+    ap.add_argument("--impls", default="packed,rowmajor,rowmajor_w2,rowmajor_w4")
     a = ap.parse_args()
     dev = "cuda"
     d, F = 4096, 14336
     shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * F, d), "down": (d, F)}
     for name in a.ops.split(","):
         N, K = shapes[name]
-        ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
+        ncopy = a.ncopy or max(2, (512 << 20) // (N * K * 2) + 1)
         wrm = [(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02) for _ in range(ncopy)]
         wpk = [ops.pack_skinny(w) for w in wrm]
         gb = N * K * 2 / 1e9
@@ -41,9 +43,12 @@ def main() -> None:
             act = ops.packed_empty(M, F, torch.bfloat16, dev)
             wsp = ops.skinny_workspace(M, N, 16, dev)
             res: dict = {}
+            tag_sfx = f"_ncopy{ncopy}"
             for _ in range(a.rounds):
                 for tag, ws_, wv in (("packed", wpk, "0"), ("rowmajor", wrm, "0"), ("rowmajor_w2", wrm, "2"),
                                      ("rowmajor_w4", wrm, "4")):
+                    if tag not in a.impls.split(","):
+                        continue
                     os.environ["K8SLLM_SKINNY_WAVES"] = wv
                     if name == "gate_up":
                         fn = (lambda i, ws_=ws_: ops.skinny_swiglu(xp, ws_[i % ncopy], out=act, rows=M, packed_out=True))
@@ -52,7 +57,7 @@ def main() -> None:
                     res.setdefault(tag, []).append(timeit(fn, a.iters))
             for tag, ts in res.items():
                 t = min(ts)
-                print(json.dumps({"op": name, "M": M, "impl": tag, "us": round(t, 2), "us_all": [round(x, 2) for x in ts],
+                print(json.dumps({"op": name, "M": M, "impl": tag + tag_sfx, "us": round(t, 2), "us_all": [round(x, 2) for x in ts],
                                   "TBps": round(gb / t * 1e3, 2)}), flush=True)
         del wrm, wpk
         torch.cuda.empty_cache()
