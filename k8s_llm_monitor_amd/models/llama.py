@@ -355,8 +355,8 @@ class CausalLM:
         """Expert-parallel MoE with all-to-all dispatch / combine, for prefill
         at TP>1.  Activations arrive replicated (tensor-parallel attention); rank r routes its
         1/tp slice of the tokens, sends every (token, expert) row to the rank owning the expert,
-        the owners run their experts on what they received (one GEMM pair per local expert over
-        contiguous rows), the results travel back by the reverse all-to-all, are combined with the
+        the owners sort what they received by local expert and run all local experts in one grouped
+        GEMM launch per projection (host sync only for the all-to-all sizes), the results travel back by the reverse all-to-all, are combined with the
         routing weights, and the slices are all-gathered to the replicated layout the next layer's
         attention expects.  Decode keeps the graph-capturable replicated form (_moe + all-reduce):
         all-to-all splits are data-dependent and need a host sync."""
@@ -383,12 +383,19 @@ class CausalLM:
         tp_all_to_all(recv, send, recv_counts, send_counts, self.ps)
         recv_exp = torch.empty(nrecv, dtype=torch.int64, device=x.device)
         tp_all_to_all(recv_exp, send_exp, recv_counts, send_counts, self.ps)
-        y = torch.zeros_like(recv)
-        for j, e in enumerate(range(self.e_lo, self.e_hi)):
-            rows = (recv_exp == e).nonzero().flatten()
-            if rows.numel():
-                h = ops.silu_mul(F.linear(recv[rows], L["w13"][j]), interleaved=self._w13_il)
-                y[rows] = F.linear(h, L["w2"][j])
+        # the received rows arrive grouped by source rank; order them by local expert and run all
+        # local experts in one grouped launch per projection (device offsets, no further sync)
+        order = torch.argsort(recv_exp, stable=True)
+        counts = torch.bincount(recv_exp[order] - self.e_lo, minlength=epr)
+        loc_off = torch.zeros(epr + 1, dtype=torch.int32, device=x.device)
+        loc_off[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        xs_l = recv[order]
+        if self._w13_il:
+            h = ops.moe_grouped_gemm(xs_l, L["w13"], loc_off, swiglu=True, zero_fill=False)
+        else:
+            h = ops.silu_mul(ops.moe_grouped_gemm(xs_l, L["w13"], loc_off, zero_fill=False))
+        y = torch.empty_like(recv)
+        y[order] = ops.moe_grouped_gemm(h, L["w2"], loc_off, zero_fill=False)
         back = x.new_empty(n * K, c.d_model)
         tp_all_to_all(back, y, send_counts, recv_counts, self.ps)
         out = ops.moe_combine(back, inv_idx, w, n) if n else back[:0]
@@ -406,7 +413,9 @@ class CausalLM:
         slices are all-gathered.  Compared with the replicated form (every rank runs its experts on
         every token, then ONE all-reduce of [M, d]) it computes only routed pairs but moves two
         all-to-alls plus an all-gather; at decode batch sizes both stream every local expert's
-        weights once (profiles/r02/README.md has the measured comparison)."""
+        weights once.  Parity with the replicated form is tested on CPU (gloo, TP 2 and 4); a GPU
+        comparison needs two GPUs (RCCL refuses two ranks on one device, gloo has no CUDA
+        all-to-all)."""
         c = self.cfg
         P, r, K, d = self.tp, self.rank, c.top_k_experts, c.d_model
         epr = c.n_experts // P
