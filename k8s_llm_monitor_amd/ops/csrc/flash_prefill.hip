@@ -352,15 +352,21 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sa[i][r] = 0.f;
+    // all 16 K fragments of the tile are read first (64 VGPRs), then the 16 MFMAs consume them:
+    // one LDS round trip per tile instead of one per MFMA pair (287 vs 301 us at 10 x 1609)
+    bf16x8 kfr[KS][2];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 2; ++i)
         // key 32 i + r32: block 2 i + (r32 >> 4), token r32 & 15; dims 16 ks + 8 hh = piece 2 ks + hh
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(
-            kt + (2 * i + (r32 >> 4)) * 4096 + ((2 * ks + hh) * 16 + (r32 & 15)) * 16);
-        sa[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sa[i], 0, 0, 0);
-      }
+        kfr[ks][i] = *reinterpret_cast<const bf16x8*>(kt + (2 * i + (r32 >> 4)) * 4096 +
+                                                      ((2 * ks + hh) * 16 + (r32 & 15)) * 16);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) sa[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[ks][i], qf[ks], sa[i], 0, 0, 0);
   };
   // causal / end-of-sequence mask of one tile's scores: only the diagonal tile and the
   // sequence's last tile - a uniform scalar branch, kept OUT of the compute block below
@@ -377,6 +383,19 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   };
   // online softmax of one tile's scores (in place -> probabilities), then O += V^T P^T
   auto softmax_pv = [&](int t, f32x16 (&sa)[2]) {
+    // the tile's 16 V fragments are read before the softmax VALU work, which hides their latency
+    const char* vt = fp2_smem + (t % NBUF) * TILE + 16384;
+    bf16x8 vfr[2][2][DT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int d = 32 * dt + r32;
+          vfr[i][s][dt] = *reinterpret_cast<const bf16x8*>(vt + (2 * i + s) * 4096 + (d * 2 + (hh ^ ((d >> 3) & 1))) * 16);
+        }
+    __builtin_amdgcn_sched_barrier(0);
     float mx = sa[0][0];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -404,7 +423,6 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
     }
-    const char* vt = fp2_smem + (t % NBUF) * TILE + 16384;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -412,13 +430,9 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
         bf16x8 pb;
 #pragma unroll
         for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sa[i][8 * s + j];
-        const char* vb = vt + (2 * i + s) * 4096;  // block 2 i + s: keys 32 i + 16 s ..
+        // block 2 i + s: keys 32 i + 16 s ..
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int d = 32 * dt + r32;
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(vb + (d * 2 + (hh ^ ((d >> 3) & 1))) * 16);
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[dt], 0, 0, 0);
-        }
+        for (int dt = 0; dt < DT; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[i][s][dt], pb, o[dt], 0, 0, 0);
       }
   };
 
