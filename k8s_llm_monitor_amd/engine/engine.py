@@ -47,6 +47,9 @@ class EngineConfig:
     chunked_prefill: bool = True  # prompts beyond a step's token budget prefill in chunks (scheduler.py)
     # prefill budget of a mixed prefill+decode step (scheduler.py); 0 = prefill steps stall decodes
     mixed_prefill_tokens: int = 16384
+    # burst policy (scheduler.py): at most this many prefill-only steps in a row while decodes wait
+    # and the prefill backlog exceeds one step; 0 = always mix.  K8SLLM_DECODE_STALL_STEPS
+    max_decode_stall_steps: int = field(default_factory=lambda: int(os.environ.get("K8SLLM_DECODE_STALL_STEPS", "8")))
     kv_cache_gb: float = 32.0
     num_blocks: Optional[int] = None
     use_graphs: bool = True
@@ -109,7 +112,8 @@ class LLMEngine:
                                                max_prefill_tokens=cfg.max_prefill_tokens,
                                                max_model_len=self.runner.max_len,
                                                chunked_prefill=cfg.chunked_prefill,
-                                               mixed_prefill_tokens=cfg.mixed_prefill_tokens), self.blocks)
+                                               mixed_prefill_tokens=cfg.mixed_prefill_tokens,
+                                               max_decode_stall_steps=cfg.max_decode_stall_steps), self.blocks)
         self.tokenizer = tokenizer_from_dir(cfg.weights, mc) if cfg.weights else tokenizer_for(mc)
         self.eos = set(mc.eos_ids)
         self.init_s = time.perf_counter() - t0

@@ -10,6 +10,12 @@ A step is one of
   prefill budget of a mixed step is ``mixed_prefill_tokens`` (a bound on the TPOT hiccup a new
   arrival costs the running decodes); a prefill-only step uses ``max_prefill_tokens``.
 
+Burst policy: while the prefill backlog is larger than one step's budget (a burst of arrivals),
+steps are prefill-only - decode rows riding along would finish early but cannot shorten the burst,
+and mixed steps cost more than the prefill they carry - for at most ``max_decode_stall_steps``
+consecutive steps, after which one mixed step runs the decodes (so sustained overload cannot starve
+them).  With a backlog of at most one step (steady arrivals) every prefill step is mixed.
+
 When the KV cache runs out during decode the most recently admitted sequence is preempted (blocks
 freed, re-queued at the front, recomputed later).  Admission of a new sequence requires its
 blocks (fresh + prefix-cache hits parked in the LRU) to be free beyond a small watermark; the
@@ -38,6 +44,9 @@ class SchedulerConfig:
     chunked_prefill: bool = True
     # mixed prefill+decode steps (see the module docstring); 0 = prefill steps stall decodes
     mixed_prefill_tokens: int = 16384
+    # burst policy (module docstring): prefill-only steps while decodes wait, at most this many in
+    # a row; 0 = always mix
+    max_decode_stall_steps: int = 8
 
 
 @dataclass
@@ -65,6 +74,7 @@ class Scheduler:
         self.blocks = blocks
         self.waiting: deque[Sequence] = deque()
         self.running: list[Sequence] = []
+        self._stalled = 0  # consecutive prefill-only steps taken while decode rows were ready
 
     def add(self, seq: Sequence) -> None:
         if len(seq.prompt_ids) == 0:
@@ -94,10 +104,27 @@ class Scheduler:
         return bool(self.waiting and len(self.running) < self.cfg.max_num_seqs) or any(
             not q.prefilled for q in self.running)
 
+    def prefill_backlog(self) -> int:
+        """Prompt tokens still to prefill: partially prefilled running sequences plus the waiting
+        requests that fit the free sequence slots."""
+        n = sum(q.num_tokens - q.num_computed for q in self.running if not q.prefilled)
+        free = self.cfg.max_num_seqs - len(self.running)
+        for i, q in enumerate(self.waiting):
+            if i >= free:
+                break
+            n += q.num_tokens
+        return n
+
     def schedule(self) -> StepPlan:
         want_prefill = self.prefill_pending()
         ready = any(q.prefilled for q in self.running)
         mix = want_prefill and ready and self.cfg.mixed_prefill_tokens > 0
+        if (mix and self._stalled < self.cfg.max_decode_stall_steps
+                and self.prefill_backlog() > self.cfg.max_prefill_tokens):
+            mix = False  # burst: prefill-only step, the decodes wait (bounded)
+            self._stalled += 1
+        elif ready:
+            self._stalled = 0
         plan = StepPlan(is_prefill=False)
         if mix:  # reserve the decode rows' slots first: preemption here frees blocks for admission
             plan.decode = self._reserve_decode(plan)

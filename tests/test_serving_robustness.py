@@ -54,7 +54,8 @@ def test_mixed_step_keeps_decodes_running_and_matches_unmixed():
     for mixed in (4096, 0):
         eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=512, num_blocks=128,
                                      use_graphs=False, seed=7, dtype="float32", prefix_caching=False,
-                                     mixed_prefill_tokens=mixed, max_prefill_tokens=32), device="cpu")
+                                     mixed_prefill_tokens=mixed, max_prefill_tokens=32,
+                                     max_decode_stall_steps=0), device="cpu")
         a = eng.add_request(prompts[0], sp)
         for _ in range(3):  # a is chunked over 2 prefills then decodes one step
             eng.step()
@@ -83,6 +84,41 @@ def test_mixed_step_scheduler_plan():
     s.add(b)
     p = s.schedule()
     assert p.is_mixed and p.decode == [a] and p.seqs == [b] and b.chunk == 16  # mixed budget caps the chunk
+
+
+def test_burst_policy_prefill_first_with_bounded_decode_stall():
+    """A prefill backlog larger than one step's budget (a burst) runs prefill-only steps while the
+    ready decodes wait, at most max_decode_stall_steps in a row, then one mixed step runs them; a
+    backlog that fits one step is mixed at once."""
+    s = Scheduler(SchedulerConfig(max_num_seqs=8, max_prefill_tokens=16, mixed_prefill_tokens=16,
+                                  max_decode_stall_steps=2), BlockManager(256, use_native=False))
+    a = Sequence(prompt_ids=list(range(10)), params=SamplingParams())
+    s.add(a)
+    s.schedule()
+    s.chunk_done(a)
+    a.output_ids.append(5)
+    for i in range(3):  # 3 x 20 distinct tokens of backlog against a 16-token step
+        s.add(Sequence(prompt_ids=list(range(100 * (i + 1), 100 * (i + 1) + 20)), params=SamplingParams()))
+    kinds = []
+    for _ in range(4):
+        p = s.schedule()
+        kinds.append("mixed" if p.is_mixed else ("prefill" if p.is_prefill else "decode"))
+        if p.is_prefill:
+            for q in p.seqs:
+                s.chunk_done(q)
+    # backlog 60, 44 -> prefill-only (2 = the bound); 28 -> the bound forces a mixed step; 12 fits
+    # one step -> mixed
+    assert kinds == ["prefill", "prefill", "mixed", "mixed"], kinds
+    # steady state: the backlog fits one step -> mixed immediately
+    s2 = Scheduler(SchedulerConfig(max_num_seqs=8, max_prefill_tokens=64, mixed_prefill_tokens=64,
+                                   max_decode_stall_steps=2), BlockManager(256, use_native=False))
+    c = Sequence(prompt_ids=list(range(10)), params=SamplingParams())
+    s2.add(c)
+    s2.schedule()
+    s2.chunk_done(c)
+    c.output_ids.append(1)
+    s2.add(Sequence(prompt_ids=list(range(100, 120)), params=SamplingParams()))
+    assert s2.schedule().is_mixed
 
 
 def _tiny_engine(**kw):
