@@ -26,6 +26,8 @@
 //            projection's A operand
 // A (activations) is row-major or fragment-packed like W; the packed form turns the A loads into
 // whole-line reads too (at M = 64 the A bytes per workgroup equal the W bytes).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8sllm {
@@ -974,6 +976,28 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     // waves = 2 or 4 forces one.
     static const int lds4[5] = {0, SkinnyRmGeom<1, 4, 0, 4>::LDS, SkinnyRmGeom<2, 4, 0, 4>::LDS,
                                 SkinnyRmGeom<3, 4, 0, 4>::LDS, SkinnyRmGeom<4, 4, 0, 4>::LDS};
+    // split-K slab projections whose 64-column grid leaves CUs idle (qkv: 96 tiles x 2 slices =
+    // 192 workgroups) use 48-column tiles when that fills the chip (128 x 2 = 256).
+    // K8SLLM_SKINNY_NT = 3 / 4 forces one.
+    static const int nt_env = getenv("K8SLLM_SKINNY_NT") ? atoi(getenv("K8SLLM_SKINNY_NT")) : 0;
+    const bool nt3_ok = epi == EPI_SLAB && N % 48 == 0;
+    const bool nt3 = nt3_ok && (nt_env == 3 || (nt_env != 4 && (long)(N / 64) * slabs_rm * experts < 224 &&
+                                                 (long)(N / 48) * slabs_rm * experts <= 256));
+    if (nt3) {
+      dim3 grid3(N / 48, slabs_rm, experts), blk3(256);
+#define K8S_RM3(MTV)                                                                                              \
+  hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 3, EPI_SLAB, 4>), grid3, blk3, 0, s, (const bf16_t*)A,            \
+                     (const bf16_t*)Wp, (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, \
+                     grp, ep)
+      switch (MT) {
+        case 1: K8S_RM3(1); break;
+        case 2: K8S_RM3(2); break;
+        case 3: K8S_RM3(3); break;
+        default: K8S_RM3(4); break;
+      }
+#undef K8S_RM3
+      return (int)hipGetLastError();
+    }
     const long nwg = (long)(N / 64) * slabs_rm * experts;
     int rw = waves == 2 || waves == 4 ? waves : 4;
     if (waves != 2 && waves != 4 && nwg > 256L * (163840 / lds4[MT])) rw = 2;
