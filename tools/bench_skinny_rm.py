@@ -31,7 +31,8 @@ def main() -> None:
     a = ap.parse_args()
     dev = "cuda"
     d, F = 4096, 14336
-    shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * F, d), "down": (d, F)}
+    shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * F, d), "down": (d, F),
+              "gate_up_32k": (32768, d), "gate_up_24k": (24576, d)}  # balance probes: 512 / 384 workgroups
     for name in a.ops.split(","):
         N, K = shapes[name]
         ncopy = a.ncopy or max(2, (512 << 20) // (N * K * 2) + 1)
@@ -40,7 +41,7 @@ def main() -> None:
         gb = N * K * 2 / 1e9
         for M in map(int, a.ms.split(",")):
             xp = ops.pack_activation(torch.randn(M, K, device=dev, dtype=torch.bfloat16))
-            act = ops.packed_empty(M, F, torch.bfloat16, dev)
+            act = ops.packed_empty(M, N // 2, torch.bfloat16, dev)
             wsp = ops.skinny_workspace(M, N, 16, dev)
             res: dict = {}
             tag_sfx = f"_ncopy{ncopy}"
@@ -50,7 +51,7 @@ def main() -> None:
                     if tag not in a.impls.split(","):
                         continue
                     os.environ["K8SLLM_SKINNY_WAVES"] = wv
-                    if name == "gate_up":
+                    if name.startswith("gate_up"):
                         fn = (lambda i, ws_=ws_: ops.skinny_swiglu(xp, ws_[i % ncopy], out=act, rows=M, packed_out=True))
                     else:
                         fn = (lambda i, ws_=ws_: ops.skinny_slabs(xp, ws_[i % ncopy], wsp, 0, rows=M))
