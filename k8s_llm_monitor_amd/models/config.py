@@ -117,6 +117,11 @@ MIXTRAL_TINY = _reg(ModelConfig(
     head_dim=64, ffn_dim=256, max_position=1024, rope_theta=10000.0, n_experts=4, top_k_experts=2,
     bos_id=1, eos_ids=(2,)))
 
+MIXTRAL_TINY_E8 = _reg(ModelConfig(  # 8 query heads, 8 experts: TP / EP 8 parity tests on CPU
+    name="mixtral-tiny-e8", arch="llama", vocab_size=512, d_model=256, n_layers=2, n_heads=8, n_kv_heads=2,
+    head_dim=32, ffn_dim=256, max_position=1024, rope_theta=10000.0, n_experts=8, top_k_experts=2,
+    bos_id=1, eos_ids=(2,)))
+
 GPT2_TINY = _reg(ModelConfig(
     name="gpt2-tiny", arch="gpt2", vocab_size=512, d_model=128, n_layers=2, n_heads=2, n_kv_heads=2,
     head_dim=64, ffn_dim=512, max_position=512, tie_embeddings=True, bos_id=0, eos_ids=(0,)))

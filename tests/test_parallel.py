@@ -1,4 +1,4 @@
-"""Tensor parallelism on CPU (gloo, world_size 2 and 4): the TP-sharded model must reproduce the
+"""Tensor parallelism on CPU (gloo, world_size 2, 4 and 8): the TP-sharded model must reproduce the
 unsharded one (column/row-parallel linears, vocab-parallel embedding + LM head, expert-parallel
 MoE), and the TP engine (leader schedules, worker mirrors via broadcast) must generate the same
 tokens as a single-rank engine."""
@@ -80,7 +80,10 @@ def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce"):
     # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
     ("llama-tiny", 4, "shm", "allreduce"), ("mixtral-tiny", 4, "shm", "allreduce"),
     # expert-parallel all-to-all MoE decode (static-capacity dispatch / combine)
-    ("mixtral-tiny", 2, "shm", "a2a"), ("mixtral-tiny", 4, "shm", "a2a")])
+    ("mixtral-tiny", 2, "shm", "a2a"), ("mixtral-tiny", 4, "shm", "a2a"),
+    # TP 8, the Llama-3-70B deployment degree: one query head per rank, each KV head on 4 ranks;
+    # EP 8: one expert per rank
+    ("llama-tiny-d128", 8, "shm", "allreduce"), ("mixtral-tiny-e8", 8, "shm", "a2a")])
 def test_tp_matches_tp1(model, world, bus, moe_decode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
