@@ -123,3 +123,22 @@ def test_moe_grouped_gemm_cpu_path():
     ys = ops.moe_grouped_gemm(x, wi, off, swiglu=True)
     g, u = (x[5:10] @ w[2].t()).chunk(2, dim=1)
     assert torch.allclose(ys[5:10], torch.nn.functional.silu(g) * u, atol=1e-4)
+
+
+def test_gemm_tile_cpu_path():
+    """ops.gemm_tile off the GPU: dense, grouped (rows outside the offsets stay zero) and SwiGLU
+    against plain fp32 references (the HIP numerics are in test_gemm_tile_gpu.py)."""
+    F_ = torch.nn.functional
+    torch.manual_seed(0)
+    x = torch.randn(37, 64)
+    w = torch.randn(256, 64) * 0.1
+    torch.testing.assert_close(ops.gemm_tile(x, w), F_.linear(x, w))
+    we = torch.randn(3, 256, 64) * 0.1
+    off = torch.tensor([5, 10, 10, 30], dtype=torch.int32)  # experts 0..2 own rows 5..29
+    y = ops.gemm_tile(x, we, off)
+    assert torch.all(y[:5] == 0) and torch.all(y[30:] == 0)
+    torch.testing.assert_close(y[5:10], F_.linear(x[5:10], we[0]))
+    torch.testing.assert_close(y[10:30], F_.linear(x[10:30], we[2]))
+    wi = ops.interleave_gate_up(we[1])
+    torch.testing.assert_close(ops.gemm_tile(x, wi, swiglu=True),
+                               ops.silu_mul(F_.linear(x, we[1]), interleaved=False))
