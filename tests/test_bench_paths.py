@@ -60,9 +60,11 @@ def test_pod_communication_path(served):
     assert all(r["completion_tokens"] == 5 and r["type"] == "pod_communication" for r in res)
 
 
-def test_bench_two_ranks_under_torchrun_cpu():
-    """The driver's multi-GPU contract rehearsed on CPU: torchrun, 2 ranks (gloo), one JSON line
-    from rank 0 with the whole-job value, n_gpus 2 and dp2 parallelism."""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_ranks_under_torchrun_cpu(n):
+    """The driver's multi-GPU contract rehearsed on CPU: torchrun, n ranks (gloo; 8 = the scaling
+    run's largest point), one JSON line from rank 0 with the whole-job value, n_gpus n and dp<n>
+    parallelism."""
     import json
     import socket
     import subprocess
@@ -72,15 +74,17 @@ def test_bench_two_ranks_under_torchrun_cpu():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch", "4",
-                        "--max-new-tokens", "4"], capture_output=True, text=True, timeout=300, cwd=root)
+    batch = 4 if n == 2 else 2
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n),
+                        "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch", str(batch),
+                        "--max-new-tokens", "4"], capture_output=True, text=True, timeout=600, cwd=root,
+                       env={**os.environ, "OMP_NUM_THREADS": "1"})
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 8
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}" and d["config"]["global_batch"] == n * batch
     assert d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0 and d["scaling"] == "weak"
     assert d["config"]["path"] == "http" and d["config"]["client"] == "process"
 
