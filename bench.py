@@ -215,7 +215,9 @@ def run_rank(a) -> None:
         from k8s_llm_monitor_amd.monitor.app import post_queries
 
         kw = dict(offsets_s=offsets, allow_errors=a.production or a.mode == "poisson")
-        return (loadgen.post_queries if loadgen else post_queries)(port, items, a.max_new_tokens, **kw)
+        if loadgen:
+            return loadgen.post_queries(port, items, a.max_new_tokens, slim=True, **kw)
+        return post_queries(port, items, a.max_new_tokens, **kw)
 
     # the clients' synthetic payloads are generated up front: building them is load-generator
     # work (~13 ms per 64-query wave), not serving work, so it stays out of the timed region

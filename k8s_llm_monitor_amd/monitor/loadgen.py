@@ -9,7 +9,8 @@ the GPU (this module imports no torch and never initialises a device).
 Protocol: one JSON request per stdin line, one JSON reply per stdout line.
 
     {"op": "query", "port": P, "items": [[question, context], ...], "max_new_tokens": N,
-     "offsets_s": [...] (optional, open-loop arrival times), "allow_errors": bool (optional)}
+     "offsets_s": [...] (optional, open-loop arrival times), "allow_errors": bool (optional),
+     "slim": bool (optional: only the timing / token-count fields travel back)}
     {"op": "podcomm", "port": P, "pairs": [[pod_a, pod_b], ...], "max_new_tokens": N}
     -> {"ok": true, "results": [...]}   (post_queries / post_pod_communication result dicts)
     -> {"ok": false, "error": "..."}
@@ -19,6 +20,12 @@ from __future__ import annotations
 import json
 import subprocess
 import sys
+
+
+# what a benchmark needs from each answer: the full analysis records (answer text, prompt
+# metadata) would cross the pipe twice for nothing
+_SLIM = ("http_status", "http_latency_ms", "t_send_s", "error", "prompt_tokens", "completion_tokens", "ttft_ms",
+         "latency_ms", "finish_reason", "type")
 
 
 def serve(stdin=None, stdout=None) -> None:
@@ -35,6 +42,8 @@ def serve(stdin=None, stdout=None) -> None:
             if req["op"] == "query":
                 res = post_queries(req["port"], [tuple(x) for x in req["items"]], req["max_new_tokens"],
                                    offsets_s=req.get("offsets_s"), allow_errors=bool(req.get("allow_errors")))
+                if req.get("slim"):
+                    res = [{k: r[k] for k in _SLIM if k in r} for r in res]
             elif req["op"] == "podcomm":
                 res = post_pod_communication(req["port"], [tuple(x) for x in req["pairs"]], req["max_new_tokens"])
             else:
@@ -67,9 +76,10 @@ class LoadGen:
         return rep["results"]
 
     def post_queries(self, port: int, items: list, max_new_tokens: int, offsets_s: list | None = None,
-                     allow_errors: bool = False) -> list:
+                     allow_errors: bool = False, slim: bool = False) -> list:
         return self._call({"op": "query", "port": port, "items": [list(x) for x in items],
-                           "max_new_tokens": max_new_tokens, "offsets_s": offsets_s, "allow_errors": allow_errors})
+                           "max_new_tokens": max_new_tokens, "offsets_s": offsets_s, "allow_errors": allow_errors,
+                           "slim": slim})
 
     def post_pod_communication(self, port: int, pairs: list, max_new_tokens: int) -> list:
         return self._call({"op": "podcomm", "port": port, "pairs": [list(x) for x in pairs],

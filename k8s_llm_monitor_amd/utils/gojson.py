@@ -121,11 +121,31 @@ def format_float(f: float) -> str:
     return s
 
 
+_json_str = __import__("json").encoder.encode_basestring  # C-accelerated, non-ASCII kept raw
+
 _ESC = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t", "\b": "\\b", "\f": "\\f",
         "<": "\\u003c", ">": "\\u003e", "&": "\\u0026", "\u2028": "\\u2028", "\u2029": "\\u2029"}
 
 
 def quote(s: str) -> str:
+    r"""Go encoding/json string literal.  Fast path: the C json encoder already produces Go's
+    escapes for quotes, backslashes, \n \r \t \b \f and the other control characters
+    (\u00xx, lowercase); Go additionally escapes < > & and U+2028 / U+2029.  Strings holding
+    lone surrogates (not valid UTF-8; Go writes U+FFFD) take the per-character path."""
+    if not s.isascii():
+        try:
+            s.encode("utf-8")
+        except UnicodeEncodeError:
+            return _quote_slow(s)
+    out = _json_str(s)
+    if "<" in out or ">" in out or "&" in out:
+        out = out.replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+    if "\u2028" in out or "\u2029" in out:
+        out = out.replace("\u2028", "\\u2028").replace("\u2029", "\\u2029")
+    return out
+
+
+def _quote_slow(s: str) -> str:
     out = ['"']
     for ch in s:
         e = _ESC.get(ch)

@@ -66,3 +66,17 @@ def test_uav_report_roundtrip():
     assert r.state.battery.remaining_percent == 55.5 and r.state.health.messages == ["a"]
     back = gojson.to_plain(r)
     assert back["state"]["battery"]["remaining_percent"] == 55.5 and back["heartbeat_interval_seconds"] == 10
+
+
+def test_quote_fast_path_matches_per_character_encoder():
+    """quote()'s C-accelerated path produces exactly the per-character Go encoder's output."""
+    import random
+
+    from k8s_llm_monitor_amd.utils import gojson
+
+    alphabet = ['"', "\\", "\n", "\r", "\t", "\b", "\f", "<", ">", "&", " ", "\x00", "\x01", "\x1f", "\x7f",
+                "a", "\u96c6", "\u00e9", "\U0001f600", "\ud800", "\udfff", "/", "'", "\u0085", "\ufeff", "\u2028", "\u2029"]
+    rng = random.Random(0)
+    for _ in range(5000):
+        s = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 24)))
+        assert gojson.quote(s) == gojson._quote_slow(s), repr(s)
