@@ -376,6 +376,12 @@ def _print_trace(trace: list, t0: float) -> None:
         cur.append(e)
     waves.append(cur)
     for w in waves:
+        # wave boundary: the previous wave's last decode step -> this wave's first arrival -> first prefill
+        prev = [e[0] for e in dec if e[0] < w[0][0]]
+        nxt = [e[0] for e in pre if e[0] >= w[0][0]]
+        if prev and nxt:
+            print(f"[trace] boundary: last decode -> first add {(w[0][0] - prev[-1]) * 1e3:.1f} ms, "
+                  f"first add -> first prefill {(nxt[0] - w[0][0]) * 1e3:.1f} ms", file=sys.stderr)
         gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
         print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"
               + (f" median gap {gaps[len(gaps) // 2] * 1e3:.2f} ms max gap {gaps[-1] * 1e3:.2f} ms" if gaps else ""),
