@@ -529,12 +529,19 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
   const int ksteps = K >> 5;
   const int ngroups = nsteps / U;
 
-  // deferred RMSNorm: this thread's partial sum of squares of one A row, loaded before the first
-  // DMA (its waits then drain nothing of the ring) and held in a register through the main loop
-  float ss = 0.f;
-  if (rn_ss != nullptr && threadIdx.x < MT * 64) {
-    const int row = min((int)(threadIdx.x >> 2), M - 1);
-    for (int c = threadIdx.x & 3; c < rn_nc; c += 4) ss += rn_ss[row * rn_nc + c];
+  // deferred RMSNorm: partial sums of squares of the A rows (4 threads per row, so a 2-wave
+  // workgroup covers 32 rows per pass and holds two), loaded before the first DMA (its waits then
+  // drain nothing of the ring) and held in registers through the main loop
+  constexpr int SSP = (MT * 64 + 64 * WAVES - 1) / (64 * WAVES);
+  float ss[SSP];
+#pragma unroll
+  for (int p = 0; p < SSP; ++p) {
+    ss[p] = 0.f;
+    const int t = threadIdx.x + p * 64 * WAVES;  // wave-uniform bound: MT * 64 is whole waves
+    if (rn_ss != nullptr && t < MT * 64) {
+      const int row = min(t >> 2, M - 1);
+      for (int c = t & 3; c < rn_nc; c += 4) ss[p] += rn_ss[row * rn_nc + c];
+    }
   }
 
   // per-lane DMA sources at k-step 0 of the slice: W instruction j covers LDS rows 8j..8j+7
@@ -612,10 +619,15 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][mt], bw[u][nt], acc[mt][nt], 0, 0, 0);
   }
   __syncthreads();  // every wave is done with its ring before the combine buffer aliases it
-  if (rn_ss != nullptr && threadIdx.x < MT * 64) {  // published by the epilogue's first barrier
-    ss += __shfl_xor(ss, 1, kWave);
-    ss += __shfl_xor(ss, 2, kWave);
-    if ((threadIdx.x & 3) == 0) s_inv[threadIdx.x >> 2] = rsqrtf(ss * rn_inv_d + rn_eps);
+#pragma unroll
+  for (int p = 0; p < SSP; ++p) {
+    const int t = threadIdx.x + p * 64 * WAVES;
+    if (rn_ss != nullptr && t < MT * 64) {  // published by the epilogue's first barrier
+      float v = ss[p];
+      v += __shfl_xor(v, 1, kWave);
+      v += __shfl_xor(v, 2, kWave);
+      if ((t & 3) == 0) s_inv[t >> 2] = rsqrtf(v * rn_inv_d + rn_eps);
+    }
   }
   skinny_epilogue_rows<MT, NT, EPI, WAVES>(acc, reinterpret_cast<float*>(smem), rn_ss != nullptr ? s_inv : nullptr,
                                            partial, Y, ldy, M, N, ntile0, s, ex, grp);

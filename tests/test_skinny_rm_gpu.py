@@ -124,3 +124,30 @@ def test_rm_grouped_moe(M, E):
         a = ref.silu_mul(F_.linear(x.cpu().float(), w13[e].cpu().float()).to(torch.bfloat16))
         ref_out += F_.linear(a.float(), w2[e].cpu().float()) * wd[:, e:e + 1].cpu()
     _close(out.cpu(), ref_out, atol=6e-2, rtol=3e-2, what="rm grouped moe")
+
+
+@pytest.mark.parametrize("M", [40, 64])
+def test_rm_deferred_rmsnorm_two_wave_grids(M):
+    """Grids of more than one round of 4-wave workgroups run 2-wave workgroups (gate_up at
+    F = 14336: 448 tiles; the LM head: 2004): every row's 1/rms must reach the epilogue, not only
+    the first 32 rows' (4 threads per row cover 32 rows per pass of a 128-thread workgroup)."""
+    K, F = 4096, 14336
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    nw = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    xn = ref.rms_norm(x.cpu(), nw.cpu(), 1e-5).to(DEV).float()
+    xw, ss = ops.add_norm_partial(x.clone(), None, 0, nw)
+    w13 = _w(2 * F, K, 0.02)
+    act = ops.skinny_swiglu(xw, ops.interleave_gate_up(w13).contiguous(), rows=M, rownorm=(ss, 1e-5))
+    act_ref = ref.silu_mul((xn @ w13.float().t()).to(torch.bfloat16).cpu())
+    _rows_close(act.cpu(), act_ref, f"rm swiglu deferred norm, 448 tiles, M{M}")
+    w = _w(32768, K, 0.02)  # 512 tiles: the bf16 epilogue (LM-head form)
+    y = ops.skinny_linear(xw, w, rows=M, rownorm=(ss, 1e-5))
+    _rows_close(y.cpu(), (xn @ w.float().t()).cpu(), f"rm linear deferred norm, M{M}")
+
+
+def _rows_close(a, b, what, tol=1e-2):
+    """Per-row relative error (bf16 double rounding of the normed input moves single elements by a
+    few ulps; a missing 1/rms moves the whole row)."""
+    e = ((a.float() - b.float()).norm(dim=1) / b.float().norm(dim=1).clamp_min(1e-6))
+    bad = (e > tol).nonzero().flatten().tolist()
+    assert not bad, f"{what}: rows {bad[:8]} off by {e.max().item():.3g} (relative)"
