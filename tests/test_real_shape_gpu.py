@@ -86,18 +86,19 @@ def test_gpu_real_shape_engine_matches_fp32_reference(model, layers):
 
 
 @pytest.mark.gpu
-def test_gpu_real_shape_decode_batch64_matches_prefill():
+@pytest.mark.parametrize("batch", [40, 64])
+def test_gpu_real_shape_decode_batch64_matches_prefill(batch):
     """The headline's decode batch: 64 rows through the skinny decode graph (2-wave gate_up
     workgroups with the deferred RMSNorm, M = 64 buckets) at Llama-3-8B dimensions.  Every greedy
     token must be the argmax, or a near-tie, of the bf16 GPU prefill forward on the teacher-forced
     sequence (hipBLASLt GEMMs and flash prefill: an independent path).  Rows 33-64 exercise what
-    batches of <= 32 never reach."""
+    batches of <= 32 never reach; 40 rows run the 64-row graph with 24 padding rows."""
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
 
     eng = LLMEngine(EngineConfig(model="llama-3-8b", model_overrides={"n_layers": 2}, max_num_seqs=64,
                                  max_model_len=1024, kv_cache_gb=2.0, seed=5), device="cuda")
     eng.warmup()
-    prompts = [f"node-{i:03d} CPU={30 + i}% pod payments-{i} restarts={i % 7} 为什么我的pod频繁重启？" for i in range(64)]
+    prompts = [f"node-{i:03d} CPU={30 + i}% pod payments-{i} restarts={i % 7} 为什么我的pod频繁重启？" for i in range(batch)]
     n_new = 8
     seqs = eng.generate(prompts, SamplingParams(max_tokens=n_new, temperature=0.0, ignore_eos=True))
     assert 64 in eng.stats()["graph_buckets"]
