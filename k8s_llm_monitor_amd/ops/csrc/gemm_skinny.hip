@@ -29,6 +29,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include <type_traits>
 
 namespace k8sllm {
 
@@ -508,7 +509,7 @@ struct SkinnyRmGeom {
   static constexpr int NLOAD = NT * 2 + MT * U;      // DMA instructions per stage
 };
 
-template <int MT, int NT, int EPI, int WAVES>
+template <int MT, int NT, int EPI, int WAVES, bool ILV>
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, long ldw, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
@@ -590,7 +591,11 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
   const int nmy = wave < ngroups ? (ngroups - wave + WAVES - 1) / WAVES : 0;
   if (nmy > 0) issue(0, wave);
   if (nmy > 1) issue(1, wave + WAVES);
-  for (int i = 0; i < nmy; ++i) {
+  // one stage: wait for it, read its fragments (the slot is then free), MFMAs.  In the main loop
+  // the next-but-one stage's DMA pieces are interleaved with the MFMAs (each piece's issue cost
+  // overlaps the MFMA pipeline instead of preceding all of it); the last two stages issue nothing.
+  // Two loops with branch-free bodies keep the accumulators in AGPRs across iterations.
+  auto body = [&](int i, auto refill) {
     const int slot = i & 1;
     if (i + 1 < nmy)
       wait_vmcnt<G::NLOAD>();  // stage i landed, stage i + 1 may still fly
@@ -608,8 +613,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers: the slot is free
     __builtin_amdgcn_sched_barrier(0);
-    if (i + 2 < nmy) issue(slot, wave + (i + 2) * WAVES);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (decltype(refill)::value) issue(slot, wave + (i + 2) * WAVES);
+    if constexpr (!ILV) __builtin_amdgcn_sched_barrier(0);  // the pre-interleave order: DMAs, then MFMAs
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -617,7 +622,18 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][mt], bw[u][nt], acc[mt][nt], 0, 0, 0);
-  }
+    if constexpr (ILV && decltype(refill)::value) {
+      constexpr int PER = (U * MT * NT + G::NLOAD - 1) / G::NLOAD;
+#pragma unroll
+      for (int k = 0; k < G::NLOAD; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // one VMEM read (LDS-DMA piece)
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // then PER MFMAs
+      }
+    }
+  };
+  int i = 0;
+  for (; i + 2 < nmy; ++i) body(i, std::true_type{});
+  for (; i < nmy; ++i) body(i, std::false_type{});
   __syncthreads();  // every wave is done with its ring before the combine buffer aliases it
 #pragma unroll
   for (int p = 0; p < SSP; ++p) {
@@ -923,6 +939,15 @@ extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed,
   return sp;
 }
 
+// K8SLLM_SKINNY_ILV=0 launches the row-major kernel without the DMA / MFMA interleave (A/B knob)
+template <int MT, int NT, int EPI, int WAVES, typename... Args>
+static void launch_rm(bool ilv, dim3 grid, dim3 blk, hipStream_t s, Args... args) {
+  if (ilv)
+    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MT, NT, EPI, WAVES, true>), grid, blk, 0, s, args...);
+  else
+    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MT, NT, EPI, WAVES, false>), grid, blk, 0, s, args...);
+}
+
 // rn_ss (optional): per-row partial sums of squares [M][rn_nc] of the un-normalised A rows
 // (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
@@ -981,6 +1006,8 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     const int slabs_rm = (K + kc - 1) / kc;
     if (epi != EPI_SLAB && epi != EPI_RESNORM && epi != EPI_ROPE && slabs_rm != 1) return -3;
     const float inv_d_rm = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
+    const char* ilv_env = getenv("K8SLLM_SKINNY_ILV");
+    const bool ilv = ilv_env == nullptr || atoi(ilv_env) != 0;
     const int MT = (M + 15) / 16;
     // 4 waves per workgroup unless the grid then needs more than one round of workgroups: each
     // wave's ring holds two 16-KiB stages at M = 64, so LDS caps residency (4 waves: 1 workgroup
@@ -998,7 +1025,7 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     if (nt3) {
       dim3 grid3(N / 48, slabs_rm, experts), blk3(256);
 #define K8S_RM3(MTV)                                                                                              \
-  hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 3, EPI_SLAB, 4>), grid3, blk3, 0, s, (const bf16_t*)A,            \
+  launch_rm<MTV, 3, EPI_SLAB, 4>(ilv, grid3, blk3, s, (const bf16_t*)A,            \
                      (const bf16_t*)Wp, (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, \
                      grp, ep)
       switch (MT) {
@@ -1016,10 +1043,10 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     dim3 grid(N / 64, slabs_rm, experts), blk(64 * rw);
 #define K8S_RM(MTV, EPV)                                                                                             \
   if (rw == 4)                                                                                                       \
-    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 4, EPV, 4>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+    launch_rm<MTV, 4, EPV, 4>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
                        (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep);     \
   else                                                                                                               \
-    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MTV, 4, EPV, 2>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+    launch_rm<MTV, 4, EPV, 2>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
                        (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep)
 #define K8S_RM_M(EPV)                  \
   switch (MT) {                        \
