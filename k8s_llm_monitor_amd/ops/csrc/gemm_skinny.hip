@@ -834,6 +834,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_wide_kernel(const bf16_t* __r
 // act_index); ss_part[m][chunk] <- sum of residual^2 over the chunk.  The consumer skinny GEMM
 // applies 1/rms per row (rn_ss).  Replaces a one-workgroup-per-row norm pass, which is latency-
 // bound at decode batch sizes (64 workgroups on 256 CUs).
+// SC > 0: the slab count as a compile-time constant, so the residual, weight and every slab load
+// are issued before the first wait (one memory round trip; with a runtime count hipcc waited for
+// the residual before the slab loop and loaded the weight after the residual store: three).
+template <int SC>
 __global__ __launch_bounds__(64) void add_norm_partial_kernel(bf16_t* __restrict__ out, long out_stride,
                                                               bf16_t* __restrict__ residual,
                                                               const float* __restrict__ partial, int S, int M,
@@ -842,28 +846,47 @@ __global__ __launch_bounds__(64) void add_norm_partial_kernel(bf16_t* __restrict
   const int row = blockIdx.x, chunk = blockIdx.y;
   const int col = chunk * 512 + threadIdx.x * 8;
   bf16_t* rr = residual + (long)row * d + col;
+  const uint4 rv = *reinterpret_cast<const uint4*>(rr);
+  const uint4 wv = *reinterpret_cast<const uint4*>(w + col);
   float acc[8];
-  unpack8(*reinterpret_cast<const uint4*>(rr), acc);
+  if constexpr (SC > 0) {
+    f32x4 pa[SC], pb[SC];
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {  // the slabs are read exactly once: non-temporal
+      const float* p = partial + ((long)s * M + row) * d + col;
+      pa[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+      pb[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+    }
+    unpack8(rv, acc);
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {
+      acc[0] += pa[s].x; acc[1] += pa[s].y; acc[2] += pa[s].z; acc[3] += pa[s].w;
+      acc[4] += pb[s].x; acc[5] += pb[s].y; acc[6] += pb[s].z; acc[7] += pb[s].w;
+    }
+  } else {
+    unpack8(rv, acc);
 #pragma unroll 4
-  for (int s = 0; s < S; ++s) {  // the slabs are read exactly once: non-temporal
-    const float* p = partial + ((long)s * M + row) * d + col;
-    const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
-    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    for (int s = 0; s < S; ++s) {
+      const float* p = partial + ((long)s * M + row) * d + col;
+      const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+      const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    }
   }
   const uint4 q = pack8(acc);
-  if (S > 0) *reinterpret_cast<uint4*>(rr) = q;
   float v[8], wf[8], o[8];
   unpack8(q, v);
-  unpack8(*reinterpret_cast<const uint4*>(w + col), wf);
+  unpack8(wv, wf);
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     ss += v[j] * v[j];
     o[j] = v[j] * wf[j];
   }
+  // the normed output first: its weight operand is then waited for before any store is in flight
   *reinterpret_cast<uint4*>(out + act_index(row, col, out_stride)) = pack8(o);
+  if (S > 0) *reinterpret_cast<uint4*>(rr) = q;
   ss = wave_sum(ss);
   if (threadIdx.x == 0) ss_part[row * (d / 512) + chunk] = ss;
 }
@@ -892,8 +915,20 @@ extern "C" int k8sllm_add_norm_partial(void* out, long out_stride, void* residua
                                        int M, const void* w, int d, float* ss_part, hipStream_t s) {
   if (M <= 0) return 0;
   if (d % 512 != 0) return -1;
-  hipLaunchKernelGGL(add_norm_partial_kernel, dim3(M, d / 512), dim3(64), 0, s, (bf16_t*)out, out_stride,
-                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, ss_part);
+  const dim3 grid(M, d / 512), blk(64);
+#define K8S_ANP(SCV)                                                                                         \
+  hipLaunchKernelGGL((add_norm_partial_kernel<SCV>), grid, blk, 0, s, (bf16_t*)out, out_stride, (bf16_t*)residual, \
+                     partial, S, M, (const bf16_t*)w, d, ss_part)
+  static const bool dyn = getenv("K8SLLM_ANP_STATIC") != nullptr && atoi(getenv("K8SLLM_ANP_STATIC")) == 0;
+  switch (dyn ? -1 : S) {
+    case 1: K8S_ANP(1); break;
+    case 2: K8S_ANP(2); break;
+    case 3: K8S_ANP(3); break;
+    case 4: K8S_ANP(4); break;
+    case 8: K8S_ANP(8); break;
+    default: K8S_ANP(0); break;
+  }
+#undef K8S_ANP
   return (int)hipGetLastError();
 }
 
