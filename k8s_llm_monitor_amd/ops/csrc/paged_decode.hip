@@ -5,8 +5,9 @@
 // whole GQA group:
 //   scores  S[t][h]   = K[t][:] . Q[h][:]          A = K   (16 tokens x 32 dims per MFMA)
 //   output  O^T[d][h] = sum_t V^T[d][t] P^T[t][h]  A = V^T (16 dims  x 32 tokens per MFMA)
-// The KV-cache layouts of rope_cache.hip make every A-operand load of a wave contiguous:
-// K loads are 1 KiB per wave-instruction, V loads 512 B.  P never leaves registers: the
+// The KV-cache layouts of rope_cache.hip make every A-operand load a 16-byte piece: K and V
+// loads are 1 KiB per wave-instruction (V by the token order described at `issue`).  P never
+// leaves registers: the
 // score accumulator of two 16-token blocks is, element for element, the B operand of the
 // PV product (token order inside the k-step is permuted identically on both operands).
 //
@@ -109,12 +110,16 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
   // between chunks.  (The single-buffered 64-token form measured 82 us per layer in the engine at
   // batch 64, ctx ~1.7k, against 75 us in isolation: the prologue and each chunk's round trip
   // were exposed.)
-  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  // Token order inside each 32-token PV step s (tiles 2s, 2s + 1): QK tile 2s + j, row c holds
+  // token 16 (c >> 3) + 8 j + 4 ((c >> 2) & 1) + (c & 3) of the step, so the score lanes of k-group
+  // kg hold tokens 16 (kg >> 1) + 4 (kg & 1) + {0..3, 8..11} - in the V cache's v_perm order
+  // (common.h) exactly positions 8 (kg & 1) .. + 7 of block 2s + (kg >> 1): ONE 16-byte load per
+  // lane, dim tile and step (was two 8-byte loads from two blocks: half the V load instructions).
   typedef bf16x8 KF[kNI][KS];
-  typedef u32x2_t VF[kNS][DT];  // ext vectors, not uint2 structs: SROA keeps them in registers
-  auto issue = [&](KF& kf, VF& vlo, VF& vhi, int c) {
+  typedef bf16x8 VF[kNS][DT];
+  auto issue = [&](KF& kf, VF& vf, int c) {
     const int wtok0 = c * kCH + wave * kTW;
-    int phys[kNI];
+    int phys[kNI];  // the wave's kNI blocks (16 tokens each)
 #pragma unroll
     for (int i = 0; i < kNI; ++i) {
       const int bi = (wtok0 >> 4) + i;
@@ -122,29 +127,28 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
     }
 #pragma unroll
     for (int i = 0; i < kNI; ++i) {
-      const bf16_t* kb = k_cache + ((long)phys[i] * Hkv + kvh) * head_block + (kg * kBS + col) * 8;
+      const int sp = i >> 1, j = i & 1;  // PV step, tile within it
+      const int blk = phys[2 * sp + (col >> 3)];
+      const int tok = 8 * j + 4 * ((col >> 2) & 1) + (col & 3);
+      const bf16_t* kb = k_cache + ((long)blk * Hkv + kvh) * head_block + (kg * kBS + tok) * 8;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         kf[i][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + s * 4 * kBS * 8));
     }
 #pragma unroll
     for (int s = 0; s < kNS; ++s) {
-      // tokens 4kg .. 4kg + 3 of each block: contiguous at position v_perm(4kg) (common.h)
-      const bf16_t* va = v_cache + ((long)phys[2 * s] * Hkv + kvh) * head_block + v_perm(4 * kg) + col * kBS;
-      const bf16_t* vb = v_cache + ((long)phys[2 * s + 1] * Hkv + kvh) * head_block + v_perm(4 * kg) + col * kBS;
+      const bf16_t* vb = v_cache + ((long)phys[2 * s + (kg >> 1)] * Hkv + kvh) * head_block + col * kBS + 8 * (kg & 1);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        vlo[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(va + 16 * dt * kBS));
-        vhi[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + 16 * dt * kBS));
-      }
+      for (int dt = 0; dt < DT; ++dt)
+        vf[s][dt] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(vb + 16 * dt * kBS));
     }
   };
   KF kf0, kf1;
-  VF vlo0, vhi0, vlo1, vhi1;
+  VF vf0, vf1;
   // the first chunks' K/V loads fly while q is loaded (FQ: reduced from the slabs and rotated)
-  issue(kf0, vlo0, vhi0, c0);
+  issue(kf0, vf0, c0);
   if constexpr (DB) {
-    if (c0 + 1 < c1) issue(kf1, vlo1, vhi1, c0 + 1);
+    if (c0 + 1 < c1) issue(kf1, vf1, c0 + 1);
   }
 
   bf16x8 qf[KS];
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const KF& kf, const VF& vlo, const VF& vhi, int c) {
+  auto compute = [&](const KF& kf, const VF& vf, int c) {
     const int wtok0 = c * kCH + wave * kTW;
 
     // ---- scores, online softmax (per lane: head `col`)
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
     for (int i = 0; i < kNI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = wtok0 + 16 * i + 4 * kg + r;
+        const int t = wtok0 + 32 * (i >> 1) + 16 * (kg >> 1) + 8 * (i & 1) + 4 * (kg & 1) + r;
         const float v = (t < n_cached) ? sacc[i][r] * scale_log2 : -INFINITY;
         sacc[i][r] = v;
         mx = fmaxf(mx, v);
@@ -255,28 +259,24 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
         pb[4 + j] = (__bf16)sacc[2 * s + 1][j];
       }
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const bf16x8 a =
-            __builtin_bit_cast(bf16x8, make_uint4(vlo[s][dt][0], vlo[s][dt][1], vhi[s][dt][0], vhi[s][dt][1]));
-        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[dt], 0, 0, 0);
-      }
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][dt], pb, oacc[dt], 0, 0, 0);
     }
   };
   if constexpr (DB) {
     for (int c = c0; c < c1; c += 2) {
-      compute(kf0, vlo0, vhi0, c);
-      if (c + 2 < c1) issue(kf0, vlo0, vhi0, c + 2);
+      compute(kf0, vf0, c);
+      if (c + 2 < c1) issue(kf0, vf0, c + 2);
       __builtin_amdgcn_sched_barrier(0);  // chunk c + 2's loads go out before chunk c + 1's MFMAs
       if (c + 1 >= c1) break;
-      compute(kf1, vlo1, vhi1, c + 1);
-      if (c + 3 < c1) issue(kf1, vlo1, vhi1, c + 3);
+      compute(kf1, vf1, c + 1);
+      if (c + 3 < c1) issue(kf1, vf1, c + 3);
       __builtin_amdgcn_sched_barrier(0);
     }
   } else {
     for (int c = c0; c < c1; ++c) {
-      if (c != c0) issue(kf0, vlo0, vhi0, c);  // chunk c0's loads were issued before the q prologue
+      if (c != c0) issue(kf0, vf0, c);  // chunk c0's loads were issued before the q prologue
       __builtin_amdgcn_sched_barrier(0);  // keep every load above: none may wait behind an MFMA
-      compute(kf0, vlo0, vhi0, c);
+      compute(kf0, vf0, c);
     }
   }
 
