@@ -132,7 +132,7 @@ class ModelRunner:
             o += n
         cu = np.zeros(len(seqs) + 1, dtype=np.int32)
         cu[1:] = np.cumsum(lens)
-        qs, st = ops.prefill_qblocks(cu.tolist())
+        qs, st = ops.prefill_qblocks(cu.tolist(), ctx_starts=starts)
         t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dt, non_blocking=True)
         logits_idx = np.concatenate([np.arange(nd, dtype=np.int64), nd + cu[1:].astype(np.int64) - 1])
         meta = AttnMeta(is_prefill=True, positions=t(pos), slot_mapping=t(slots), cu_seqlens=t(cu),

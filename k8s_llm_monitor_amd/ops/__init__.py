@@ -629,16 +629,19 @@ def paged_decode_fused(slabs: torch.Tensor, nslabs: int, positions: torch.Tensor
     return out
 
 
-def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128) -> tuple[list[int], list[int]]:
+def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128,
+                    ctx_starts: Optional[list[int]] = None) -> tuple[list[int], list[int]]:
     """Q-block schedule for flash_prefill: (seq index, first q row) per 128-row block, heaviest
-    (largest first row, i.e. longest causal span) first so the tail of the grid is short."""
+    first so the tail of the grid is short.  A block's work is its causal key span: the sequence's
+    cached prefix (``ctx_starts``, chunked prefill) plus its first row."""
     items = []
     for i in range(len(cu_seqlens_cpu) - 1):
         n = cu_seqlens_cpu[i + 1] - cu_seqlens_cpu[i]
+        c = ctx_starts[i] if ctx_starts is not None else 0
         for s in range(0, n, block):
-            items.append((s, i))
+            items.append((c + s, s, i))
     items.sort(key=lambda t: -t[0])
-    return [i for _, i in items], [s for s, _ in items]
+    return [i for _, _, i in items], [s for _, s, _ in items]
 
 
 def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int, D: int, scale: float,
