@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s3 -o run -- python3 bench.py --steps 2 --warmup 1 > gpurun_out/prof_s3.log 2>&1 || { tail -30 gpurun_out/prof_s3.log; exit 1; }
 tail -1 gpurun_out/prof_s3.log | cut -c1-200
 f=$(find gpurun_out/prof_s3 -name "*results.db" | head -1)
-python3 tools/rocpd_summary.py $f --top 40 --title "session-3 headline bench (deferred-norm fix, DMA/MFMA interleave, one-round-trip add_norm_partial)" > gpurun_out/prof_s3_summary.md
+python3 tools/rocpd_summary.py $f --top 40 --title "session-3 final headline bench (deferred-norm fix, DMA/MFMA interleave, 16-byte decode V loads, span-ordered flash q-blocks)" > gpurun_out/prof_s3_summary.md
 python3 - "$f" > gpurun_out/prof_s3_steps.txt <<'PY'
 import sqlite3, sys
 c = sqlite3.connect(sys.argv[1])
