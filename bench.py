@@ -279,7 +279,10 @@ def run_rank(a) -> None:
         loadgen.close()
     ptoks = sum(r.get("prompt_tokens", 0) for r in ok)
     gtoks = sum(r.get("completion_tokens", 0) for r in ok)
-    _finish(a, ps, comm, elapsed, len(ok), ptoks, gtoks, res, stats, devices, eng, on_gpu)
+    # `value` counts complete answers: a production-mode answer cut at its deadline is reported
+    # separately (requests.deadline_truncated_rank0), not as a served query
+    n_full = sum(1 for r in ok if r.get("finish_reason") != "deadline")
+    _finish(a, ps, comm, elapsed, n_full, ptoks, gtoks, res, stats, devices, eng, on_gpu)
 
 
 def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, on_gpu) -> None:
@@ -341,7 +344,10 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
         out["requests"] = {"sent": len(res) * dp, "ok_rank0": len(ok), "rejected_503_rank0":
                            sum(r.get("http_status") == 503 for r in res),
                            "timeout_504_rank0": sum(r.get("http_status") == 504 for r in res),
-                           "deadline_truncated_rank0": sum(r.get("finish_reason") == "deadline" for r in ok)}
+                           "deadline_truncated_rank0": sum(r.get("finish_reason") == "deadline" for r in ok),
+                           "refused_cannot_finish_rank0": stats.get("infeasible_rejected"),
+                           "value_counts": "complete answers (deadline-truncated excluded)"}
+        out["tpot_model_ms"] = stats.get("tpot_model_ms")
         out["ttft_ms"] = {"p50": _pct(ttft, 0.5), "p99": _pct(ttft, 0.99)}
         out["tpot_ms"] = {"p50": _pct(tpot, 0.5), "p99": _pct(tpot, 0.99)}
         if a.mode == "poisson":

@@ -231,8 +231,11 @@ class LLMEngine:
             if q.status in (SeqStatus.FINISHED, SeqStatus.ABORTED):
                 continue  # stopped on the previous step; this step's token is discarded
             tok = int(tok)
-            i = q.output_ids.index(self.PENDING)
-            q.output_ids[i] = tok
+            out = q.output_ids
+            i = len(out) - 1  # placeholders trail the answer (at most two steps in flight): O(1)
+            while i > 0 and out[i - 1] == self.PENDING:
+                i -= 1
+            out[i] = tok
             self.counters["generated_tokens"] += 1
             if q.t_first_token is None:
                 q.t_first_token = now
@@ -265,6 +268,7 @@ class LLMEngine:
             self.bus.send_obj(self._pack(plan))
         if plan.is_prefill:
             toks = self.runner.prefill(plan.seqs, plan.decode)
+            self._check_collectives()  # prefill / mixed steps route small all-reduces through custom AR too
             self.counters["prefill_steps"] += 1
             if plan.decode:
                 self.counters["mixed_steps"] += 1
@@ -364,10 +368,12 @@ class LLMEngine:
                 h = self.runner.decode_launch_raw(*payload)
                 if pending is not None:  # keep at most two steps enqueued (staging is double-buffered)
                     self.runner.decode_collect(pending)
+                    self._check_collectives()
                 pending = h
                 continue
             if pending is not None:
                 self.runner.decode_collect(pending)
+                self._check_collectives()
                 pending = None
             if kind == KIND_STOP:
                 return
@@ -377,6 +383,7 @@ class LLMEngine:
                          for ids, bt, p, nc, ch in items]
                 dviews = [_View(None, n, bt, last, SamplingParams(*p)) for last, n, bt, p in dec]
                 self.runner.prefill(views, dviews)
+                self._check_collectives()
 
     def stop_workers(self) -> None:
         if self._inflight is not None:
@@ -391,6 +398,46 @@ def _params_t(p: SamplingParams) -> tuple:
 
 class _Skip(Exception):
     pass
+
+
+class TpotModel:
+    """Decode step time (ms) as a function of the batch size, learned online: an EWMA per batch
+    size seen, and a least-squares line t(b) = a + c*b over those sizes (a decode step streams the
+    weights once - the constant - plus per-row KV and activations - the slope).  ``estimate`` is
+    None until a step has been seen; with one size seen, that time is used for every size up to
+    it and grows in proportion beyond it."""
+
+    def __init__(self, alpha: float = 0.25):
+        self.alpha = alpha
+        self.ew: dict[int, float] = {}
+        self._fit: Optional[tuple] = None
+
+    def record(self, b: int, ms: float) -> None:
+        if b <= 0 or ms <= 0:
+            return
+        old = self.ew.get(b)
+        self.ew[b] = ms if old is None else (1 - self.alpha) * old + self.alpha * ms
+        self._fit = None
+
+    def estimate(self, b: int) -> Optional[float]:
+        if not self.ew:
+            return None
+        b = max(1, b)
+        if len(self.ew) == 1:
+            (b0, t0), = self.ew.items()
+            return t0 if b <= b0 else t0 * b / b0
+        if self._fit is None:
+            xs, ys = list(self.ew), list(self.ew.values())
+            n = len(xs)
+            mx, my = sum(xs) / n, sum(ys) / n
+            vx = sum((x - mx) ** 2 for x in xs)
+            c = max(0.0, sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / vx) if vx > 0 else 0.0
+            self._fit = (my - c * mx, c, min(ys))
+        a, c, lo = self._fit
+        return max(lo, a + c * b)
+
+    def snapshot(self) -> dict:
+        return {str(b): round(t, 3) for b, t in sorted(self.ew.items())}
 
 
 class EngineOverloaded(RuntimeError):
@@ -413,6 +460,12 @@ class EngineService:
     * deadlines - ``submit(deadline=...)`` stops the sequence at the deadline with finish_reason
       "deadline" (a truncated answer, KV freed), and a request still waiting when its deadline
       passes is dropped with EngineOverloaded;
+    * deadline-feasible admission - a waiting request with a deadline starts only when the learned
+      decode step time at the batch it would join (TpotModel) x its max_tokens, plus its prefill,
+      fits its deadline AND every running request's remaining tokens still fit theirs; a request
+      that cannot finish in time even once the first running answer completes is refused at once
+      (EngineOverloaded -> 503) instead of being truncated later (reference budget:
+      cmd/server/main.go:147-148 15 s write timeout, internal/config/config.go:145 llm.timeout);
     * cancellation - ``cancel(fut)`` aborts the sequence and frees its KV blocks before the next
       step;
     * step failures - an exception inside a step fails only the requests in flight, resets the
@@ -441,6 +494,10 @@ class EngineService:
         # prefill throughput estimate (tokens/s, EWMA over prefill steps) for deadline admission
         self._prefill_tps: Optional[float] = None
         self._waiting_est = 0  # prompt tokens waiting in the scheduler (engine thread writes)
+        self.tpot = TpotModel()
+        self.deadline_margin = 1.05  # safety factor on the estimated completion time
+        self.infeasible = 0  # refused because the answer could not finish before its deadline
+        engine.sched.admit_gate = self._admit_ok
         self._thread.start()
 
     @property
@@ -501,15 +558,73 @@ class EngineService:
                 self._streams.pop(s.seq_id, None)
                 self.cancelled += 1
 
-    def _expire_waiting(self) -> None:
-        """Drop waiting (not yet admitted) requests whose deadline has passed."""
+    def _prefill_s(self, seq: Sequence) -> float:
+        return (seq.num_tokens / self._prefill_tps) if self._prefill_tps else 0.0
+
+    def _admit_ok(self, seq: Sequence, n_after: int) -> bool:
+        """Scheduler admission gate (engine thread): does ``seq`` finish before its deadline at the
+        batch it would join, without pushing a running request past its own deadline?"""
+        t = self.tpot.estimate(n_after)
+        if t is None:
+            return True
         now = time.perf_counter()
-        for s in [s for s in self.engine.sched.waiting if s.deadline is not None and now >= s.deadline]:
-            self.engine.abort(s)
+        step_s = t * 1e-3 * self.deadline_margin
+        pre = self._prefill_s(seq)
+        if seq.deadline is not None and now + pre + seq.params.max_tokens * step_s > seq.deadline:
+            return False
+        for q in self.engine.sched.running:
+            if q.deadline is not None:
+                rem = max(0, q.params.max_tokens - len(q.output_ids))
+                if now + pre + rem * step_s > q.deadline:
+                    return False
+        return True
+
+    def _infeasible(self, seq: Sequence, now: float) -> bool:
+        """A never-started request that cannot finish before its deadline even if it starts when
+        the first running answer completes (or now, if the gate admits it now)."""
+        running = self.engine.sched.running
+        t = self.tpot.estimate(max(1, len(running)))
+        if t is None or seq.deadline is None:
+            return False
+        step_s = t * 1e-3 * self.deadline_margin
+        wait = 0.0
+        if not self._admit_ok(seq, len(running) + 1):
+            rem = [max(0, q.params.max_tokens - len(q.output_ids)) for q in running]
+            wait = min(rem) * step_s if rem else 0.0
+        return now + wait + self._prefill_s(seq) + seq.params.max_tokens * step_s > seq.deadline
+
+    def _expire_waiting(self) -> None:
+        """Waiting requests whose deadline has passed: one that never started is dropped
+        (EngineOverloaded, HTTP 503); a preempted one that already generated tokens ends with
+        finish_reason "deadline" and its partial answer, like a running sequence at its deadline."""
+        eng = self.engine
+        now = time.perf_counter()
+        for s in [s for s in eng.sched.waiting if s.deadline is not None and now >= s.deadline]:
+            partial = [t for t in s.output_ids if t >= 0]
+            if partial:
+                s.output_ids[:] = partial
+                s.t_finish = now
+                eng.counters["deadline_stops"] += 1
+                eng._finish(s, "deadline")
+                if self._streams:
+                    self._push_streams()
+                if isinstance(s.user, Future) and not s.user.done():
+                    self.latencies_ms.append(s.timings()["latency_ms"])
+                    s.user.set_result((eng.decode_text(s), s))
+                continue
+            eng.abort(s)
             self._streams.pop(s.seq_id, None)
             self.expired += 1
             if isinstance(s.user, Future) and not s.user.done():
                 s.user.set_exception(EngineOverloaded("request expired in the queue before it could start"))
+        # never-started requests that can no longer finish in time: refuse now, not at the deadline
+        for s in [s for s in eng.sched.waiting if s.deadline is not None and not s.output_ids
+                  and self._infeasible(s, now)]:
+            eng.abort(s)
+            self._streams.pop(s.seq_id, None)
+            self.infeasible += 1
+            if isinstance(s.user, Future) and not s.user.done():
+                s.user.set_exception(EngineOverloaded("the answer cannot finish before the deadline at the current load"))
 
     def _drain(self, block: bool) -> None:
         try:
@@ -576,8 +691,15 @@ class EngineService:
         if not eng.has_work():
             return
         p0, t0 = eng.counters["prefill_steps"], time.perf_counter()
+        d0 = eng.counters["decode_steps"]
+        paced = eng._inflight is not None or not eng.cfg.pipeline  # this step waits for a GPU step
         ptok0 = eng.runner.n_steps.get("prefill_tokens", 0)
         finished = eng.step()
+        if paced and eng.counters["decode_steps"] > d0 and eng.counters["prefill_steps"] == p0:
+            # decode-only step: with pipelining, launching step N waits for step N-1, so the
+            # interval is one GPU step at (about) this batch size
+            rows = eng._inflight[0] if eng._inflight is not None else eng.sched.running
+            self.tpot.record(len(rows), (time.perf_counter() - t0) * 1e3)
         if eng.counters["prefill_steps"] > p0:
             dt = time.perf_counter() - t0
             n = eng.runner.n_steps.get("prefill_tokens", 0) - ptok0
@@ -637,6 +759,8 @@ class EngineService:
         d["cancelled"] = self.cancelled
         d["rejected"] = self.rejected
         d["expired"] = self.expired
+        d["infeasible_rejected"] = self.infeasible
+        d["tpot_model_ms"] = self.tpot.snapshot()
         d["prefill_tokens_per_s_est"] = round(self._prefill_tps, 1) if self._prefill_tps else None
         d["healthy"] = self.healthy
         if self._error is not None:

@@ -84,7 +84,7 @@ class ModelRunner:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.n_steps = {"prefill": 0, "decode": 0}
-        self.on_launched = None  # hook after every decode launch (TP: enqueue the custom-AR error readback)
+        self.on_launched = None  # hook after every step's launch (TP: enqueue the custom-AR error readback)
 
     # --------------------------------------------------------------------- helpers
     def bucket_for(self, n: int) -> int:
@@ -165,6 +165,8 @@ class ModelRunner:
         topp = torch.tensor([s.params.top_p for s in rows], dtype=torch.float32).to(dev)
         tok = self._sample(logits, temp, topk, topp)
         self.n_steps["prefill"] += 1
+        if self.on_launched is not None:  # TP: the custom-AR error flag, read back with the tokens
+            self.on_launched()
         return tok[: len(rows)].cpu().tolist()
 
     # --------------------------------------------------------------------- decode

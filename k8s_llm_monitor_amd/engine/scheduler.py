@@ -75,6 +75,9 @@ class Scheduler:
         self.waiting: deque[Sequence] = deque()
         self.running: list[Sequence] = []
         self._stalled = 0  # consecutive prefill-only steps taken while decode rows were ready
+        # optional admission gate ``(seq, running_after) -> bool`` (EngineService: deadline-feasible
+        # admission); False keeps the head of the queue waiting (FIFO: nothing behind it starts)
+        self.admit_gate = None
 
     def add(self, seq: Sequence) -> None:
         if len(seq.prompt_ids) == 0:
@@ -144,6 +147,8 @@ class Scheduler:
                 seq = self.waiting[0]
                 n = seq.num_tokens - self.blocks.cached_prefix_tokens(seq)  # tokens left to compute
                 if n > budget and not self.cfg.chunked_prefill and plan.seqs:
+                    break
+                if self.admit_gate is not None and not self.admit_gate(seq, len(self.running) + 1):
                     break
                 if not self.blocks.can_allocate(seq) or not self.blocks.allocate(seq):
                     break  # allocate() undoes its prefix matches on failure: seq stays queued

@@ -772,7 +772,7 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
 
 
 def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] = None, swiglu: bool = False,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, algo: int = 0) -> torch.Tensor:
     """Prefill-sized ``x @ w^T`` on the 256 x 256 MFMA tile kernel (csrc/gemm_tile.hip).
 
     Dense: ``w`` [N, K].  Grouped: ``w`` [E, N, K] and ``offsets`` [E + 1] int32 device offsets of
@@ -798,7 +798,7 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
                 if b > a:
                     out[a:b] = one(x[a:b], w[e])
         return out
-    native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None, swiglu)
+    native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None, swiglu, algo)
     return out
 
 

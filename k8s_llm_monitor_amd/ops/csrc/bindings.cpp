@@ -40,7 +40,7 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E, long w_es,
-                     int epi, hipStream_t s);
+                     int epi, int algo, hipStream_t s);
 int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* offsets, int E, long rows, int N, int K,
                             long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
@@ -363,7 +363,8 @@ void moe_grouped_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, torch::
 // 256 x 256 MFMA GEMM (gemm_tile.hip) for prefill-sized projections: y = x . w^T, x [M, K], w [N, K]
 // (dense, offsets None) or w [E, N, K] with device offsets [E + 1] (grouped over expert-sorted rows,
 // no host sync).  swiglu: w gate/up-interleaved per 128 rows, y [M, N / 2] = silu(gate) * up.
-void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, bool swiglu) {
+void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, bool swiglu,
+               int64_t algo) {
   dev_bf16(y, "y"); dev_bf16(x, "x"); dev_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.is_contiguous() && y.is_contiguous(),
               "gemm_tile: x [M, K], w contiguous, y contiguous");
@@ -373,7 +374,12 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "gemm_tile: N % 256 == 0, K % 64 == 0");
+  if (algo == 0) {
+    TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
+                "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
+  } else {
+    TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "gemm_tile: N % 256 == 0, K % 64 == 0");
+  }
   TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (swiglu ? N / 2 : N), "gemm_tile: y shape");
   const int* op = nullptr;
   if (grouped) {
@@ -381,7 +387,8 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
     TORCH_CHECK(offsets->numel() == E + 1, "gemm_tile: offsets must hold E + 1 entries");
     op = offsets->data_ptr<int>();
   }
-  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, op, E, (long)N * K, swiglu ? 1 : 0, cur()),
+  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, op, E, (long)N * K, swiglu ? 1 : 0,
+                         (int)algo, cur()),
         "gemm_tile");
 }
 
@@ -748,7 +755,8 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("layer_norm", &layer_norm);
   m.def("silu_mul", &silu_mul);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
-  m.def("gemm_tile", &gemm_tile);
+  m.def("gemm_tile", &gemm_tile, py::arg("y"), py::arg("x"), py::arg("w"), py::arg("offsets"), py::arg("swiglu"),
+        py::arg("algo") = 0);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("embedding", &embedding);
   m.def("resolve_ids", &resolve_ids);

@@ -298,6 +298,205 @@ __global__ __launch_bounds__(512, 1) void gemm_tile256_kernel(const bf16_t* __re
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 4-wave variant: the same 256 x 256 output tile, but each wave owns a 128 x 128 quarter (64
+// accumulators of v_mfma_f32_16x16x32_bf16 = 256 f32 per lane, one wave per SIMD).  Per 32-deep k
+// step a wave reads 16 ds_read_b128 for 64 MFMAs (0.25 per MFMA, the 8-wave kernel above needs
+// 0.375) - the LDS-read pressure the round-2 ablation named as its limiter.
+//
+//  * K in 32-deep tiles; a tile = A 256 rows x 64 B + B 256 rows x 64 B = 32 KiB; a 4-slot LDS ring
+//    (128 KiB, one __shared__ array).  Tile t+4 is DMA'd into tile t's slot while tile t is
+//    computed from registers, so every fill has ~3 tiles (~3k cycles) to land.
+//  * fragments of tile t+1 are read (16 ds_read_b128) in between tile t's MFMAs into the second
+//    register set; one raw s_barrier per tile, preceded by lgkmcnt(0) and a counted vmcnt that
+//    leaves the two youngest tiles' DMAs in flight (never vmcnt(0) in the main loop).
+//  * 64-B LDS rows: logical 16-B chunk c of row r sits at physical chunk c ^ ((4 - ((r >> 2) & 3)) & 3)
+//    (applied to the DMA source address; the LDS side is lane-linear), which puts every
+//    16-lane group of a fragment ds_read_b128 on 16 distinct bank quads (rows 0-15, chunk l >> 4).
+__device__ __forceinline__ int swz64(int q) { return (4 - q) & 3; }
+
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EPI, bool GROUPED, int ABL = 0>  // ABL (diagnosis builds): 1 no MFMA, 2 no in-loop DMA
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                         bf16_t* __restrict__ Y, const int* __restrict__ offsets,
+                                                         int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
+  constexpr int SLOT = 32768, BOFF = 16384;
+  __shared__ __attribute__((aligned(16))) char smem[4 * SLOT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- logical tile: bijective XCD remap, then groups of 8 m-tiles ----
+  const int nwg = n_mt * n_nt;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = lid / (GM * n_nt), first_m = grp * GM;
+  const int gsz = min(n_mt - first_m, GM);
+  const int in_g = lid - grp * GM * n_nt;
+  const int mt = first_m + in_g % gsz, nt = in_g / gsz;
+
+  int row0, mrows;
+  const bf16_t* Wt = W;
+  if constexpr (GROUPED) {
+    int e = -1, acc_t = 0;
+    row0 = 0;
+    mrows = 0;
+    for (int x = 0; x < E; ++x) {
+      const int o0 = offsets[x], o1 = offsets[x + 1];
+      const int tiles = (o1 - o0 + 255) >> 8;
+      if (e < 0 && mt < acc_t + tiles) {
+        e = x;
+        row0 = o0 + (mt - acc_t) * 256;
+        mrows = min(256, o1 - row0);
+      }
+      acc_t += tiles;
+    }
+    if (e < 0) return;  // uniform: past the last expert's tiles
+    Wt = W + (long)e * w_es;
+  } else {
+    row0 = mt * 256;
+    mrows = min(256, M - row0);
+  }
+  const int n0 = nt * 256;
+  const int nrows = min(256, N - n0);
+
+  // ---- DMA: operand o (0 X, 1 W), piece p (0..3) covers 16-row group p * 4 + wave; lane ->
+  // row (lane >> 2) of the group, physical chunk lane & 3 ----
+  uint32_t soff[2][4];
+  {
+    const int cl = (lane & 3) ^ swz64((lane >> 4) & 3);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rl = (p * 4 + wave) * 16 + (lane >> 2);
+      soff[0][p] = (uint32_t)(((long)min(rl, mrows - 1) * K + cl * 8) * 2);  // rows past the end: clamped, never stored
+      soff[1][p] = (uint32_t)(((long)min(rl, nrows - 1) * K + cl * 8) * 2);
+    }
+  }
+  // buffer descriptors over this tile's X rows / W rows (built from wave-uniform values only, so
+  // hipcc keeps them in SGPRs: no waterfall loops, cdna_hip_programming.md T20); the DMA is
+  // buffer_load_dwordx4 ... lds with the lane's constant voffset and the k offset in soffset
+  auto rsrc = [](const void* base, long bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t xr = rsrc(reinterpret_cast<const char*>(X) + (long)row0 * K * 2, (long)mrows * K * 2);
+  const __amdgpu_buffer_rsrc_t wr = rsrc(reinterpret_cast<const char*>(Wt) + (long)n0 * K * 2, (long)nrows * K * 2);
+  const int nk = K >> 5;
+
+  // piece g (= o * 4 + p) of k-tile kt into ring slot `slot` & 3
+  auto piece = [&](int g, int kt, int slot) {
+    const int o = g >> 2, p = g & 3;
+    char* dst = smem + (slot & 3) * SLOT + o * BOFF + (p * 4 + wave) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], kt * 64, 0, 0);
+  };
+  auto issue_tile = [&](int kt, int slot) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) piece(g, kt, slot);
+  };
+
+  // fragment read: lane row lane & 15 of a 16-row block, logical chunk lane >> 4
+  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz64((lane >> 2) & 3)) << 4);
+  auto frag = [&](int kt, int o, int blk) -> bf16x8 {
+    const char* b = smem + (kt & 3) * SLOT + o * BOFF + ((o ? wn : wm) * 8 + blk) * 1024 + rd;
+    return *reinterpret_cast<const bf16x8*>(b);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // one k-tile: 64 MFMAs from (ca, cb); between them the fragments of tile t+1 into (na, nb) and
+  // the DMA of tile t+4 into tile t's slot; then lgkmcnt(0), vmcnt(16) (tiles t+3, t+4 stay in
+  // flight: tile t+2 has landed), one barrier.  Past the last tile the reads and DMAs are clamped
+  // to tile nk-1 (re-writing identical bytes into a slot nobody reads any more), so every step
+  // has the same body and the same counts.
+  auto step = [&](int t, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
+    const int tr = min(t + 1, nk - 1), tl = min(t + 4, nk - 1);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (ABL == 1) {
+          asm volatile("" ::"v"(cb[j]), "v"(ca[g]));  // keep the fragment reads alive
+        } else {
+          acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      na[g] = frag(tr, 0, g);
+      nb[g] = frag(tr, 1, g);
+      if constexpr (ABL != 2) piece(g, tl, t);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    lgkm_wait0();
+    vm_wait_n<16>();
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // prologue: tiles 0..3 in flight (clamped); tile 0 read synchronously; tile 1 landed before the loop
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) issue_tile(min(kt, nk - 1), kt);
+  vm_wait_n<24>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    fa0[g] = frag(0, 0, g);
+    fb0[g] = frag(0, 1, g);
+  }
+  lgkm_wait0();
+  vm_wait_n<16>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < nk; t += 2) {  // nk even (K % 64 == 0)
+    step(t, fa0, fb0, fa1, fb1);
+    step(t + 1, fa1, fb1, fa0, fb0);
+  }
+  vm_wait_n<0>();
+
+  // ---- epilogue: acc[i][j][r] = Y[m][n], m = wm*128 + i*16 + (lane & 15),
+  // n = wn*128 + j*16 + 4 (lane >> 4) + r ----
+  const int ml = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    __builtin_amdgcn_sched_barrier(0);  // one row block's accumulators at a time (no hoisted AGPR reads)
+    const int m = wm * 128 + i * 16 + ml;
+    if (m >= mrows) continue;
+    if constexpr (EPI == TILE_EPI_SWIGLU) {
+      bf16_t* yrow = Y + (long)(row0 + m) * (N >> 1) + ((n0 + wn * 128) >> 1) + nq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = bf2f(f2bf(acc[i][j][r])), up = bf2f(f2bf(acc[i][j + 4][r]));
+          o[r] = gt * up / (1.f + __expf(-gt));
+        }
+        *reinterpret_cast<uint2*>(yrow + j * 16) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      }
+    } else {
+      bf16_t* yrow = Y + (long)(row0 + m) * N + n0 + wn * 128 + nq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (wn * 128 + j * 16 >= nrows) break;
+        const f32x4 v = acc[i][j];
+        *reinterpret_cast<uint2*>(yrow + j * 16) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
@@ -305,28 +504,49 @@ using namespace k8sllm;
 // Dense (offsets == nullptr): Y [M][N] (SwiGLU: [M][N / 2]) = X [M][K] . W[N][K]^T.
 // Grouped: W [E][N][K] with expert stride w_es elements; M = total expert-sorted rows (the grid
 // bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
+// algo 0: 4-wave 128 x 128 wave tiles (gemm_w4_kernel, N % 16 == 0, K % 64 == 0; SwiGLU N % 256);
+// algo 1: 8-wave 128 x 64 wave tiles (gemm_tile256_kernel, N % 256 == 0, K % 64 == 0).
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
-                                long w_es, int epi, hipStream_t s) {
+                                long w_es, int epi, int algo, hipStream_t s) {
   if (M <= 0) return 0;
-  if (N % 256 != 0 || K % 64 != 0 || K < 64) return -1;
   const bool grouped = offsets != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
-  // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert)
-  if ((long)N * K * 2 >= (1L << 31)) return -3;
-  const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = N / 256;
+  if (algo == 0) {
+    if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
+  } else if (N % 256 != 0 || K % 64 != 0 || K < 64) {
+    return -1;
+  }
+  // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert / n-tile)
+  if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
+  const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = (N + 255) / 256;
   const long nwg = (long)n_mt * n_nt;
   if (nwg > (1L << 30)) return -2;
-  dim3 grid((unsigned)nwg), blk(512);
-#define K8_TILE_LAUNCH(EPI_, G_)                                                                                  \
-  hipLaunchKernelGGL((gemm_tile256_kernel<EPI_, G_>), grid, blk, 0, s, (const bf16_t*)X, (const bf16_t*)W,      \
-                     (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
-  if (grouped) {
-    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true);
-    else K8_TILE_LAUNCH(TILE_EPI_BF16, true);
-  } else {
-    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false);
-    else K8_TILE_LAUNCH(TILE_EPI_BF16, false);
+  dim3 grid((unsigned)nwg);
+#define K8_TILE_LAUNCH(KER_, NT_, EPI_, G_)                                                                         \
+  hipLaunchKernelGGL((KER_<EPI_, G_>), grid, dim3(NT_), 0, s, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y,     \
+                     offsets, E, M, N, K, w_es, n_mt, n_nt)
+#define K8_TILE_EPI(KER_, NT_)                                                                                     \
+  if (grouped) {                                                                                                   \
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_SWIGLU, true);                                  \
+    else K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_BF16, true);                                                          \
+  } else {                                                                                                         \
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_SWIGLU, false);                                 \
+    else K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_BF16, false);                                                         \
   }
+  if (algo == 0) {
+    K8_TILE_EPI(gemm_w4_kernel, 256)
+  } else if (algo == 10 || algo == 11) {  // diagnosis builds of the 4-wave kernel (dense, bf16 out)
+    if (grouped || epi != TILE_EPI_BF16) return -1;
+    if (algo == 10)
+      hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 1>), grid, dim3(256), 0, s, (const bf16_t*)X,
+                         (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);
+    else
+      hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 2>), grid, dim3(256), 0, s, (const bf16_t*)X,
+                         (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);
+  } else {
+    K8_TILE_EPI(gemm_tile256_kernel, 512)
+  }
+#undef K8_TILE_EPI
 #undef K8_TILE_LAUNCH
   return (int)hipGetLastError();
 }

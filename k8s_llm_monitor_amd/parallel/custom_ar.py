@@ -10,10 +10,15 @@ buffer (prefill activations) keep RCCL (``parallel/comm.tp_all_reduce`` picks pe
 The same protocol provides a one-shot all-gather (the vocab-parallel logits, C-4), so a TP decode
 step captured in a hipGraph contains no RCCL call at all.
 
-On by default at TP 2..8 on the GPU (``K8SLLM_CUSTOM_AR=0`` keeps RCCL for everything): validated
-on one MI355X with two processes sharing the GPU (tests/test_custom_ar.py, tests/test_tp_gpu.py).
+On by default at TP 2..8 on the GPU (``K8SLLM_CUSTOM_AR=0`` keeps RCCL for everything), but only
+after a startup self-test on the actual devices is exact (``self_test``: integer-valued bf16
+all-reduces and all-gathers of several sizes against CPU-group references, exact in any summation
+order, as RCCL's are);
+a rank that sees a mismatch or a raised error flag turns it off on every rank of the group.
+Validated on one MI355X with two processes sharing the GPU (tests/test_custom_ar.py,
+tests/test_tp_gpu.py); no multi-GPU xGMI run exists yet, which is what the self-test guards.
 A call whose peer never arrives sets the error flag instead of hanging; the engine enqueues a copy
-of the flag after every decode step (``error_async``) and fails the step if it was set.
+of the flag after every step (``error_async``) and fails the step if it was set.
 """
 from __future__ import annotations
 
@@ -86,8 +91,49 @@ def enabled() -> bool:
     return os.environ.get("K8SLLM_CUSTOM_AR", "1") != "0"
 
 
+def self_test(car: CustomAllReduce, ps, sizes=None) -> bool:
+    """Collective over the TP group: the custom all-reduce / all-gather on the real devices against
+    exact references built over the CPU group, on integer-valued bf16 data (sums stay integers
+    < 256, exact in any summation order - what RCCL returns too).  True on every rank only if every
+    rank passed."""
+    dev = ps.device
+    sizes = sizes or (8, 4096, 64 * 4096, car.max_elems)
+    ok = True
+    try:
+        for n in sizes:
+            n = max(8, min(int(n), car.max_elems)) // 8 * 8
+            g = torch.Generator().manual_seed(7919 + n)
+            xc = (torch.randint(-8, 9, (n,), generator=g) + ps.tp_rank).to(torch.bfloat16)
+            x = xc.to(dev)
+            y = car.all_reduce(x)
+            m = min(n, car.max_elems // car.world // 8 * 8)
+            gat = car.all_gather(x[:m].contiguous())
+            # references over the CPU group: exact integer sums / the ranks' slices
+            ref = xc.float()
+            dist.all_reduce(ref, group=ps.cpu_group)
+            gref = [torch.empty_like(xc[:m]) for _ in range(car.world)]
+            dist.all_gather(gref, xc[:m].contiguous(), group=ps.cpu_group)
+            torch.cuda.synchronize(dev)
+            ok = (ok and torch.equal(y.cpu(), ref.to(torch.bfloat16)) and torch.equal(gat.cpu(), torch.stack(gref))
+                  and not car.error())
+    except Exception:  # noqa: BLE001 - any failure disables the custom path
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ps.cpu_group)
+    return bool(flag.item())
+
+
 def maybe_create(ps) -> Optional[CustomAllReduce]:
-    """Collective over the TP group: a CustomAllReduce on the GPU at TP 2..8 (unless disabled)."""
+    """Collective over the TP group: a CustomAllReduce on the GPU at TP 2..8 (unless disabled),
+    kept only if its startup self-test against RCCL passes on every rank."""
     if not (enabled() and ps.tp_size > 1 and ps.tp_size <= 8 and ps.device.type == "cuda"):
         return None
-    return CustomAllReduce(ps.tp_rank, ps.tp_size, cpu_group=ps.cpu_group)
+    car = CustomAllReduce(ps.tp_rank, ps.tp_size, cpu_group=ps.cpu_group)
+    if os.environ.get("K8SLLM_CUSTOM_AR_SELFTEST", "1") != "0" and not self_test(car, ps):
+        import logging
+
+        logging.getLogger("parallel").warning("custom all-reduce failed its startup self-test: RCCL carries "
+                                              "every TP collective")
+        car.close()
+        return None
+    return car

@@ -11,8 +11,11 @@ Layout of the world:
 * ``dp``  - independent engine replicas (``world // tp``).  No collectives on the hot path; the
             control plane routes requests round-robin.
 * ``ep``  - expert parallel for Mixtral shares the TP group: attention activations are already
-            replicated across it, so each rank runs its local experts on the tokens routed to
-            them and the partial outputs are summed by the same all-reduce the dense MLP uses.
+            replicated across it and each rank owns n_experts / tp experts.  Prefill dispatches
+            (token, expert) rows to the owning rank by all-to-all and combines them by the reverse
+            all-to-all (models/llama.py ``_moe_a2a``, the default, ``K8SLLM_MOE_COMM``); decode
+            runs every local expert on the replicated rows and sums by all-reduce, or by the
+            static-capacity all-to-all (``K8SLLM_MOE_DECODE=a2a``).
 
 The reference has no GPU communication at all (SURVEY.md §2.11 "There is no NCCL, MPI, Gloo").
 """
@@ -112,7 +115,7 @@ def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optio
                 st.tp_group, st.cpu_group = grp, cpu
         from .custom_ar import maybe_create
 
-        st.custom_ar = maybe_create(st)  # K8SLLM_CUSTOM_AR=1, GPU, TP 2..8; else RCCL only
+        st.custom_ar = maybe_create(st)  # GPU, TP 2..8, self-test vs RCCL passed (K8SLLM_CUSTOM_AR=0: off)
     set_state(st)
     return st
 

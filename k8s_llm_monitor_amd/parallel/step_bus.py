@@ -62,7 +62,11 @@ class ShmStepBus:
     """Leader publishes into a native shared-memory ring; worker ``tp_rank - 1`` is reader index
     ``tp_rank - 1``.  Collective over the TP group's CPU group (name exchange + barrier)."""
 
-    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 600.0):
+    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 600.0, poll_s: float = 1.0):
+        """``timeout_s`` bounds the LEADER's publish back-pressure (a worker that stopped consuming).
+        A worker waits for the next step without a deadline - an idle server publishes nothing for
+        as long as no request arrives - and polls the leader's liveness every ``poll_s`` instead,
+        so a dead leader still surfaces (ConnectionError) rather than hanging the worker."""
         from ..runtime import native_runtime
 
         rt = native_runtime()
@@ -70,6 +74,7 @@ class ShmStepBus:
             raise RuntimeError("native StepChannel unavailable")
         self.ps = ps
         self.timeout_s = timeout_s
+        self.poll_s = poll_s
         src = ps.rank - ps.tp_rank
         name = [f"/k8sllm_step_{os.getpid()}_{uuid.uuid4().hex[:12]}" if ps.tp_rank == 0 else None]
         ok = [True]
@@ -86,6 +91,7 @@ class ShmStepBus:
                 ok[0] = False
         oks: list = [None] * ps.tp_size  # every rank learns whether every rank has the channel
         dist.all_gather_object(oks, ok[0], group=ps.cpu_group)
+        self.leader_pid = int(name[0].split("_")[2])  # TP ranks share a node (shared memory)
         if ps.tp_rank == 0 and ok[0]:
             self.ch.unlink()  # every rank that could map it has: the name is no longer needed
         if not all(oks):
@@ -108,13 +114,34 @@ class ShmStepBus:
         self._publish(struct.pack("<i", KIND_STOP))
 
     def recv(self) -> bytes:
-        m = self.ch.recv(self.reader, self.timeout_s)
-        if m is None:
-            raise TimeoutError("no step from the TP leader within the step-bus timeout")
-        return m
+        while True:
+            m = self.ch.recv(self.reader, self.poll_s)
+            if m is not None:
+                return m
+            if not _pid_alive(self.leader_pid):
+                raise ConnectionError(f"TP leader (pid {self.leader_pid}) exited without sending STOP")
 
     def close(self) -> None:
         self.ch.close()
+
+
+def _pid_alive(pid: int) -> bool:
+    """False once ``pid`` has exited - including an exited but not yet reaped (zombie) process,
+    which signal 0 would still report as present."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            return f.read().rsplit(b")", 1)[1].split()[0] not in (b"Z", b"X")
+    except FileNotFoundError:
+        return False
+    except OSError:  # no procfs: fall back to signal 0
+        pass
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:  # exists, owned by someone else
+        return True
+    return True
 
 
 def make_step_bus(ps, slot_bytes: int):

@@ -173,3 +173,26 @@ def test_dev_mode_script_without_cluster():
     r = subprocess.run(["bash", "scripts/test_with_mock_k8s.sh", str(port)], capture_output=True, text=True,
                        timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_web_console_pages(mon):
+    """W1/W2: both pages are served, every API path they poll answers 200 on a live monitor, and
+    the console's status/error bar, manual refresh (with loading state) and UAV/CRD summary card
+    are present (reference web/index.html:537-621,796, web/metrics.html:244)."""
+    import re
+
+    a = mon.app
+    for page in ("/", "/metrics.html"):
+        r = a.handle("GET", page)
+        assert r.code == 200 and r.ctype.startswith("text/html"), page
+    assert a.handle("GET", "/index.html").code == 301  # Go FileServer: /index.html -> ./
+    idx = a.handle("GET", "/").body.decode()
+    met = a.handle("GET", "/metrics.html").body.decode()
+    for needle in ('id="status"', 'id="refresh"', "刷新中…", "活跃 UAV / CRD 记录", 'id="nodeCount"', 'id="podCount"',
+                   "errors.push"):
+        assert needle in idx, needle
+    assert 'id="reload"' in met and 'id="err"' in met and "errs.push" in met
+    for path in sorted(set(re.findall(r"'(/api/v1/[a-z/]+)'", idx + met))):
+        if path in ("/api/v1/query", "/api/v1/metrics/engine"):  # POST-only / optional (no engine here)
+            continue
+        assert a.handle("GET", path).code == 200, path

@@ -24,28 +24,56 @@ def _close(a, b, atol, rtol=0.0, what=""):
     assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.4g}"
 
 
+ALGOS = [0, 1]  # 0: 4-wave 128 x 128 wave tiles (prefill default), 1: 8-wave 128 x 64
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (255, 512, 128), (300, 256, 192), (1000, 1536, 1024),
-                                   (2048, 768, 4096), (513, 512, 14336 // 4)])
-def test_gemm_tile_dense(M, N, K):
+                                   (2048, 768, 4096), (513, 512, 14336 // 4), (4096, 1024, 640)])
+def test_gemm_tile_dense(M, N, K, algo):
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
-    y = ops.gemm_tile(x, w)
+    y = ops.gemm_tile(x, w, algo=algo)
     _close(y.cpu(), F_.linear(x.cpu().float(), w.cpu().float()), atol=3e-2, rtol=2e-2, what=f"dense {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N", [(77, 400), (600, 16), (257, 1296)])
+def test_gemm_tile_w4_n_tail(M, N):
+    """The 4-wave kernel takes any N % 16 == 0 (partial last n-tile: clamped DMA rows, masked stores)."""
+    K = 320
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    y = ops.gemm_tile(x, w, algo=0)
+    _close(y.cpu(), F_.linear(x.cpu().float(), w.cpu().float()), atol=3e-2, rtol=2e-2, what=f"tail {M}x{N}")
+
+
+def test_gemm_tile_w4_asymmetric_identity():
+    """A = I with an asymmetric B: a transposed C-write or a swapped fragment map cannot pass."""
+    K = 256
+    x = torch.zeros(256, K, device=DEV, dtype=torch.bfloat16)
+    x[:, :] = torch.eye(256, K, device=DEV, dtype=torch.bfloat16)
+    n = torch.arange(512, device=DEV).float()[:, None]
+    k = torch.arange(K, device=DEV).float()[None, :]
+    w = ((n * 3 + k * 7) % 61 - 30).to(torch.bfloat16)  # small integers: exact in bf16
+    y = ops.gemm_tile(x, w, algo=0)
+    assert torch.equal(y.float().cpu(), w.float().t().cpu()[:256])
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("M", [7, 700])
-def test_gemm_tile_swiglu(M):
+def test_gemm_tile_swiglu(M, algo):
     K, F = 512, 768
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w13 = (torch.randn(2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
-    y = ops.gemm_tile(x, ops.interleave_gate_up(w13).contiguous(), swiglu=True)
+    y = ops.gemm_tile(x, ops.interleave_gate_up(w13).contiguous(), swiglu=True, algo=algo)
     r = ref.silu_mul(F_.linear(x.cpu().float(), w13.cpu().float()).to(torch.bfloat16))
     _close(y.cpu(), r, atol=3e-2, rtol=2e-2, what="swiglu")
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("counts", [[300, 0, 129, 1], [256, 512, 5, 700, 0, 0, 33, 64], [1]])
 @pytest.mark.parametrize("swiglu", [False, True])
-def test_gemm_tile_grouped(counts, swiglu):
+def test_gemm_tile_grouped(counts, swiglu, algo):
     E, K, N = len(counts), 512, 512
     rows = sum(counts)
     x = torch.randn(rows, K, device=DEV, dtype=torch.bfloat16)
@@ -53,7 +81,7 @@ def test_gemm_tile_grouped(counts, swiglu):
     if swiglu:
         w = torch.stack([ops.interleave_gate_up(we) for we in w]).contiguous()
     off = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device=DEV)
-    y = ops.gemm_tile(x, w, off, swiglu=swiglu)
+    y = ops.gemm_tile(x, w, off, swiglu=swiglu, algo=algo)
     o = 0
     for e, n in enumerate(counts):
         if n:

@@ -147,3 +147,68 @@ def test_moe_all_to_all_matches_allreduce_and_tp1():
     for rank, errs in res:
         assert not isinstance(errs, str), errs
         assert max(errs) < 2e-3, f"rank {rank}: {errs}"
+
+
+def _idle_worker(rank, world, port, q, leader_dies):
+    """An idle TP leader (no request for longer than the step-bus timeout) must not kill its
+    worker; a leader that exits without STOP must surface on the worker as ConnectionError."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), K8SLLM_STEP_BUS="shm")
+    torch.set_num_threads(2)
+    from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from k8s_llm_monitor_amd.parallel.state import init_parallel
+
+    try:
+        ps = init_parallel(tp_size=world, device="cpu")
+        ecfg = EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=128, num_blocks=64, use_graphs=False,
+                            seed=5, dtype="float32")
+        eng = LLMEngine(ecfg, device="cpu", pstate=ps)
+        eng.bus.timeout_s, eng.bus.poll_s = 0.3, 0.1  # the idle gap below is 10x the bus timeout
+        if ps.tp_rank == 0:
+            time.sleep(3.0)
+            if leader_dies:
+                _put_and_exit(q, (rank, "exit"), 0)  # no STOP, no teardown
+            seqs = [eng.add_request("node NotReady", SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))]
+            while eng.has_work():
+                eng.step()
+            eng.stop_workers()
+            q.put((rank, seqs[0].output_ids))
+        else:
+            try:
+                eng.worker_loop()
+                q.put((rank, "stopped"))
+            except ConnectionError as e:
+                q.put((rank, f"conn:{e}"))
+        _put_and_exit(q, None, 0)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        _put_and_exit(q, (rank, "ERR " + repr(e) + traceback.format_exc()), 1)
+
+
+def _put_and_exit(q, item, code):
+    if item is not None:
+        q.put(item)
+    q.close()
+    q.join_thread()  # flush the queue's feeder thread before the hard exit
+    os._exit(code)
+
+
+@pytest.mark.parametrize("leader_dies", [False, True])
+def test_step_bus_idle_leader(leader_dies):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_worker, args=(r, 2, port, q, leader_dies)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert not any(isinstance(v, str) and v.startswith("ERR") for v in res.values()), res
+    if leader_dies:
+        assert res[0] == "exit" and res[1].startswith("conn:"), res
+    else:
+        assert len(res[0]) == 4 and res[1] == "stopped", res

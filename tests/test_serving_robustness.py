@@ -248,3 +248,45 @@ def test_http_flood_sees_503_not_504_and_frees_kv():
         srv.shutdown()
         svc.close()
     assert eng.blocks.num_free == eng.runner.num_blocks
+
+
+def test_tpot_model_fit():
+    from k8s_llm_monitor_amd.engine.engine import TpotModel
+
+    m = TpotModel(alpha=1.0)
+    assert m.estimate(4) is None
+    m.record(8, 40.0)
+    assert m.estimate(4) == 40.0 and m.estimate(16) == 80.0  # one size: flat below, proportional above
+    m.record(1, 10.0)
+    m.record(64, 280.0)
+    assert abs(m.estimate(32) - (10.0 + 270.0 / 63 * 31)) < 2.0  # the line through the points
+    assert m.estimate(0) >= 10.0
+
+
+def test_deadline_feasible_admission_refuses_instead_of_truncating():
+    """with a learned step time that makes only a few answers fit the deadline,
+    the service starts only those (every one completes, none is deadline-truncated) and refuses
+    the rest at once with EngineOverloaded (HTTP 503) instead of truncating them later."""
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_model_len=512, num_blocks=256,
+                                 use_graphs=False, seed=3, dtype="float32", admit_window_ms=0), device="cpu")
+    svc = EngineService(eng)
+    try:
+        # frozen step-time model: 20 ms at batch 1, +20 ms per extra row (CPU steps are far faster,
+        # so admitted answers finish well inside their deadline)
+        svc.tpot.record(1, 20.0)
+        svc.tpot.record(8, 160.0)
+        svc.tpot.record = lambda *a, **k: None
+        sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+        deadline = time.perf_counter() + 2.0  # 24 steps fit up to ~3 rows (24 * 60 ms * 1.05 = 1.5 s)
+        futs = [svc.submit(f"pod-{i} CrashLoopBackOff, why?", sp, deadline=deadline) for i in range(8)]
+        ok, refused = [], 0
+        for f in futs:
+            try:
+                ok.append(f.result(timeout=60)[1])
+            except EngineOverloaded:
+                refused += 1
+        assert 1 <= len(ok) <= 4 and refused == 8 - len(ok), (len(ok), refused)
+        assert all(s.finish_reason == "length" and len(s.output_ids) == 24 for s in ok)
+        assert svc.stats()["infeasible_rejected"] == refused
+    finally:
+        svc.close()

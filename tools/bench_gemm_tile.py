@@ -42,14 +42,18 @@ def main() -> None:
         xin = xf if K == F else x
         y = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
         cases.append((name, 2 * T * N * K, {
-            "tile": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y)),
+            "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
+            "w4_nomfma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=10)),
+            "w4_nodma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=11)),
+            "tile": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
             "hipblaslt": (lambda i, xin=xin, w=w, y=y: torch.matmul(xin, w.t(), out=y)),
         }))
     w13 = ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02).contiguous()
     gu = torch.empty(T, 2 * F, device=dev, dtype=torch.bfloat16)
     act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
-        "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act)),
+        "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
+        "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
         "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
         "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
     }))
@@ -80,12 +84,14 @@ def main() -> None:
                 torch.matmul(hs[lo:hi], we2[e].t(), out=ys[lo:hi])
 
     cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
-        "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha)),
+        "w4": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=0)),
+        "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
         "hipblaslt_loop": loop13,
     }))
     cases.append(("moe_w2", 2 * rows * d * F, {
-        "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys)),
+        "w4": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=0)),
+        "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
         "hipblaslt_loop": loop2,
     }))
