@@ -519,8 +519,9 @@ class CausalLM:
         Per layer at decode (5-7 launches): qkv skinny (split-K slabs) -> paged_decode_fused (slab
         reduce, RoPE, KV write, attention) -> o skinny (slabs) -> add_norm_partial (residual add,
         deferred mlp norm) -> gate_up skinny with the SwiGLU epilogue -> down skinny (slabs) ->
-        add_norm_partial.  TP>1: the row-parallel o / down sum their slabs to bf16 (reduce_slabs),
-        all-reduce over RCCL / the one-shot IPC all-reduce, then fused_add_rms_norm.
+        add_norm_partial.  TP>1: each row-parallel o / down tail is ONE launch with the IPC
+        all-reduce (slab sum + all-reduce + residual add + RMSNorm + packed A: _tp_tail); over
+        RCCL, reduce_slabs + all-reduce + fused_add_rms_norm + pack_activation.
         On the CPU the same ops run as fp32 references with the kernels' split-K slicing, so the
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
@@ -604,8 +605,10 @@ class CausalLM:
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
                 # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated
                 # MLP output comes back from _moe_a2a_decode
-                y = self._row_parallel_sum(ws, ns, M, residual)
-                xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], eps)
+                xn = self._tp_tail(ws, ns, residual, L["mlp_norm"], packed=False)
+                if xn is None:
+                    xn = ops.fused_add_rms_norm(self._row_parallel_sum(ws, ns, M, residual), residual,
+                                                L["mlp_norm"], eps)
                 z = self._moe_a2a_decode(L, xn)
                 nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
                 xr = ops.fused_add_rms_norm(z, residual, nw, eps)
@@ -625,6 +628,9 @@ class CausalLM:
         if self._fuse_resnorm:
             x = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, None, 0, self.final_norm, eps)
             return self._logits(x)
+        x = self._tp_tail(ws, ns, residual, self.final_norm, packed=False)
+        if x is not None:
+            return self._logits(x)
         x = self._row_parallel_sum(ws, ns, M, residual)
         if x is None:
             x = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, self.final_norm, eps)
@@ -641,15 +647,29 @@ class CausalLM:
         chosen) - the caller's residual-add kernel summing the slabs is the expert combine.  Host
         sync free, so the step stays in the decode hipGraph."""
         c = self.cfg
-        y = self._row_parallel_sum(ws, ns, M, residual)
-        if y is None:
-            xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps)
-        else:
-            xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
+        xn = self._tp_tail(ws, ns, residual, L["mlp_norm"], packed=False)
+        if xn is None:
+            y = self._row_parallel_sum(ws, ns, M, residual)
+            if y is None:
+                xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps)
+            else:
+                xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
         ids, w = ops.moe_route(F.linear(xn, L["router"]).float(), c.top_k_experts, True)
         wd = torch.zeros(M, c.n_experts, dtype=torch.float32, device=xn.device).scatter_(1, ids.long(), w)
         act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
+
+    def _tp_tail(self, ws, ns: int, residual: torch.Tensor, norm_w, packed: bool) -> Optional[torch.Tensor]:
+        """TP>1 on the GPU with the IPC all-reduce: the row-parallel tail (slab sum, all-reduce,
+        residual add, RMSNorm, the next GEMM's input layout) as ONE fused launch
+        (custom_ar.hip car_fused_tail_kernel); None where it does not apply."""
+        car = self.ps.custom_ar
+        M, d = residual.shape
+        if self.tp == 1 or ns == 0 or car is None or not residual.is_cuda or not car.fits_tail(M, d):
+            return None
+        out = (ops.packed_empty(M, d, residual.dtype, residual.device) if packed
+               else torch.empty_like(residual))
+        return car.fused_tail(ws, ns, residual, norm_w, self.cfg.norm_eps, out, packed)
 
     def _row_parallel_sum(self, ws, ns: int, M: int, residual: torch.Tensor) -> Optional[torch.Tensor]:
         """TP>1: the row-parallel projection's slabs summed to bf16 and all-reduced; None at TP=1."""
@@ -661,6 +681,9 @@ class CausalLM:
     def _norm_tail(self, residual: torch.Tensor, ws, ns: int, norm_w, rows: Optional[int] = None) -> tuple:
         """residual += the projection's slabs; returns (A operand for the next skinny GEMM, rownorm)."""
         eps = self.cfg.norm_eps
+        xp = self._tp_tail(ws, ns, residual, norm_w, packed=True)
+        if xp is not None:
+            return xp, None
         y = self._row_parallel_sum(ws, ns, residual.shape[0], residual)
         if y is not None:  # TP>1: all-reduced partial sums, complete norm, packed A
             return ops.pack_activation(ops.fused_add_rms_norm(y, residual, norm_w, eps)), None

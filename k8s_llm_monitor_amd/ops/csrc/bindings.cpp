@@ -62,7 +62,9 @@ int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, i
 void* k8sllm_car_create(int rank, int world, long max_elems, void* handles, int* err);
 int k8sllm_car_handle_size();
 int k8sllm_car_open(void* state, const void* all_handles);
-int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
+int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, int algo, hipStream_t s);
+int k8sllm_car_fused_tail(void* state, const float* slabs, int ns, long slab_stride, void* residual, const void* w,
+                          void* out, long ldo, int M, int d, float eps, int packed, long spin_limit, hipStream_t s);
 int k8sllm_car_error(void* state);
 int k8sllm_car_all_gather(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
 int k8sllm_car_error_async(void* state, void* host_dst, hipStream_t s);
@@ -374,7 +376,7 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  if (algo == 0) {
+  if (algo == 0 || algo == 2) {
     TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
                 "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
   } else {
@@ -722,12 +724,30 @@ void car_open(int64_t state, py::bytes all_handles) {
   check(k8sllm_car_open((void*)(intptr_t)state, a.data()), "car_open (hipIpcOpenMemHandle)");
 }
 
-void car_all_reduce(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit) {
+void car_all_reduce(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit, int64_t algo) {
   dev_bf16(in, "in"); dev_bf16(out, "out");
   TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "car_all_reduce layout");
   check(k8sllm_car_all_reduce((void*)(intptr_t)state, in.data_ptr(), out.data_ptr(), (long)in.numel(),
-                              (long)spin_limit, cur()),
+                              (long)spin_limit, (int)algo, cur()),
         "car_all_reduce");
+}
+
+// TP row-parallel tail in one launch: slabs [ns, M, d] fp32 -> reduced over ranks -> residual +=,
+// RMSNorm * w -> out (row-major [M, d] or fragment-packed when packed).
+void car_fused_tail(int64_t state, torch::Tensor slabs, int64_t ns, torch::Tensor residual, torch::Tensor w,
+                    torch::Tensor out, double eps, bool packed, int64_t spin_limit) {
+  dev_bf16(residual, "residual"); dev_bf16(w, "w"); dev_bf16(out, "out");
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == torch::kFloat32 && slabs.is_contiguous(), "slabs fp32");
+  TORCH_CHECK(residual.dim() == 2 && residual.is_contiguous() && w.is_contiguous() && out.is_contiguous(),
+              "car_fused_tail layout");
+  const int M = (int)residual.size(0), d = (int)residual.size(1);
+  TORCH_CHECK(slabs.numel() >= ns * (long)M * d && w.numel() == d, "car_fused_tail sizes");
+  TORCH_CHECK(packed ? out.numel() >= (long)((M + 15) / 16) * 16 * d : out.numel() >= (long)M * d,
+              "car_fused_tail out size");
+  check(k8sllm_car_fused_tail((void*)(intptr_t)state, slabs.data_ptr<float>(), (int)ns, (long)M * d,
+                              residual.data_ptr(), w.data_ptr(), out.data_ptr(), d, M, d, (float)eps, packed ? 1 : 0,
+                              (long)spin_limit, cur()),
+        "car_fused_tail");
 }
 
 void car_all_gather(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit) {
@@ -778,7 +798,9 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("add_norm_partial", &add_norm_partial);
   m.def("car_create", &car_create);
   m.def("car_open", &car_open);
-  m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_all_reduce", &car_all_reduce, py::arg("state"), py::arg("in"), py::arg("out"), py::arg("spin_limit"),
+        py::arg("algo") = -1);
+  m.def("car_fused_tail", &car_fused_tail);
   m.def("car_error", &car_error);
   m.def("car_all_gather", &car_all_gather);
   m.def("car_error_async", &car_error_async);

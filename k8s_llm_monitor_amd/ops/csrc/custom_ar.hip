@@ -1,31 +1,40 @@
-// One-shot all-reduce over IPC-mapped peer buffers for latency-bound tensor-parallel decode
+// IPC all-reduce / all-gather over mapped peer buffers for latency-bound tensor-parallel decode
 // messages ("a custom one-shot all-reduce: IPC-mapped peer buffers via
 // hipIpcGetMemHandle, then each GPU reads all 7 peers over the 7 links simultaneously and reduces
 // locally; hipGraph-capturable, with RCCL as fallback").
 //
 // An 8-GPU MI355X node is a full xGMI mesh (7 links per GPU).  A ring all-reduce of a decode-sized
 // message (64 rows x 8192 x bf16 = 1 MiB for Llama-3-70B at TP=8) pays 2(W-1) latency-bound hops
-// on ONE link per direction; one-shot pays one hop and pulls from all 7 peers at once.
+// on ONE link per direction; one-shot pays one hop and pulls from all 7 peers at once.  Above
+// ~0.5 MiB the one-shot form pulls (W-1) x n bytes per rank; the TWO-SHOT form (reduce-scatter,
+// then all-gather, inside one launch) pulls 2 (W-1) / W x n - 1.75 n at W = 8 instead of 7 n -
+// for one more flag round.
 //
 // Per call (epoch e = 1 + the number of calls this rank has completed; ONE counter per rank in the
 // signal block, advanced on the device by the call's last workgroup, so hipGraph replays advance it
 // and every workgroup of a call uses the same buffer half whatever the call's size):
-//   1. workgroup b copies its slice of the input into this rank's registered staging buffer
-//      (half e & 1 of a double buffer);
+//   1. workgroup b writes its slice of the message into this rank's registered staging buffer
+//      (half e & 1 of a double buffer) - a copy of the input, or (fused tail) the projection's
+//      split-K partial sum computed straight into it, so that path has no staging copy at all;
 //   2. lane 0: system-scope release (writes the XCD L2 back) -> flag[rank][b] = e in EVERY rank's
 //      signal block (remote stores over xGMI);
 //   3. lanes r < W poll flag[r][b] >= e in this rank's signal block (bounded spin: a peer that never
 //      arrives sets `err` and the kernel still exits - it can never hang the GPU);
 //   4. system-scope acquire, then the result from the peers' staged slices (plain 16-byte loads):
 //      ALL-REDUCE: out[slice] = sum over ranks in RANK ORDER (bit-identical on every rank, as the
-//      replicated TP forward requires); ALL-GATHER: out[r * n + slice] = rank r's slice.
+//      replicated TP forward requires); ALL-GATHER: out[r * n + slice] = rank r's slice;
+//      TWO-SHOT: rank r reduces part r of the slice IN PLACE in its own staging buffer, flags a
+//      second round (flag2), and every rank then copies part r from rank r;
+//      FUSED TAIL (one workgroup per row): residual += the reduced row, RMSNorm, and the next
+//      projection's input written in its final layout - the row-parallel o / down tail of a TP
+//      decode layer in ONE launch instead of reduce_slabs + all-reduce + add-norm + pack.
 //   5. the last workgroup to finish (done counter) publishes epoch = e.
 // Buffer-reuse safety: a rank writes half e & 1 only after completing call e - 1, which required a
 // flag of call e - 1 from every peer, i.e. every peer had started call e - 1 and therefore finished
-// reading half e & 1 in call e - 2.  With a per-call epoch this holds for any sequence of message
-// sizes (per-slot epochs, the previous design, broke it when consecutive calls differed in size).
+// reading half e & 1 in call e - 2 (both rounds of a two-shot call e - 2 included).  With a per-call
+// epoch this holds for any sequence of message sizes and call kinds.
 // Signal blocks live in uncached device memory (hipDeviceMallocUncached); data buffers are plain
-// hipMalloc memory ordered by the release/acquire pair.
+// hipMalloc memory ordered by the release/acquire pairs.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -34,13 +43,14 @@
 namespace k8sllm {
 
 constexpr int CAR_MAX_RANKS = 8;
-constexpr int CAR_MAX_WG = 64;
+constexpr int CAR_MAX_WG = 256;
 
 struct CarSignal {
-  uint32_t flag[CAR_MAX_RANKS][CAR_MAX_WG];  // flag[src][b]: epoch of src's latest staged slice b
-  uint32_t epoch;                            // calls completed by this rank
-  uint32_t done;                             // workgroups of the current call that have finished
-  uint32_t err;                              // set when a peer did not arrive within the spin bound
+  uint32_t flag[CAR_MAX_RANKS][CAR_MAX_WG];   // flag[src][b]: epoch of src's latest staged slice b
+  uint32_t flag2[CAR_MAX_RANKS][CAR_MAX_WG];  // two-shot: epoch of src's reduced part of slice b
+  uint32_t epoch;                             // calls completed by this rank
+  uint32_t done;                              // workgroups of the current call that have finished
+  uint32_t err;                               // set when a peer did not arrive within the spin bound
 };
 
 struct CarPeers {
@@ -48,36 +58,34 @@ struct CarPeers {
   CarSignal* sig[CAR_MAX_RANKS];   // every rank's signal block, mapped here
 };
 
-// n: elements of THIS rank's input (the all-gather output holds world * n).
-template <bool GATHER>
-__global__ __launch_bounds__(256) void car_oneshot_kernel(const bf16_t* in, bf16_t* out,  // may alias (reduce)
-                                                          long n, long max_elems, int rank, int world, CarPeers p,
-                                                          long spin_limit) {
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
-  CarSignal* my = p.sig[rank];
+// this call's epoch (1 + calls completed), read once per workgroup
+__device__ __forceinline__ uint32_t car_epoch(CarSignal* my) {
   __shared__ uint32_t s_e;
-  if (tid == 0) s_e = __hip_atomic_load(&my->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (threadIdx.x == 0) s_e = __hip_atomic_load(&my->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
-  const uint32_t e = s_e;
-  const long half = (long)(e & 1) * max_elems;
-  const long nv = n >> 3;  // 16-byte vectors
-  const long per = (nv + nb - 1) / nb;
-  const long v0 = (long)b * per, v1 = min(nv, v0 + per);
+  return s_e;
+}
 
-  uint4* mine = reinterpret_cast<uint4*>(p.buf[rank] + half);
-  const uint4* src = reinterpret_cast<const uint4*>(in);
-  for (long v = v0 + tid; v < v1; v += 256) mine[v] = src[v];
+// Publish this workgroup's slice b (every thread's stores issued) and wait for every peer's slice
+// b of this call: flags[src][b] in the signal blocks (flag or flag2 round).
+template <bool ROUND2>
+__device__ __forceinline__ void car_exchange(const CarPeers& p, int rank, int world, int b, uint32_t e,
+                                             long spin_limit) {
+  CarSignal* my = p.sig[rank];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the staged slice reaches memory
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int r = 0; r < world; ++r)
-      __hip_atomic_store(&p.sig[r]->flag[rank][b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int r = 0; r < world; ++r) {
+      uint32_t* f = ROUND2 ? &p.sig[r]->flag2[rank][b] : &p.sig[r]->flag[rank][b];
+      __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
-  if (tid < world) {
+  if ((int)threadIdx.x < world) {
+    uint32_t* f = ROUND2 ? &my->flag2[threadIdx.x][b] : &my->flag[threadIdx.x][b];
     long it = 0;
-    while ((int)(__hip_atomic_load(&my->flag[tid][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (++it > spin_limit) {
         __hip_atomic_store(&my->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -86,37 +94,151 @@ __global__ __launch_bounds__(256) void car_oneshot_kernel(const bf16_t* in, bf16
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' slices are visible to this CU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  uint4* dst = reinterpret_cast<uint4*>(out);
-  if constexpr (GATHER) {
-    for (int r = 0; r < world; ++r) {
-      const uint4* peer = reinterpret_cast<const uint4*>(p.buf[r] + half);
-      for (long v = v0 + tid; v < v1; v += 256) dst[(long)r * nv + v] = peer[v];
-    }
-  } else {
-    for (long v = v0 + tid; v < v1; v += 256) {
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int r = 0; r < world; ++r) {  // fixed rank order: identical sums on every rank
-        float f[8];
-        unpack8(reinterpret_cast<const uint4*>(p.buf[r] + half)[v], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += f[j];
-      }
-      dst[v] = pack8(acc);
-    }
-  }
+}
+
+// the call's last workgroup to finish publishes the epoch for the next call on this stream
+__device__ __forceinline__ void car_finish(CarSignal* my, uint32_t e) {
   __syncthreads();
-  if (tid == 0) {  // the call's last workgroup publishes the epoch for the next call on this stream
+  if (threadIdx.x == 0) {
     const uint32_t d = __hip_atomic_fetch_add(&my->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d + 1 == (uint32_t)nb) {
+    if (d + 1 == gridDim.x) {
       __hip_atomic_store(&my->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&my->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+__device__ __forceinline__ void sum_ranks8(const CarPeers& p, int world, long half, long v, float* acc) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int r = 0; r < world; ++r) {  // fixed rank order: identical sums on every rank
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(p.buf[r] + half)[v], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+}
+
+// MODE 0: one-shot all-reduce, 1: one-shot all-gather, 2: two-shot all-reduce.
+// n: elements of THIS rank's input (the all-gather output holds world * n).
+template <int MODE>
+__global__ __launch_bounds__(256) void car_kernel(const bf16_t* in, bf16_t* out,  // may alias (reduce)
+                                                  long n, long max_elems, int rank, int world, CarPeers p,
+                                                  long spin_limit) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  CarSignal* my = p.sig[rank];
+  const uint32_t e = car_epoch(my);
+  const long half = (long)(e & 1) * max_elems;
+  const long nv = n >> 3;  // 16-byte vectors
+  const long per = (nv + nb - 1) / nb;
+  const long v0 = (long)b * per, v1 = min(nv, v0 + per);
+
+  uint4* mine = reinterpret_cast<uint4*>(p.buf[rank] + half);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  for (long v = v0 + tid; v < v1; v += 256) mine[v] = src[v];
+  car_exchange<false>(p, rank, world, b, e, spin_limit);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  if constexpr (MODE == 1) {
+    for (int r = 0; r < world; ++r) {
+      const uint4* peer = reinterpret_cast<const uint4*>(p.buf[r] + half);
+      for (long v = v0 + tid; v < v1; v += 256) dst[(long)r * nv + v] = peer[v];
+    }
+  } else if constexpr (MODE == 0) {
+    for (long v = v0 + tid; v < v1; v += 256) {
+      float acc[8];
+      sum_ranks8(p, world, half, v, acc);
+      dst[v] = pack8(acc);
+    }
+  } else {
+    // part r of slice b = vectors [v0 + r * pp, v0 + (r + 1) * pp): reduced by rank r in place
+    const long pp = (v1 - v0 + world - 1) / world;
+    const long a0 = v0 + rank * pp, a1 = min(v1, a0 + pp);
+    for (long v = a0 + tid; v < a1; v += 256) {
+      float acc[8];
+      sum_ranks8(p, world, half, v, acc);
+      mine[v] = pack8(acc);
+    }
+    car_exchange<true>(p, rank, world, b, e, spin_limit);
+    for (int r = 0; r < world; ++r) {
+      const uint4* peer = reinterpret_cast<const uint4*>(p.buf[r] + half);
+      const long r0 = v0 + r * pp, r1 = min(v1, r0 + pp);
+      for (long v = r0 + tid; v < r1; v += 256) dst[v] = peer[v];
+    }
+  }
+  car_finish(my, e);
+}
+
+// Fused row-parallel tail of a TP decode layer, one workgroup per row m of an [M, d] message:
+//   partial = bf16(sum over the ns fp32 split-K slabs of THIS rank's projection)  -> staging
+//   y = bf16(sum over ranks, rank order); residual = bf16(residual + y) (written back)
+//   out = bf16(residual * rsqrt(mean(residual^2) + eps) * w), row-major (ldo) or, when PACKED,
+//         in the fragment-packed A layout of the next skinny GEMM (act_index)
+// - exactly the arithmetic of reduce_slabs -> all-reduce -> fused_add_rms_norm -> pack_activation.
+template <int NC, bool PACKED>
+__global__ __launch_bounds__(256) void car_fused_tail_kernel(const float* __restrict__ slabs, int ns, long slab_stride,
+                                                             bf16_t* __restrict__ residual,
+                                                             const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+                                                             long ldo, int d, float eps, long max_elems, int rank,
+                                                             int world, CarPeers p, long spin_limit) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  CarSignal* my = p.sig[rank];
+  const uint32_t e = car_epoch(my);
+  const long half = (long)(e & 1) * max_elems;
+  const long row = (long)m * d;
+  bf16_t* mine = p.buf[rank] + half + row;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < d) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < ns; ++sl) {
+        const float4* q = reinterpret_cast<const float4*>(slabs + sl * slab_stride + row + idx);
+        const float4 a = q[0], b2 = q[1];
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b2.x; acc[5] += b2.y; acc[6] += b2.z; acc[7] += b2.w;
+      }
+      *reinterpret_cast<uint4*>(mine + idx) = pack8(acc);
+    }
+  }
+  car_exchange<false>(p, rank, world, m, e, spin_limit);
+  float v[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < d) {
+      float acc[8], r[8];
+      sum_ranks8(p, world, half, (row + idx) >> 3, acc);
+      unpack8(*reinterpret_cast<const uint4*>(residual + row + idx), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[c][j] = bf2f(f2bf(bf2f(f2bf(acc[j])) + r[j]));
+        ss += v[c][j] * v[c][j];
+      }
+      *reinterpret_cast<uint4*>(residual + row + idx) = pack8(v[c]);
+    }
+  }
+  ss = block_sum<256>(ss, red);
+  const float inv = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < d) {
+      float wf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
+      const long oi = PACKED ? act_index(m, idx, -(long)(d >> 5)) : (long)m * ldo + idx;
+      *reinterpret_cast<uint4*>(out + oi) = pack8(o);
+    }
+  }
+  car_finish(my, e);
 }
 
 struct CarState {
@@ -192,19 +314,35 @@ extern "C" int k8sllm_car_open(void* state, const void* all_handles) {
   return 0;
 }
 
-// out = sum over ranks of in (n bf16, n % 8 == 0, n <= max_elems); in may alias out.
-extern "C" int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit,
-                                     hipStream_t s) {
-  auto* st = (CarState*)state;
-  if (n <= 0) return 0;
+static int car_check(CarState* st, long n) {
   if (n % 8 || n > st->max_elems) return -1;
   for (int r = 0; r < st->world; ++r)
     if (st->peers.buf[r] == nullptr) return -2;  // not opened
-  const long nv = n / 8;
-  int nb = (int)((nv + 255) / 256);
-  nb = nb < 1 ? 1 : (nb > CAR_MAX_WG ? CAR_MAX_WG : nb);
-  hipLaunchKernelGGL(car_oneshot_kernel<false>, dim3(nb), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n,
-                     st->max_elems, st->rank, st->world, st->peers, spin_limit);
+  return 0;
+}
+
+// workgroups for an n-element message: one per 2048 elements (8 per thread), at most CAR_MAX_WG -
+// the copy / reduce loops are bandwidth-bound, so a 16 MiB message uses every one of 256 CUs
+static int car_grid(long n) {
+  const long nb = (n / 8 + 255) / 256;
+  return (int)(nb < 1 ? 1 : (nb > CAR_MAX_WG ? CAR_MAX_WG : nb));
+}
+
+// out = sum over ranks of in (n bf16, n % 8 == 0, n <= max_elems); in may alias out.
+// algo: 0 one-shot, 1 two-shot, -1 auto (two-shot from 512 KiB at W > 2)
+extern "C" int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, int algo,
+                                     hipStream_t s) {
+  auto* st = (CarState*)state;
+  if (n <= 0) return 0;
+  if (int rc = car_check(st, n)) return rc;
+  if (algo < 0) algo = (st->world > 2 && n * 2 >= (512L << 10)) ? 1 : 0;
+  const int nb = car_grid(n);
+  if (algo == 1)
+    hipLaunchKernelGGL(car_kernel<2>, dim3(nb), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n, st->max_elems,
+                       st->rank, st->world, st->peers, spin_limit);
+  else
+    hipLaunchKernelGGL(car_kernel<0>, dim3(nb), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n, st->max_elems,
+                       st->rank, st->world, st->peers, spin_limit);
   return (int)hipGetLastError();
 }
 
@@ -214,14 +352,33 @@ extern "C" int k8sllm_car_all_gather(void* state, const void* in, void* out, lon
                                      hipStream_t s) {
   auto* st = (CarState*)state;
   if (n <= 0) return 0;
-  if (n % 8 || n > st->max_elems) return -1;
-  for (int r = 0; r < st->world; ++r)
-    if (st->peers.buf[r] == nullptr) return -2;
-  const long nv = n / 8;
-  int nb = (int)((nv + 255) / 256);
-  nb = nb < 1 ? 1 : (nb > CAR_MAX_WG ? CAR_MAX_WG : nb);
-  hipLaunchKernelGGL(car_oneshot_kernel<true>, dim3(nb), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n,
+  if (int rc = car_check(st, n)) return rc;
+  hipLaunchKernelGGL(car_kernel<1>, dim3(car_grid(n)), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n,
                      st->max_elems, st->rank, st->world, st->peers, spin_limit);
+  return (int)hipGetLastError();
+}
+
+// Fused TP row-parallel tail (see car_fused_tail_kernel): slabs [ns][M][d] fp32 (slab_stride
+// elements apart), residual [M][d] bf16 updated in place, w [d], out [M][ldo] row-major or
+// fragment-packed (packed != 0; ldo ignored).  M <= CAR_MAX_WG, d % 8 == 0, d <= 8192.
+extern "C" int k8sllm_car_fused_tail(void* state, const float* slabs, int ns, long slab_stride, void* residual,
+                                     const void* w, void* out, long ldo, int M, int d, float eps, int packed,
+                                     long spin_limit, hipStream_t s) {
+  auto* st = (CarState*)state;
+  if (M <= 0) return 0;
+  if (M > CAR_MAX_WG || d % 8 || d > 8192 || ns < 1 || (packed && d % 32)) return -1;
+  if (int rc = car_check(st, (long)M * d)) return rc;
+  const int nc = (d + 2047) / 2048;
+#define K8_TAIL(NC_, PK_)                                                                                          \
+  hipLaunchKernelGGL((car_fused_tail_kernel<NC_, PK_>), dim3(M), dim3(256), 0, s, slabs, ns, slab_stride,        \
+                     (bf16_t*)residual, (const bf16_t*)w, (bf16_t*)out, ldo, d, eps, st->max_elems, st->rank,    \
+                     st->world, st->peers, spin_limit)
+  if (packed) {
+    if (nc <= 2) K8_TAIL(2, true); else K8_TAIL(4, true);
+  } else {
+    if (nc <= 2) K8_TAIL(2, false); else K8_TAIL(4, false);
+  }
+#undef K8_TAIL
   return (int)hipGetLastError();
 }
 

@@ -300,32 +300,38 @@ __global__ __launch_bounds__(512, 1) void gemm_tile256_kernel(const bf16_t* __re
 
 // ------------------------------------------------------------------------------------------------
 // 4-wave variant: the same 256 x 256 output tile, but each wave owns a 128 x 128 quarter (64
-// accumulators of v_mfma_f32_16x16x32_bf16 = 256 f32 per lane, one wave per SIMD).  Per 32-deep k
-// step a wave reads 16 ds_read_b128 for 64 MFMAs (0.25 per MFMA, the 8-wave kernel above needs
-// 0.375) - the LDS-read pressure the round-2 ablation named as its limiter.
+// accumulators of v_mfma_f32_16x16x32_bf16 = 256 f32 per lane in AGPRs, one wave per SIMD).  Per
+// 32-deep k sub-step a wave reads 16 ds_read_b128 for 64 MFMAs (0.25 per MFMA; the 8-wave kernel
+// above needs 0.375).
 //
-//  * K in 32-deep tiles; a tile = A 256 rows x 64 B + B 256 rows x 64 B = 32 KiB; a 4-slot LDS ring
-//    (128 KiB, one __shared__ array).  Tile t+4 is DMA'd into tile t's slot while tile t is
-//    computed from registers, so every fill has ~3 tiles (~3k cycles) to land.
-//  * fragments of tile t+1 are read (16 ds_read_b128) in between tile t's MFMAs into the second
-//    register set; one raw s_barrier per tile, preceded by lgkmcnt(0) and a counted vmcnt that
-//    leaves the two youngest tiles' DMAs in flight (never vmcnt(0) in the main loop).
-//  * 64-B LDS rows: logical 16-B chunk c of row r sits at physical chunk c ^ ((4 - ((r >> 2) & 3)) & 3)
-//    (applied to the DMA source address; the LDS side is lane-linear), which puts every
-//    16-lane group of a fragment ds_read_b128 on 16 distinct bank quads (rows 0-15, chunk l >> 4).
-__device__ __forceinline__ int swz64(int q) { return (4 - q) & 3; }
-
+//  * K in 64-deep tiles with 128-B LDS rows, so every DMA row segment is one whole 128-B line
+//    (a 32-deep / 64-B-row build of this kernel issued twice the L2 requests, and its TA spent a
+//    third of the kernel stalled on the cache: profiles/r03/gemm_pmc_qkv.jsonl).
+//  * LDS = a ring of five 32 KiB half-slots (160 KiB, one __shared__ array); half-tile h (A_t = 2t,
+//    B_t = 2t + 1) lives in slot h % 5.  A_{t+2} is DMA'd during sub-step (t, 0) and B_{t+2} during
+//    (t, 1), each into the slot its predecessor h - 5 left once its last fragments were read, so A
+//    has 3 and B 2 sub-steps (~2-3k cycles) to land.
+//  * fragments of the next sub-step are read (16 ds_read_b128) in between the current one's MFMAs
+//    into the second register set: (t, 1) during (t, 0), (t + 1, 0) during (t, 1).  ONE raw
+//    s_barrier per tile, before (t, 1): lgkmcnt(0) and vmcnt(8) (tile t + 1 has landed, A_{t+2}
+//    stays in flight) - never vmcnt(0) in the loop.
+//  * 128-B LDS rows: logical 16-B chunk c of row r sits at physical chunk c ^ ((r >> 1) & 7)
+//    (applied to the DMA source address; the LDS side is lane-linear), so each 16-lane group of a
+//    fragment ds_read_b128 (rows 0-15 of a block) hits 16 distinct bank quads.
+//  * the DMA is buffer_load_dwordx4 ... lds against SGPR buffer descriptors of this tile's rows:
+//    lane offsets are per-lane constants, the k offset goes in soffset (no 64-bit address math).
 template <int N>
 __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, bool GROUPED, int ABL = 0>  // ABL (diagnosis builds): 1 no MFMA, 2 no in-loop DMA
+// CPX / CPW: cache-policy bits of the X / W DMA loads (17 = sc0 sc1: bypass the CU's L1)
+template <int EPI, bool GROUPED, int ABL = 0, int CPX = 0, int CPW = 0>  // ABL (diagnosis): 1 no MFMA, 2 no in-loop DMA
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
-  constexpr int SLOT = 32768, BOFF = 16384;
-  __shared__ __attribute__((aligned(16))) char smem[4 * SLOT];
+  constexpr int HS = 32768;  // one half-slot: 256 rows x 128 B
+  __shared__ __attribute__((aligned(16))) char smem[5 * HS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -365,21 +371,18 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   const int n0 = nt * 256;
   const int nrows = min(256, N - n0);
 
-  // ---- DMA: operand o (0 X, 1 W), piece p (0..3) covers 16-row group p * 4 + wave; lane ->
-  // row (lane >> 2) of the group, physical chunk lane & 3 ----
-  uint32_t soff[2][4];
-  {
-    const int cl = (lane & 3) ^ swz64((lane >> 4) & 3);
+  // ---- DMA of one half-tile (256 rows x 128 B = 32 pieces of 1 KiB): piece p (0..7) of this
+  // wave covers rows (p * 4 + wave) * 8 .. + 7; lane -> row + (lane >> 3), physical chunk lane & 7 ----
+  uint32_t soff[2][8];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int rl = (p * 4 + wave) * 16 + (lane >> 2);
-      soff[0][p] = (uint32_t)(((long)min(rl, mrows - 1) * K + cl * 8) * 2);  // rows past the end: clamped, never stored
-      soff[1][p] = (uint32_t)(((long)min(rl, nrows - 1) * K + cl * 8) * 2);
-    }
+  for (int p = 0; p < 8; ++p) {
+    const int rl = (p * 4 + wave) * 8 + (lane >> 3);
+    const int cl = (lane & 7) ^ ((rl >> 1) & 7);
+    soff[0][p] = (uint32_t)(((long)min(rl, mrows - 1) * K + cl * 8) * 2);  // rows past the end: clamped, never stored
+    soff[1][p] = (uint32_t)(((long)min(rl, nrows - 1) * K + cl * 8) * 2);
   }
-  // buffer descriptors over this tile's X rows / W rows (built from wave-uniform values only, so
-  // hipcc keeps them in SGPRs: no waterfall loops, cdna_hip_programming.md T20); the DMA is
-  // buffer_load_dwordx4 ... lds with the lane's constant voffset and the k offset in soffset
+  // buffer descriptors over this tile's X rows / W rows, built from wave-uniform values only so
+  // hipcc keeps them in SGPRs (no waterfall loops, cdna_hip_programming.md T20)
   auto rsrc = [](const void* base, long bytes) {
     const uint64_t a = reinterpret_cast<uint64_t>(base);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
@@ -388,23 +391,29 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   };
   const __amdgpu_buffer_rsrc_t xr = rsrc(reinterpret_cast<const char*>(X) + (long)row0 * K * 2, (long)mrows * K * 2);
   const __amdgpu_buffer_rsrc_t wr = rsrc(reinterpret_cast<const char*>(Wt) + (long)n0 * K * 2, (long)nrows * K * 2);
-  const int nk = K >> 5;
+  const int nk = K >> 6;
 
-  // piece g (= o * 4 + p) of k-tile kt into ring slot `slot` & 3
-  auto piece = [&](int g, int kt, int slot) {
-    const int o = g >> 2, p = g & 3;
-    char* dst = smem + (slot & 3) * SLOT + o * BOFF + (p * 4 + wave) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], kt * 64, 0, 0);
+  // piece p of half-tile (operand o, k-tile kt) into half-slot `slot`; k-tiles past the end re-read
+  // the last one (identical bytes into a slot no live fragment read uses), so every sub-step
+  // issues the same count and the vmcnt arithmetic never changes
+  auto piece = [&](int o, int p, int kt, int slot) {
+    char* dst = smem + slot * HS + (p * 4 + wave) * 1024;
+    if (o)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)dst, 16, soff[1][p], min(kt, nk - 1) * 128, 0, CPW);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)dst, 16, soff[0][p], min(kt, nk - 1) * 128, 0, CPX);
   };
-  auto issue_tile = [&](int kt, int slot) {
+  auto issue_half = [&](int o, int kt) {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) piece(g, kt, slot);
+    for (int p = 0; p < 8; ++p) piece(o, p, kt, (2 * kt + o) % 5);
   };
 
-  // fragment read: lane row lane & 15 of a 16-row block, logical chunk lane >> 4
-  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz64((lane >> 2) & 3)) << 4);
-  auto frag = [&](int kt, int o, int blk) -> bf16x8 {
-    const char* b = smem + (kt & 3) * SLOT + o * BOFF + ((o ? wn : wm) * 8 + blk) * 1024 + rd;
+  // fragment read: lane row lane & 15 of a 16-row block, 16-B chunk 4 ks + (lane >> 4)
+  int rd[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) rd[ks] = (lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+  auto frag = [&](int slot, int ks, int o, int blk) -> bf16x8 {
+    const char* b = smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + rd[ks];
     return *reinterpret_cast<const bf16x8*>(b);
   };
 
@@ -416,65 +425,82 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
-  // one k-tile: 64 MFMAs from (ca, cb); between them the fragments of tile t+1 into (na, nb) and
-  // the DMA of tile t+4 into tile t's slot; then lgkmcnt(0), vmcnt(16) (tiles t+3, t+4 stay in
-  // flight: tile t+2 has landed), one barrier.  Past the last tile the reads and DMAs are clamped
-  // to tile nk-1 (re-writing identical bytes into a slot nobody reads any more), so every step
-  // has the same body and the same counts.
-  auto step = [&](int t, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
-    const int tr = min(t + 1, nk - 1), tl = min(t + 4, nk - 1);
+  // one 32-deep sub-step: 64 MFMAs from (ca, cb); between the row blocks' MFMA groups the 16
+  // fragment reads of the next sub-step (k-half nks, slots sa / sb) - the W fragments first (the
+  // next sub-step's FIRST row block needs all eight of them), then the X fragments, all issued in
+  // the first six groups so no read is still in flight when the next sub-step (or the barrier's
+  // lgkmcnt(0)) needs it - and one DMA piece of half-tile (o, kt) into slot `ds` per group
+  // Issue order (sched_group_barrier): one DMA piece after each of the first 8 MFMAs (the global
+  // loads have the farthest to go), then one fragment read after each of the next 16 - every
+  // non-MFMA instruction sits in an MFMA's shadow instead of in a cluster that leaves the matrix
+  // pipe idle (nodma builds: 1.71 / 1.81 PF/s on qkv / down with it, from 1.51 / 1.69).
+  auto sub = [&](bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], int sa, int sb, int nks,
+                 int o, int kt, int ds) {
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        const int n = g * 8 + j;  // MFMA number in the sub-step; what rides in its shadow:
         if constexpr (ABL == 1) {
           asm volatile("" ::"v"(cb[j]), "v"(ca[g]));  // keep the fragment reads alive
         } else {
           acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
         }
+        if (n < 8) {  // the 8 DMA pieces first (the global loads have the farthest to go)
+          if constexpr (ABL != 2) piece(o, n, kt, ds);
+        } else if (n < 16) {  // then W fragments 0-7 (the next sub-step's first row block needs all)
+          nb[n - 8] = frag(sb, nks, 1, n - 8);
+        } else if (n < 24) {  // then X fragments 0-7
+          na[n - 16] = frag(sa, nks, 0, n - 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      na[g] = frag(tr, 0, g);
-      nb[g] = frag(tr, 1, g);
-      if constexpr (ABL != 2) piece(g, tl, t);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    lgkm_wait0();
-    vm_wait_n<16>();
-    __builtin_amdgcn_s_barrier();
   };
 
-  // prologue: tiles 0..3 in flight (clamped); tile 0 read synchronously; tile 1 landed before the loop
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) issue_tile(min(kt, nk - 1), kt);
-  vm_wait_n<24>();
+  // prologue: A_0 B_0 A_1 B_1 in flight; tile 0 landed -> read its first k-half
+  issue_half(0, 0);
+  issue_half(1, 0);
+  issue_half(0, 1);
+  issue_half(1, 1);
+  vm_wait_n<16>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    fa0[g] = frag(0, 0, g);
-    fb0[g] = frag(0, 1, g);
+    fa0[g] = frag(0, 0, 0, g);
+    fb0[g] = frag(1, 0, 1, g);
   }
-  lgkm_wait0();
-  vm_wait_n<16>();
-  __builtin_amdgcn_s_barrier();
 
-  for (int t = 0; t < nk; t += 2) {  // nk even (K % 64 == 0)
-    step(t, fa0, fb0, fa1, fb1);
-    step(t + 1, fa1, fb1, fa0, fb0);
+  for (int t = 0; t < nk; ++t) {
+    const int sa = (2 * t) % 5, sb = (2 * t + 1) % 5;            // tile t's half-slots
+    const int sa1 = (2 * t + 2) % 5, sb1 = (2 * t + 3) % 5;      // tile t+1's
+    // (t, 0): MFMAs on k-half 0; read k-half 1 of tile t; DMA A_{t+2}
+    sub(fa0, fb0, fa1, fb1, sa, sb, 1, 0, t + 2, (2 * t + 4) % 5);
+    lgkm_wait0();
+    vm_wait_n<8>();  // B_{t+1} landed (only A_{t+2} younger)
+    __builtin_amdgcn_s_barrier();
+    // (t, 1): MFMAs on k-half 1; read k-half 0 of tile t+1 (garbage past the end, never used); DMA B_{t+2}
+    sub(fa1, fb1, fa0, fb0, sa1, sb1, 0, 1, t + 2, (2 * t + 5) % 5);
   }
   vm_wait_n<0>();
 
   // ---- epilogue: acc[i][j][r] = Y[m][n], m = wm*128 + i*16 + (lane & 15),
-  // n = wn*128 + j*16 + 4 (lane >> 4) + r ----
+  // n = wn*128 + j*16 + 4 (lane >> 4) + r.  Staged through LDS (the ring is idle now): each wave
+  // writes its quarter as bf16 rows (8-B ds_write per 4 columns), then reads back whole rows and
+  // stores 16 B per lane, 256 contiguous bytes per row - half the store instructions of writing
+  // the accumulator layout directly, which is what bounds a store tail (T21). ----
+  lgkm_wait0();
+  __builtin_amdgcn_s_barrier();  // every wave is done with the ring (its last DMAs retired above)
+  constexpr int OUTW = EPI == TILE_EPI_SWIGLU ? 64 : 128;  // output columns of this wave's quarter
+  constexpr int RS = OUTW * 2 + 16;                        // LDS row stride (16-B pad: 2-way writes)
+  char* stage = smem + wave * (128 * RS);
   const int ml = lane & 15, nq = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     __builtin_amdgcn_sched_barrier(0);  // one row block's accumulators at a time (no hoisted AGPR reads)
-    const int m = wm * 128 + i * 16 + ml;
-    if (m >= mrows) continue;
+    char* srow = stage + (i * 16 + ml) * RS + nq * 2;
     if constexpr (EPI == TILE_EPI_SWIGLU) {
-      bf16_t* yrow = Y + (long)(row0 + m) * (N >> 1) + ((n0 + wn * 128) >> 1) + nq;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float o[4];
@@ -483,18 +509,242 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
           const float gt = bf2f(f2bf(acc[i][j][r])), up = bf2f(f2bf(acc[i][j + 4][r]));
           o[r] = gt * up / (1.f + __expf(-gt));
         }
-        *reinterpret_cast<uint2*>(yrow + j * 16) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+        *reinterpret_cast<uint2*>(srow + j * 32) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
       }
     } else {
-      bf16_t* yrow = Y + (long)(row0 + m) * N + n0 + wn * 128 + nq;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (wn * 128 + j * 16 >= nrows) break;
         const f32x4 v = acc[i][j];
-        *reinterpret_cast<uint2*>(yrow + j * 16) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        *reinterpret_cast<uint2*>(srow + j * 32) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
       }
     }
   }
+  lgkm_wait0();
+  constexpr int CPR = OUTW / 8;  // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per wave instruction
+  const int ldy = EPI == TILE_EPI_SWIGLU ? (N >> 1) : N;
+  const int col0 = EPI == TILE_EPI_SWIGLU ? ((n0 + wn * 128) >> 1) : n0 + wn * 128;
+  const int ncols = EPI == TILE_EPI_SWIGLU ? (nrows >> 1) - wn * 64 : nrows - wn * 128;
+  const int rr = lane / CPR, cc = lane % CPR;
+  // branch-free masked stores: a buffer descriptor over this m-tile's rows drops every store past
+  // row mrows (out of range), and a lane whose columns are past N gets an out-of-range offset
+  const __amdgpu_buffer_rsrc_t yr = rsrc(Y + (long)row0 * ldy, (long)mrows * ldy * 2);
+  const uint32_t yo = cc * 8 < ncols ? (uint32_t)(((wm * 128 + rr) * ldy + col0 + cc * 8) * 2) : 0x80000000u;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int b = 0; b < 128 / RPI; b += 8) {  // 8 row groups per batch: reads issued back to back
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const u32x4*>(stage + ((b + u) * RPI + rr) * RS + cc * 16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(v[u], yr, yo + (uint32_t)((b + u) * RPI * ldy * 2), 0, 0);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent form of the 4-wave kernel (the prefill default): one workgroup per CU loops over its
+// XCD's tiles, and the LDS-DMA ring runs on ACROSS tiles - the first two k-tiles of the next tile
+// are fetched during the last two k-tiles of the current one, exactly like any other k-tile - so
+// a tile starts with its data already in LDS.  In the one-launch-per-tile form every CU issued
+// its 128 KiB prologue and its 128 KiB of output in the same instant (all tiles of a round start
+// and end together): ~14 us of fixed cost per tile round, 15 % of a 4096-deep projection
+// (profiles/r03, fixed cost vs k-tiles fit).  Rows past M and k beyond the operand rows read as
+// zeros through the buffer descriptors' range checks (no clamping, so the lane's DMA offset is
+// one constant), and the epilogue stores straight from the accumulators through a descriptor
+// over the tile's rows (rows past M are dropped by the range check).
+template <int EPI, bool GROUPED>
+__global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
+                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
+  constexpr int HS = 32768;
+  __shared__ __attribute__((aligned(16))) char smem[5 * HS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = K >> 6;
+
+  // ---- this workgroup's tiles: XCD x owns a contiguous chunk of the logical tile order (split
+  // bijectively over the 8 XCDs); its `per` workgroups take every per-th tile of the chunk ----
+  const int nwg = n_mt * n_nt;
+  const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, sl = blockIdx.x >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int cnt = q8 + (xcd < r8 ? 1 : 0);
+
+  auto rsrc = [](const void* base, long bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo_ = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo_), 0, nb, 0x00020000);
+  };
+  struct Tile {
+    int idx, row0, mrows, n0, nrows;
+    __amdgpu_buffer_rsrc_t xr, wr;
+  };
+  constexpr int GM = 8;
+  // the first valid tile at chunk index >= idx (idx >= cnt: none)
+  auto find = [&](int idx) -> Tile {
+    Tile tl;
+    for (; idx < cnt; idx += per) {
+      const int lid = lo + idx;
+      const int grp = lid / (GM * n_nt), first_m = grp * GM;
+      const int gsz = min(n_mt - first_m, GM);
+      const int in_g = lid - grp * GM * n_nt;
+      const int mt = first_m + in_g % gsz, nt = in_g / gsz;
+      int row0 = mt * 256, mrows = M - row0;
+      const bf16_t* Wt = W;
+      if constexpr (GROUPED) {
+        int e = -1, acc_t = 0;
+        for (int x = 0; x < E; ++x) {
+          const int o0 = offsets[x], o1 = offsets[x + 1];
+          const int tiles = (o1 - o0 + 255) >> 8;
+          if (e < 0 && mt < acc_t + tiles) {
+            e = x;
+            row0 = o0 + (mt - acc_t) * 256;
+            mrows = o1 - row0;
+          }
+          acc_t += tiles;
+        }
+        if (e < 0) continue;  // past the last expert's tiles
+        Wt = W + (long)e * w_es;
+      }
+      tl.idx = idx;
+      tl.row0 = row0;
+      tl.mrows = min(256, mrows);
+      tl.n0 = nt * 256;
+      tl.nrows = min(256, N - tl.n0);
+      tl.xr = rsrc(X + (long)row0 * K, (long)tl.mrows * K * 2);
+      tl.wr = rsrc(Wt + (long)tl.n0 * K, (long)tl.nrows * K * 2);
+      return tl;
+    }
+    tl.idx = cnt;
+    return tl;
+  };
+
+  Tile cur = find(sl);
+  if (cur.idx >= cnt) return;  // uniform: nothing for this workgroup
+  Tile nxt = find(cur.idx + per);
+
+  // ---- DMA: piece p of a half-tile = rows (p * 4 + wave) * 8 + (lane >> 3); the lane's offset
+  // (row, swizzled 16-B chunk) is one constant, p and k go to soffset ----
+  const int rl0 = wave * 8 + (lane >> 3);
+  const uint32_t vo = (uint32_t)(((long)rl0 * K + (((lane & 7) ^ ((rl0 >> 1) & 7)) * 8)) * 2);
+  // global k-tile stream position of the next DMA: half-tiles h = 2 * gk + o live in slot h % 5
+  auto piece = [&](const __amdgpu_buffer_rsrc_t& r, int p, int kt, int slot) {
+    char* dst = smem + slot * HS + (p * 4 + wave) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, vo, kt * 128 + p * 64 * K, 0, 0);
+  };
+
+  int rd[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) rd[ks] = (lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+  auto frag = [&](int slot, int ks, int o, int blk) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + rd[ks]);
+  };
+
+  f32x4 acc[8][8];
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // one 32-deep sub-step (see gemm_w4_kernel); FIRST: the tile's first sub-step (C = 0)
+  auto sub = [&](bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], int sa, int sb, int nks,
+                 const __amdgpu_buffer_rsrc_t& dr, int kt, int ds, auto first) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (decltype(first)::value)
+          acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        else
+          acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 3 * g; q < 3 * g + 3 && q < 16; ++q) {
+        if (q < 8) nb[q] = frag(sb, nks, 1, q);
+        else na[q - 8] = frag(sa, nks, 0, q - 8);
+      }
+      piece(dr, g, kt, ds);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue (first tile only): k-tiles 0 and 1 (of the next tile when nk == ... nk >= 2 here)
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) piece((h & 1) ? cur.wr : cur.xr, p, h >> 1, h);
+  vm_wait_n<16>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    fa0[g] = frag(0, 0, 0, g);
+    fb0[g] = frag(1, 0, 1, g);
+  }
+
+  int h0 = 0;  // (2 * global k-tile) % 5 of the current k-tile
+  const int ldy = EPI == TILE_EPI_SWIGLU ? (N >> 1) : N;
+  const int ml = lane & 15, nq = 4 * (lane >> 4);
+  while (true) {
+    for (int t = 0; t < nk; ++t) {
+      const int sa = h0, sb = h0 + 1 == 5 ? 0 : h0 + 1;
+      const int sa1 = h0 + 2 >= 5 ? h0 - 3 : h0 + 2, sb1 = h0 + 3 >= 5 ? h0 - 2 : h0 + 3;
+      const int da = h0 + 4 >= 5 ? h0 - 1 : h0 + 4, db = h0;  // A/B half-slots of k-tile t + 2
+      // the k-tile two ahead: of this tile, or the next one's (a dummy re-read after the last tile)
+      const bool in_cur = t + 2 < nk || nxt.idx >= cnt;
+      const __amdgpu_buffer_rsrc_t ax = in_cur ? cur.xr : nxt.xr, aw = in_cur ? cur.wr : nxt.wr;
+      const int k2 = t + 2 < nk ? t + 2 : (nxt.idx >= cnt ? nk - 1 : t + 2 - nk);
+      if (t == 0)
+        sub(fa0, fb0, fa1, fb1, sa, sb, 1, ax, k2, da, std::true_type{});
+      else
+        sub(fa0, fb0, fa1, fb1, sa, sb, 1, ax, k2, da, std::false_type{});
+      lgkm_wait0();
+      vm_wait_n<8>();
+      __builtin_amdgcn_s_barrier();
+      sub(fa1, fb1, fa0, fb0, sa1, sb1, 0, aw, k2, db, std::false_type{});
+      h0 = sa1;
+    }
+    // ---- epilogue of `cur`: acc[i][j][r] = Y[m][n], m = wm*128 + i*16 + (lane & 15),
+    // n = wn*128 + j*16 + 4 (lane >> 4) + r; 8-B stores through a descriptor over the tile's rows ----
+    {
+      const __amdgpu_buffer_rsrc_t yr = rsrc(Y + (long)cur.row0 * ldy, (long)cur.mrows * ldy * 2);
+      const int col0 = EPI == TILE_EPI_SWIGLU ? ((cur.n0 + wn * 128) >> 1) : cur.n0 + wn * 128;
+      const int ncols = EPI == TILE_EPI_SWIGLU ? (cur.nrows >> 1) - wn * 64 : cur.nrows - wn * 128;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t ro = (uint32_t)((wm * 128 + i * 16 + ml) * ldy * 2);
+        if constexpr (EPI == TILE_EPI_SWIGLU) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gt = bf2f(f2bf(acc[i][j][r])), up = bf2f(f2bf(acc[i][j + 4][r]));
+              o[r] = gt * up / (1.f + __expf(-gt));
+            }
+            const int c = j * 16 + nq;
+            const uint32_t off = c < ncols ? ro + (uint32_t)((col0 + c) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, yr, off, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4 v = acc[i][j];
+            const int c = j * 16 + nq;
+            const uint32_t off = c < ncols ? ro + (uint32_t)((col0 + c) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])}, yr, off, 0, 0);
+          }
+        }
+      }
+    }
+    if (nxt.idx >= cnt) break;
+    cur = nxt;
+    nxt = find(cur.idx + per);
+  }
+  vm_wait_n<0>();
 }
 
 }  // namespace k8sllm
@@ -505,13 +755,14 @@ using namespace k8sllm;
 // Grouped: W [E][N][K] with expert stride w_es elements; M = total expert-sorted rows (the grid
 // bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
 // algo 0: 4-wave 128 x 128 wave tiles (gemm_w4_kernel, N % 16 == 0, K % 64 == 0; SwiGLU N % 256);
+// algo 2: its persistent form (gemm_w4p_kernel, K >= 128; same shape rules);
 // algo 1: 8-wave 128 x 64 wave tiles (gemm_tile256_kernel, N % 256 == 0, K % 64 == 0).
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
                                 long w_es, int epi, int algo, hipStream_t s) {
   if (M <= 0) return 0;
   const bool grouped = offsets != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
-  if (algo == 0) {
+  if (algo == 0 || algo == 2) {
     if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
   } else if (N % 256 != 0 || K % 64 != 0 || K < 64) {
     return -1;
@@ -533,8 +784,23 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_SWIGLU, false);                                 \
     else K8_TILE_LAUNCH(KER_, NT_, TILE_EPI_BF16, false);                                                         \
   }
-  if (algo == 0) {
+  if (algo == 2 && K >= 128) {  // persistent: one workgroup per CU (multiple of 8: whole XCDs)
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = dim3((unsigned)max(8, min((long)(cus & ~7), (nwg + 7) & ~7L)));
+    K8_TILE_EPI(gemm_w4p_kernel, 256)
+  } else if (algo == 0 || algo == 2) {
     K8_TILE_EPI(gemm_w4_kernel, 256)
+  } else if (algo >= 20 && algo <= 23) {  // cache-policy variants of the 4-wave kernel (dense, bf16 out)
+    if (grouped || epi != TILE_EPI_BF16) return -1;
+#define K8_CP(CX, CW)                                                                                             \
+  hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 0, CX, CW>), grid, dim3(256), 0, s, (const bf16_t*)X, \
+                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+    if (algo == 20) K8_CP(17, 0);
+    else if (algo == 21) K8_CP(0, 17);
+    else if (algo == 22) K8_CP(17, 17);
+    else K8_CP(2, 2);
+#undef K8_CP
   } else if (algo == 10 || algo == 11) {  // diagnosis builds of the 4-wave kernel (dense, bf16 out)
     if (grouped || epi != TILE_EPI_BF16) return -1;
     if (algo == 10)

@@ -67,14 +67,26 @@ class CustomAllReduce:
         """Enqueue a copy of the error flag into ``host_flag`` (pinned int32) on the current stream."""
         self._n.car_error_async(self.state, host_flag)
 
-    def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
-        """In-place sum over the group (x must satisfy ``fits``)."""
-        self._n.car_all_reduce(self.state, x, x, self.spin_limit)
+    def all_reduce_(self, x: torch.Tensor, algo: int = -1) -> torch.Tensor:
+        """In-place sum over the group (x must satisfy ``fits``).  ``algo``: 0 one-shot, 1 two-shot
+        (reduce-scatter + all-gather in one launch), -1 auto (two-shot from 512 KiB at TP > 2)."""
+        self._n.car_all_reduce(self.state, x, x, self.spin_limit, algo)
         return x
 
-    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+    def all_reduce(self, x: torch.Tensor, algo: int = -1) -> torch.Tensor:
         out = torch.empty_like(x)
-        self._n.car_all_reduce(self.state, x, out, self.spin_limit)
+        self._n.car_all_reduce(self.state, x, out, self.spin_limit, algo)
+        return out
+
+    def fits_tail(self, M: int, d: int) -> bool:
+        return 0 < M <= 256 and d % 32 == 0 and d <= 8192 and M * d <= self.max_elems
+
+    def fused_tail(self, slabs: torch.Tensor, nslabs: int, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                   out: torch.Tensor, packed: bool) -> torch.Tensor:
+        """The TP row-parallel tail of a decode layer in ONE launch: this rank's split-K slabs
+        [nslabs, M, d] summed, all-reduced over the group, ``residual += `` the result, RMSNorm * w
+        written to ``out`` (row-major, or fragment-packed for the next skinny GEMM)."""
+        self._n.car_fused_tail(self.state, slabs, nslabs, residual, norm_w, out, eps, packed, self.spin_limit)
         return out
 
     def error(self) -> bool:

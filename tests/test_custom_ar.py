@@ -95,6 +95,37 @@ def _rank_main(rank: int, world: int, port: int, q) -> None:
             if not torch.equal(got, torch.stack(parts)):
                 bad.append(("gather", n))
             car.all_reduce(xc[:8].cuda())
+        # two-shot (reduce-scatter + all-gather in one launch) and one-shot interleaved at many
+        # sizes: the same rank-order fp32 sums, so both must equal the reference exactly
+        for it, n in enumerate([8, 64 * 4096, 4096 * 8 + 8, 1 << 20, 24, 64 * 8192, 8] * 2):
+            xc = torch.randn(n, generator=g).bfloat16()
+            for algo in (1, 0):
+                out = car.all_reduce(xc.cuda(), algo=algo)
+                if not torch.equal(out.cpu(), ref_sum(xc)):
+                    bad.append(("two-shot" if algo else "one-shot", it, n))
+        # fused TP tail: slab sum -> all-reduce -> residual add -> RMSNorm -> row-major / packed
+        from k8s_llm_monitor_amd import ops
+
+        for M, d, ns, packed in ((5, 512, 2, False), (64, 4096, 3, True), (17, 8192, 1, True), (40, 1024, 4, False)):
+            slabs = torch.randn(ns, M, d, generator=g)
+            res = torch.randn(M, d, generator=g).bfloat16()
+            w = (1 + 0.1 * torch.randn(d, generator=g)).bfloat16()
+            part = slabs.sum(0).bfloat16()
+            y = ref_sum(part.reshape(-1)).reshape(M, d).float()
+            r2 = (res.float() + y).bfloat16().float()
+            ref_out = (r2 * torch.rsqrt(r2.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()).bfloat16()
+            rg = res.cuda()
+            out = ops.packed_empty(M, d, torch.bfloat16, "cuda") if packed else torch.empty(M, d, dtype=torch.bfloat16,
+                                                                                             device="cuda")
+            car.fused_tail(slabs.cuda().contiguous(), ns, rg, w.cuda(), 1e-5, out, packed)
+            got = out.cpu()
+            if packed:
+                got = ops.unpack_skinny(got.view(-1, d // 32, 64, 8))[:M]
+            if not torch.equal(rg.cpu(), r2.bfloat16()):
+                bad.append(("tail-residual", M, d))
+            err = (got.float() - ref_out.float()).abs().max().item()
+            if err > 2e-2 * ref_out.float().abs().max().item():
+                bad.append(("tail-out", M, d, packed, err))
         # hipGraph: three captured calls per replay, fresh inputs every replay
         n = 64 * 4096
         sin = torch.empty(n, dtype=torch.bfloat16, device="cuda")

@@ -43,6 +43,11 @@ def main() -> None:
         y = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
         cases.append((name, 2 * T * N * K, {
             "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
+            "w4p": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=2)),
+            "w4_cpx": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=20)),
+            "w4_cpw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=21)),
+            "w4_cpxw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=22)),
+            "w4_nt": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=23)),
             "w4_nomfma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=10)),
             "w4_nodma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=11)),
             "tile": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
@@ -53,6 +58,7 @@ def main() -> None:
     act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
+        "w4p": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2)),
         "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
         "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
         "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
@@ -85,12 +91,14 @@ def main() -> None:
 
     cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=0)),
+        "w4p": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=2)),
         "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
         "hipblaslt_loop": loop13,
     }))
     cases.append(("moe_w2", 2 * rows * d * F, {
         "w4": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=0)),
+        "w4p": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=2)),
         "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
         "hipblaslt_loop": loop2,
