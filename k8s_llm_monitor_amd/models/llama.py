@@ -7,9 +7,12 @@ the remote ``callLLMAPI`` step of the doc sketch ``docs/metrics-usage-example.md
 Hot path per layer (GPU), all on the current HIP stream so a decode step captures into one
 hipGraph:
 
-  fused_add_rms_norm (HIP) -> QKV GEMM (hipBLASLt) -> rope_and_cache (HIP: RoPE + paged KV write)
+  fused_add_rms_norm (HIP) -> QKV GEMM -> rope_and_cache (HIP: RoPE + paged KV write)
   -> flash_prefill | paged_decode (HIP MFMA) -> o_proj GEMM (+ RCCL all-reduce at TP>1)
-  -> fused_add_rms_norm (HIP) -> gate_up GEMM -> silu_mul (HIP) -> down GEMM (+ all-reduce)
+  -> fused_add_rms_norm (HIP) -> gate_up GEMM + SwiGLU -> down GEMM (+ all-reduce)
+
+Prefill GEMMs go through ops.prefill_linear: the hand-written 4-wave MFMA kernel
+(ops/csrc/gemm_tile.hip, SwiGLU fused in its epilogue) or hipBLASLt per measured shape.
 
 Dense decode runs all four projections through the skinny MFMA GEMM over the same row-major
 weights prefill uses (ops/csrc/gemm_skinny.hip, LDS-DMA whole-line staging; ``_init_skinny``):
@@ -230,7 +233,7 @@ class CausalLM:
 
     def _attention(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv) -> torch.Tensor:
         o = self._attn_core(L, x, meta, kv)
-        y = F.linear(o, L["wo"])
+        y = ops.prefill_linear(o, L["wo"]) if "bo" not in L else F.linear(o, L["wo"])
         if "bo" in L and self.rank == 0:
             y += L["bo"]
         return tp_all_reduce(y, self.ps)
@@ -264,8 +267,10 @@ class CausalLM:
                                               workspace=meta.decode_ws, out=out)
             partial = ws
             qkv = torch.empty(T, ops.skinny_wdims(L["wqkv_p"])[0], dtype=self.dtype, device=self.device)
+        elif "bqkv" in L:
+            qkv = F.linear(x, L["wqkv"], L["bqkv"])
         else:
-            qkv = F.linear(x, L["wqkv"], L.get("bqkv"))
+            qkv = ops.prefill_linear(x, L["wqkv"])
         if not (slabs is not None and self._fuse_rope):
             ops.rope_and_cache(qkv, meta.positions, cs, k_cache, v_cache,
                                meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, self.D,
@@ -307,8 +312,11 @@ class CausalLM:
             if not meta.is_prefill and self.tp > 1 and self.moe_decode == "a2a":
                 return self._moe_a2a_decode(L, x)
             return tp_all_reduce(self._moe(L, x, meta), self.ps)
-        h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=self._w13_il)
-        return tp_all_reduce(F.linear(h, L["w2"]), self.ps)
+        if self._w13_il:
+            h = ops.prefill_linear(x, L["w13"], swiglu=True)
+        else:
+            h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=False)
+        return tp_all_reduce(ops.prefill_linear(h, L["w2"]), self.ps)
 
     def _moe(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         """Top-k MoE over this rank's experts [e_lo, e_hi).  Prefill: tokens are sorted by expert

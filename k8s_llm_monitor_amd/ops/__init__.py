@@ -802,6 +802,33 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
     return out
 
 
+# Prefill projections (qkv / o / gate_up + SwiGLU / down) on the hand-written 4-wave MFMA GEMM
+# (csrc/gemm_tile.hip gemm_w4_kernel) or hipBLASLt (torch F.linear).  K8SLLM_PREFILL_GEMM=tile|blas
+# forces one; the default routes the shapes where the tile kernel measured at least at parity
+# (profiles/r03/README.md).
+PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "auto")
+TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
+
+
+def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ w^T`` for a prefill-sized ``x`` [M, K] and row-major ``w`` [N, K]; ``swiglu``: ``w`` is
+    gate/up-interleaved (interleave_gate_up) and the result is silu(gate) * up [M, N / 2] - fused
+    into the tile kernel's epilogue, or F.linear + silu_mul on the library path."""
+    M, K = x.shape
+    N = w.shape[0]
+    mode = PREFILL_GEMM
+    tile_ok = (_gpu(x) and M >= TILE_MIN_M and N % 16 == 0 and K % 64 == 0 and K >= 128
+               and (not swiglu or N % 256 == 0) and N * K * 2 < (1 << 31))
+    use_tile = tile_ok and (mode == "tile" or (mode == "auto" and swiglu))
+    if use_tile:
+        return gemm_tile(x, w, swiglu=swiglu, out=out, algo=0)
+    y = torch.nn.functional.linear(x, w)
+    if swiglu:
+        return silu_mul(y, out=out, interleaved=True)
+    return out.copy_(y) if out is not None else y
+
+
 def moe_combine(y: torch.Tensor, inv_idx: torch.Tensor, w: torch.Tensor, T: int) -> torch.Tensor:
     if not _gpu(y):
         return ref.moe_combine(y, inv_idx, w, T)

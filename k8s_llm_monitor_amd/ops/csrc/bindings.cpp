@@ -67,6 +67,7 @@ int k8sllm_car_fused_tail(void* state, const float* slabs, int ns, long slab_str
                           void* out, long ldo, int M, int d, float eps, int packed, long spin_limit, hipStream_t s);
 int k8sllm_car_error(void* state);
 int k8sllm_car_all_gather(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
+int k8sllm_car_all_to_all(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
 int k8sllm_car_error_async(void* state, void* host_dst, hipStream_t s);
 void k8sllm_car_destroy(void* state);
 }
@@ -759,6 +760,15 @@ void car_all_gather(int64_t state, torch::Tensor in, torch::Tensor out, int64_t 
         "car_all_gather");
 }
 
+void car_all_to_all(int64_t state, torch::Tensor in, torch::Tensor out, int64_t spin_limit) {
+  dev_bf16(in, "in"); dev_bf16(out, "out");
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && out.numel() == in.numel() &&
+                  out.data_ptr() != in.data_ptr(), "car_all_to_all layout");
+  check(k8sllm_car_all_to_all((void*)(intptr_t)state, in.data_ptr(), out.data_ptr(), (long)in.numel(),
+                              (long)spin_limit, cur()),
+        "car_all_to_all");
+}
+
 int64_t car_error(int64_t state) { return k8sllm_car_error((void*)(intptr_t)state); }
 
 void car_error_async(int64_t state, torch::Tensor host) {
@@ -801,6 +811,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("car_all_reduce", &car_all_reduce, py::arg("state"), py::arg("in"), py::arg("out"), py::arg("spin_limit"),
         py::arg("algo") = -1);
   m.def("car_fused_tail", &car_fused_tail);
+  m.def("car_all_to_all", &car_all_to_all);
   m.def("car_error", &car_error);
   m.def("car_all_gather", &car_all_gather);
   m.def("car_error_async", &car_error_async);

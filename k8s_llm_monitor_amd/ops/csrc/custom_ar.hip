@@ -124,8 +124,9 @@ __device__ __forceinline__ void sum_ranks8(const CarPeers& p, int world, long ha
   }
 }
 
-// MODE 0: one-shot all-reduce, 1: one-shot all-gather, 2: two-shot all-reduce.
-// n: elements of THIS rank's input (the all-gather output holds world * n).
+// MODE 0: one-shot all-reduce, 1: one-shot all-gather, 2: two-shot all-reduce, 3: all-to-all.
+// n: elements of THIS rank's input (the all-gather output holds world * n; the all-to-all input
+// and output are [world][n / world]: out[p] = peer p's in[rank]).
 template <int MODE>
 __global__ __launch_bounds__(256) void car_kernel(const bf16_t* in, bf16_t* out,  // may alias (reduce)
                                                   long n, long max_elems, int rank, int world, CarPeers p,
@@ -140,9 +141,24 @@ __global__ __launch_bounds__(256) void car_kernel(const bf16_t* in, bf16_t* out,
 
   uint4* mine = reinterpret_cast<uint4*>(p.buf[rank] + half);
   const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  if constexpr (MODE == 3) {
+    // workgroup b owns vectors [a0, a1) of EVERY destination's block, so the peer's workgroup b
+    // staged exactly the part of block `rank` this workgroup reads back (flag[peer][b])
+    const long mv = nv / world, pm = (mv + nb - 1) / nb;
+    const long a0 = (long)b * pm, a1 = min(mv, a0 + pm);
+    for (int q = 0; q < world; ++q)
+      for (long v = a0 + tid; v < a1; v += 256) mine[q * mv + v] = src[q * mv + v];
+    car_exchange<false>(p, rank, world, b, e, spin_limit);
+    for (int r = 0; r < world; ++r) {
+      const uint4* peer = reinterpret_cast<const uint4*>(p.buf[r] + half);
+      for (long v = a0 + tid; v < a1; v += 256) dst[r * mv + v] = peer[(long)rank * mv + v];
+    }
+    car_finish(my, e);
+    return;
+  }
   for (long v = v0 + tid; v < v1; v += 256) mine[v] = src[v];
   car_exchange<false>(p, rank, world, b, e, spin_limit);
-  uint4* dst = reinterpret_cast<uint4*>(out);
   if constexpr (MODE == 1) {
     for (int r = 0; r < world; ++r) {
       const uint4* peer = reinterpret_cast<const uint4*>(p.buf[r] + half);
@@ -355,6 +371,20 @@ extern "C" int k8sllm_car_all_gather(void* state, const void* in, void* out, lon
   if (int rc = car_check(st, n)) return rc;
   hipLaunchKernelGGL(car_kernel<1>, dim3(car_grid(n)), dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, n,
                      st->max_elems, st->rank, st->world, st->peers, spin_limit);
+  return (int)hipGetLastError();
+}
+
+// out[world][m] = (peer p's in[rank]) for p in rank order; in [world][m] (m = n / world bf16,
+// m % 8 == 0, n <= max_elems); out must not alias in.  Static shapes: hipGraph-capturable (the EP
+// decode dispatch / combine of fixed per-pair capacity).
+extern "C" int k8sllm_car_all_to_all(void* state, const void* in, void* out, long n, long spin_limit,
+                                     hipStream_t s) {
+  auto* st = (CarState*)state;
+  if (n <= 0) return 0;
+  if (n % ((long)st->world * 8)) return -1;
+  if (int rc = car_check(st, n)) return rc;
+  hipLaunchKernelGGL(car_kernel<3>, dim3(car_grid(n / st->world)), dim3(256), 0, s, (const bf16_t*)in,
+                     (bf16_t*)out, n, st->max_elems, st->rank, st->world, st->peers, spin_limit);
   return (int)hipGetLastError();
 }
 

@@ -425,15 +425,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
-  // one 32-deep sub-step: 64 MFMAs from (ca, cb); between the row blocks' MFMA groups the 16
-  // fragment reads of the next sub-step (k-half nks, slots sa / sb) - the W fragments first (the
-  // next sub-step's FIRST row block needs all eight of them), then the X fragments, all issued in
-  // the first six groups so no read is still in flight when the next sub-step (or the barrier's
-  // lgkmcnt(0)) needs it - and one DMA piece of half-tile (o, kt) into slot `ds` per group
-  // Issue order (sched_group_barrier): one DMA piece after each of the first 8 MFMAs (the global
-  // loads have the farthest to go), then one fragment read after each of the next 16 - every
-  // non-MFMA instruction sits in an MFMA's shadow instead of in a cluster that leaves the matrix
-  // pipe idle (nodma builds: 1.71 / 1.81 PF/s on qkv / down with it, from 1.51 / 1.69).
+  // One 32-deep sub-step: 64 MFMAs from (ca, cb), each carrying at most one other instruction in
+  // its shadow (explicit order: a sched_barrier after every MFMA).  The 8 DMA pieces of the
+  // sub-step ride MFMAs 4, 12, ..., 60 - evenly spread: an LDS-DMA instruction holds its wave's
+  // issue for tens of cycles (MI355X_MICROARCH.md, LDS-DMA piece issue cost), and bunched pieces
+  // starve the matrix pipe (measured: all 16 pieces of a k-tile in one sub-step, 8-13 % slower;
+  // 8 in a row at the sub-step start, 3-4 % slower than spread).  The 16 fragment reads of the
+  // next sub-step ride the other MFMAs from the first on (W blocks first: the next sub-step's first
+  // row block needs all eight), done by MFMA 17.
   auto sub = [&](bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], int sa, int sb, int nks,
                  int o, int kt, int ds) {
     __builtin_amdgcn_sched_barrier(0);
@@ -441,18 +440,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     for (int g = 0; g < 8; ++g) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int n = g * 8 + j;  // MFMA number in the sub-step; what rides in its shadow:
+        const int n = g * 8 + j;
         if constexpr (ABL == 1) {
           asm volatile("" ::"v"(cb[j]), "v"(ca[g]));  // keep the fragment reads alive
         } else {
           acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
         }
-        if (n < 8) {  // the 8 DMA pieces first (the global loads have the farthest to go)
-          if constexpr (ABL != 2) piece(o, n, kt, ds);
-        } else if (n < 16) {  // then W fragments 0-7 (the next sub-step's first row block needs all)
-          nb[n - 8] = frag(sb, nks, 1, n - 8);
-        } else if (n < 24) {  // then X fragments 0-7
-          na[n - 16] = frag(sa, nks, 0, n - 16);
+        const int q = n - (n > 4) - (n > 12);  // read index: skips the DMA slots 4 and 12
+        if (j == 4) {
+          if constexpr (ABL != 2) piece(o, g, kt, ds);
+        } else if (q < 8) {
+          nb[q] = frag(sb, nks, 1, q);
+        } else if (q < 16) {
+          na[q - 8] = frag(sa, nks, 0, q - 8);
         }
         __builtin_amdgcn_sched_barrier(0);
       }

@@ -78,6 +78,16 @@ class CustomAllReduce:
         self._n.car_all_reduce(self.state, x, out, self.spin_limit, algo)
         return out
 
+    def fits_a2a(self, x: torch.Tensor) -> bool:
+        """x [world, ...] bf16 with a per-destination block of a multiple of 8 elements."""
+        return (self.fits(x) and x.shape[0] == self.world and (x.numel() // self.world) % 8 == 0)
+
+    def all_to_all(self, x: torch.Tensor) -> torch.Tensor:
+        """out[p] = rank p's x[this rank] for x [world, ...] (fixed equal blocks; graph-capturable)."""
+        out = torch.empty_like(x)
+        self._n.car_all_to_all(self.state, x, out, self.spin_limit)
+        return out
+
     def fits_tail(self, M: int, d: int) -> bool:
         return 0 < M <= 256 and d % 32 == 0 and d <= 8192 and M * d <= self.max_elems
 
