@@ -255,6 +255,19 @@ def run_rank(a) -> None:
             out.append(d)
         return out
 
+    # progress heartbeat on stderr (a long wave otherwise prints nothing for minutes)
+    import threading
+
+    hb_stop = threading.Event()
+
+    def heartbeat() -> None:
+        t_hb = time.perf_counter()
+        while not hb_stop.wait(30.0):
+            c = eng.counters
+            print(f"[bench] rank {rank} +{time.perf_counter() - t_hb:.0f}s prefill {c['prefill_steps']} "
+                  f"decode {c['decode_steps']} mixed {c['mixed_steps']}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True, name="bench-heartbeat").start()
     for w in range(a.warmup):
         step(w)
     leaders_barrier()
@@ -268,6 +281,7 @@ def run_rank(a) -> None:
         torch.cuda.synchronize()
     leaders_barrier()
     elapsed = time.perf_counter() - t0
+    hb_stop.set()
     ok = [r for r in res if r.get("http_status", 200) == 200]
     stats = svc.stats()
     if eng.trace is not None and rank == 0:

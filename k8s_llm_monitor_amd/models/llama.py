@@ -411,19 +411,33 @@ class CausalLM:
             out = torch.cat([out, out.new_zeros(chunk - n, c.d_model)])
         return tp_all_gather_rows(out, self.ps)[:T]
 
+    def _a2a_equal(self, x: torch.Tensor) -> torch.Tensor:
+        """All-to-all of equal blocks x [P, ...] -> out[p] = rank p's x[this rank]: the IPC kernel
+        (custom_ar.hip, one launch, graph-capturable) on the GPU, else the group backend."""
+        car = self.ps.custom_ar
+        if car is not None and x.is_cuda and car.fits_a2a(x):
+            return car.all_to_all(x)
+        out = torch.empty_like(x)
+        n = x.shape[0]
+        tp_all_to_all(out.view(n, -1), x.reshape(n, -1), [1] * n, [1] * n, self.ps)
+        return out
+
     def _moe_a2a_decode(self, L: dict, x: torch.Tensor) -> torch.Tensor:
         """Expert-parallel MoE for DECODE steps with static shapes, so the
         step stays capturable in a hipGraph: rank r routes its ceil(M/P) slice of the (replicated)
-        rows; every (token, slot) pair is sent to the rank owning its expert through a fixed-
-        capacity all-to-all (cap = slice x top-k rows per rank pair, zero rows where a pair goes
-        elsewhere); each rank runs its local experts over what it received (masked per expert),
+        rows; every (token, slot) pair goes to the rank owning its expert through a fixed-capacity
+        all-to-all (cap = slice x top-k rows per rank pair, zero rows where a pair goes elsewhere;
+        the IPC all-to-all kernel on the GPU, custom_ar.hip); the owner runs its local experts on
+        what it received on the grouped skinny MFMA kernels (one launch for gate/up + SwiGLU of
+        every local expert, one for their down projections into split-K slabs weighted one-hot by
+        each row's expert - the slab sum IS the per-row expert selection), in chunks of 64 rows;
         the results return by the reverse all-to-all, are weighted and summed per token, and the
-        slices are all-gathered.  Compared with the replicated form (every rank runs its experts on
-        every token, then ONE all-reduce of [M, d]) it computes only routed pairs but moves two
-        all-to-alls plus an all-gather; at decode batch sizes both stream every local expert's
-        weights once.  Parity with the replicated form is tested on CPU (gloo, TP 2 and 4); a GPU
-        comparison needs two GPUs (RCCL refuses two ranks on one device, gloo has no CUDA
-        all-to-all)."""
+        slices are all-gathered.  Against the replicated form (every rank runs its experts on
+        every token, then one all-reduce) it computes only routed pairs but streams the local
+        expert weights once per 64-row chunk of the P x cap x K received rows, and moves two
+        all-to-alls plus an all-gather - so at decode batch sizes, where the step is bound by
+        streaming every expert's weights, the replicated form stays the default
+        (K8SLLM_MOE_DECODE=a2a selects this one)."""
         c = self.cfg
         P, r, K, d = self.tp, self.rank, c.top_k_experts, c.d_model
         epr = c.n_experts // P
@@ -439,20 +453,33 @@ class CausalLM:
         dest = (ids // epr).view(-1)  # [cap*K]
         sel = dest.unsqueeze(0) == torch.arange(P, device=x.device).unsqueeze(1)  # [P, cap*K]
         send = pair_x.unsqueeze(0) * sel.unsqueeze(-1).to(x.dtype)
-        send_e = torch.where(sel, (ids.view(-1) % epr).unsqueeze(0), torch.full_like(sel, -1, dtype=torch.long))
-        recv = torch.empty_like(send)
-        recv_e = torch.empty_like(send_e)
-        tp_all_to_all(recv.view(P * npair, d), send.view(P * npair, d), [npair] * P, [npair] * P, self.ps)
-        tp_all_to_all(recv_e.view(-1), send_e.view(-1), [npair] * P, [npair] * P, self.ps)
-        rows = recv.view(P * npair, d)
-        re = recv_e.view(-1, 1)
-        y = torch.zeros(P * npair, d, dtype=torch.float32, device=x.device)
-        for j in range(epr):
-            h = ops.silu_mul(F.linear(rows, L["w13"][j]), interleaved=self._w13_il)
-            y += F.linear(h, L["w2"][j]).float() * (re == j).float()
-        back = torch.empty(P * npair, d, dtype=x.dtype, device=x.device)
-        tp_all_to_all(back, y.to(x.dtype), [npair] * P, [npair] * P, self.ps)
-        res = back.view(P, npair, d)[dest, torch.arange(npair, device=x.device)]  # [cap*K, d]
+        # expert ids travel as bf16 (exact small integers, -1 = no pair), padded to 8 per block
+        ne = -(-npair // 8) * 8
+        send_e = torch.full((P, ne), -1.0, dtype=x.dtype, device=x.device)
+        send_e[:, :npair] = torch.where(sel, (ids.view(-1) % epr).unsqueeze(0), torch.full_like(sel, -1,
+                                                                                              dtype=torch.long)).to(x.dtype)
+        recv = self._a2a_equal(send.contiguous())
+        recv_e = self._a2a_equal(send_e)
+        R = P * npair
+        rows = recv.view(R, d)
+        re = recv_e[:, :npair].reshape(-1).float()
+        onehot = (re.unsqueeze(1) == torch.arange(epr, device=x.device, dtype=torch.float32).unsqueeze(0)).float()
+        ws = self._skinny_ws
+        if ws is not None and "w13_pg" in L:
+            y = torch.empty(R, d, dtype=x.dtype, device=x.device)
+            for c0 in range(0, R, ops.SKINNY_MAX_M):
+                mc = min(ops.SKINNY_MAX_M, R - c0)
+                act = ops.skinny_grouped_swiglu(ops.pack_activation(rows[c0:c0 + mc]), L["w13_pg"], rows=mc)
+                ns = ops.skinny_grouped_slabs(act, L["w2_pg"], ws, mc, onehot[c0:c0 + mc].contiguous(), splits=1)
+                ops.reduce_slabs(ws, ns, mc, d, dtype=x.dtype, out=y[c0:c0 + mc])
+        else:
+            yf = torch.zeros(R, d, dtype=torch.float32, device=x.device)
+            for j in range(epr):
+                h = ops.silu_mul(F.linear(rows, L["w13"][j]), interleaved=self._w13_il)
+                yf += F.linear(h, L["w2"][j]).float() * onehot[:, j:j + 1]
+            y = yf.to(x.dtype)
+        back = self._a2a_equal(y.view(P, npair, d))
+        res = back[dest, torch.arange(npair, device=x.device)]  # [cap*K, d]
         z = (res.view(cap, K, d).float() * w.unsqueeze(-1)).sum(1).to(x.dtype)
         return tp_all_gather_rows(z, self.ps)[:M]
 

@@ -68,6 +68,9 @@ def tp_all_gather_rows(x: torch.Tensor, ps=None) -> torch.Tensor:
     if st.tp_size == 1:
         return x
     x = x.contiguous()
+    car = st.custom_ar
+    if car is not None and car.fits_gather(x):  # one-shot IPC gather (EP decode slices)
+        return car.all_gather(x).reshape((st.tp_size * x.shape[0],) + tuple(x.shape[1:]))
     out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     if _rccl(st, x):
         dist.all_gather_into_tensor(out, x, group=st.tp_group)

@@ -40,6 +40,7 @@ class CustomAllReduce:
         if world < 2 or world > 8:
             raise ValueError("custom all-reduce supports 2..8 ranks")
         self.rank, self.world = rank, world
+        self.n_a2a_launches = 0
         self.max_elems = (max_bytes // 2) // 8 * 8
         self.spin_limit = int(spin_limit)
         self._n = native()
@@ -86,6 +87,7 @@ class CustomAllReduce:
         """out[p] = rank p's x[this rank] for x [world, ...] (fixed equal blocks; graph-capturable)."""
         out = torch.empty_like(x)
         self._n.car_all_to_all(self.state, x, out, self.spin_limit)
+        self.n_a2a_launches += 1  # host-side launches (graph captures included, replays not)
         return out
 
     def fits_tail(self, M: int, d: int) -> bool:
