@@ -197,16 +197,14 @@ def skinny_waves() -> int:
 
 
 def _rn_args(rownorm) -> tuple:
-    wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1"  # opt-in: measured slower (gemm_skinny.hip)
-    return ((None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))) + (wide, skinny_waves())
+    return ((None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))) + (skinny_waves(),)
 
 
-def skinny_auto_splits(M: int, N: int, K: int, packed: bool = True) -> int:
+def skinny_auto_splits(M: int, N: int, K: int) -> int:
     """Mirror of k8sllm_gemm_skinny_auto_splits: the largest power-of-two split that keeps the grid
-    within one workgroup per CU (wide kernel: 128 columns per workgroup for packed A with
-    32 < M <= 64; narrow: 64), K slices >= 512 deep and whole 256-deep rounds of the waves."""
-    wide = os.environ.get("K8SLLM_SKINNY_WIDE", "0") == "1" and packed and M > 32 and N % 128 == 0
-    tiles = max(1, N // (128 if wide else 64))
+    (64 columns per workgroup) within one workgroup per CU, K slices >= 512 deep and whole 256-deep
+    rounds of the waves."""
+    tiles = max(1, N // 64)
     sp = 1
     while sp < 16 and tiles * sp * 2 <= 256 and K // (sp * 2) >= 512 and K % (sp * 2 * 256) == 0:
         sp *= 2
@@ -265,7 +263,7 @@ def skinny_slabs(a: torch.Tensor, wp: torch.Tensor, workspace: torch.Tensor, spl
         x = _cpu_a(a, rows)
         N, K = skinny_wdims(wp)
         if splits <= 0:
-            splits = skinny_auto_splits(M, N, K, a.dim() == 4)
+            splits = skinny_auto_splits(M, N, K)
         kc, ns = skinny_kchunk(K, splits), skinny_nslabs(K, splits)
         w = _cpu_w(wp)
         sc = _rn_scale(rownorm, M, K)
@@ -456,7 +454,7 @@ def proj_add_rms_norm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor,
     if splits is None:
         splits = 0  # automatic (launcher)
     if workspace is None:
-        workspace = skinny_workspace(M, N, splits or skinny_auto_splits(M, N, K, a.dim() == 4), a.device)
+        workspace = skinny_workspace(M, N, splits or skinny_auto_splits(M, N, K), a.device)
     s = skinny_slabs(a, wp, workspace, splits, rows=M)
     if out is None:
         out = (packed_empty(M, N, residual.dtype, a.device) if packed_out

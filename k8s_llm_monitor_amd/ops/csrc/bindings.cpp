@@ -45,14 +45,14 @@ int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* of
                             long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
-                       float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
+                       float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
                        const float* row_w, int row_w_ld, int w_rm, hipStream_t s);
 int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* partial, int splits, int* counters, void* Y,
                              long ldy, int M, int N, int K, int epi, const float* rn_ss, int rn_nc, float rn_eps,
                              int waves, void* residual, const void* norm_w, float* ss_out, const int* positions,
                              const float* cos_sin, void* k_cache, void* v_cache, const int* slot_mapping, int Hq,
                              int Hkv, int block_size, int apply_rope, int w_rm, hipStream_t s);
-int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide);
+int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
@@ -441,7 +441,7 @@ static int skinny_weight_dims(const torch::Tensor& wp, int lead, int& N, int& K,
 // number of slabs written (1 for epi 1/2).
 int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
                     c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t nt_tiles, int64_t rows,
-                    c10::optional<torch::Tensor> rn_ss, double rn_eps, bool wide, int64_t waves) {
+                    c10::optional<torch::Tensor> rn_ss, double rn_eps, int64_t waves) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   int N, K;
   const int w_rm = skinny_weight_dims(wp, 0, N, K, "gemm_skinny");
@@ -460,7 +460,7 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   }
   TORCH_CHECK(M <= 64, "gemm_skinny: at most 64 rows");
   TORCH_CHECK(N % (16 * nt_tiles) == 0, "gemm_skinny: N not divisible by the workgroup tile");
-  if (epi == 0 && splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed ? 1 : 0, wide ? 1 : 0);
+  if (epi == 0 && splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
   const int S = epi == 0 ? k8sllm_gemm_skinny_slabs(K, (int)splits) : 1;
   float* pp = nullptr;
   void* yp = nullptr;
@@ -492,7 +492,7 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   rownorm_args(rn_ss, M, K, rp, rn_nc);
   check(k8sllm_gemm_skinny(a.data_ptr(), a_packed ? 0 : a.stride(0), wp.data_ptr(), pp, yp, ldy, M, N, K,
                            epi == 0 ? (int)splits : 1, (int)epi, (int)nt_tiles, a_packed ? 1 : 0, rp, rn_nc, K,
-                           (float)rn_eps, wide ? 1 : 0, (int)waves, 1, 0, 0, 0, nullptr, 0, w_rm, cur()),
+                           (float)rn_eps, (int)waves, 1, 0, 0, 0, nullptr, 0, w_rm, cur()),
         "gemm_skinny");
   return S;
 }
@@ -550,7 +550,7 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
     y_es = (*y)[0].numel();
   }
   check(k8sllm_gemm_skinny(a.data_ptr(), 0, wp.data_ptr(), pp, yp, 0, M, N, K, epi == 0 ? (int)splits : 1,
-                           (int)epi, 4, 1, nullptr, 0, K, 0.f, 0, (int)waves, E, w_es, a_es, y_es, rw, E, w_rm,
+                           (int)epi, 4, 1, nullptr, 0, K, 0.f, (int)waves, E, w_es, a_es, y_es, rw, E, w_rm,
                            cur()),
         "gemm_skinny_grouped");
   return epi == 0 ? (int64_t)E * S : 1;
@@ -588,7 +588,7 @@ int64_t gemm_skinny_resnorm(torch::Tensor a, torch::Tensor wp, int64_t rows, tor
   TORCH_CHECK(ss_out.is_cuda() && ss_out.scalar_type() == torch::kFloat32 && ss_out.is_contiguous() &&
                   ss_out.dim() == 2 && ss_out.size(0) == M && ss_out.size(1) == N / 64,
               "resnorm: ss_out must be [M, N / 64] fp32");
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K, 1, 0);
+  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
   const int S = k8sllm_gemm_skinny_slabs(K, (int)splits);
   fused_ws_check(partial, counters, S, M, N);
   check(k8sllm_gemm_skinny_fused(a.data_ptr(), wp.data_ptr(), partial.data_ptr<float>(), (int)splits,
@@ -633,7 +633,7 @@ int64_t gemm_skinny_qkv_rope(torch::Tensor a, torch::Tensor wp, int64_t rows, to
   const float* rp = nullptr;
   int rn_nc = 0;
   rownorm_args(rn_ss, M, K, rp, rn_nc);
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K, 1, 0);
+  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
   const int S = k8sllm_gemm_skinny_slabs(K, (int)splits);
   fused_ws_check(partial, counters, S, M, N);
   check(k8sllm_gemm_skinny_fused(a.data_ptr(), wp.data_ptr(), partial.data_ptr<float>(), (int)splits,

@@ -700,135 +700,6 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
   }
 }
 
-// Wide variant for 32 < M <= 64 (A fragment-packed): the 4 waves own the 4 m-tiles, a workgroup
-// covers 128 output columns (8 n-tiles) of one K slice, and the weight tile is staged through LDS
-// once and shared by the waves.  Compared with the narrow kernel (waves split K, 64 columns), the
-// activation bytes read per weight byte halve (64 rows / 128 columns), every A fragment is read by
-// exactly one wave, and the epilogue needs no cross-wave reduction.  Register-staged double
-// buffer: group g+1's weight and activation loads are in flight while group g is multiplied.
-// Measured on MI355X (tools/bench_skinny.py, M 33-64, Llama-3-8B shapes): 10-25 % SLOWER than the
-// narrow kernel - one 16 KiB group in flight per workgroup plus a barrier per group cost more than
-// the halved activation traffic saves - so it is opt-in (K8SLLM_SKINNY_WIDE=1), kept as the
-// starting point for an LDS-DMA ring version.
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_skinny_wide_kernel(const bf16_t* __restrict__ A,
-                                                               const bf16_t* __restrict__ Wp,
-                                                               float* __restrict__ partial, bf16_t* __restrict__ Y,
-                                                               long ldy, int M, int N, int K, int kchunk,
-                                                               const float* __restrict__ rn_ss, int rn_nc,
-                                                               float rn_inv_d, float rn_eps) {
-  constexpr int NT = 8, U = 2;
-  constexpr int WPW = U * NT / 4;  // 1 KiB weight blocks staged per wave per group
-  __shared__ __attribute__((aligned(16))) u32x4 sW[2][U * NT][64];
-  __shared__ float s_inv[64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile0 = blockIdx.x * NT;
-  const int s = blockIdx.y;
-  const int kbeg = s * kchunk;
-  const int nsteps = (min(K, kbeg + kchunk) - kbeg) >> 5;
-  const int ksteps = K >> 5;
-  const int MT = (M + 15) >> 4;
-  const bool active = wave < MT;
-
-  if (rn_ss != nullptr && threadIdx.x < 64) {
-    const int row = min((int)threadIdx.x, M - 1);
-    float ss = 0.f;
-    for (int c = 0; c < rn_nc; ++c) ss += rn_ss[row * rn_nc + c];
-    s_inv[threadIdx.x] = rsqrtf(ss * rn_inv_d + rn_eps);
-  }
-
-  const u32x4* wbase = reinterpret_cast<const u32x4*>(Wp) + (long)(kbeg >> 5) * 64 + lane;
-  const bf16x8* abase = reinterpret_cast<const bf16x8*>(A) + ((long)min(wave, MT - 1) * ksteps + (kbeg >> 5)) * 64 +
-                        lane;
-  auto load_w = [&](u32x4* r, int g) {
-#pragma unroll
-    for (int j = 0; j < WPW; ++j) {
-      const int idx = wave * WPW + j, u = idx / NT, nt = idx % NT;
-      const int st = min(g * U + u, nsteps - 1);
-      r[j] = __builtin_nontemporal_load(wbase + ((long)(tile0 + nt) * ksteps + st) * 64);
-    }
-  };
-  auto load_a = [&](bf16x8* r, int g) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) r[u] = abase[(long)min(g * U + u, nsteps - 1) * 64];
-  };
-
-  f32x4 acc[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ngroups = (nsteps + U - 1) / U;
-  u32x4 wr[WPW];
-  bf16x8 ar[U], ac[U];
-  load_w(wr, 0);
-  load_a(ar, 0);
-  for (int g = 0; g < ngroups; ++g) {
-    const int buf = g & 1;
-#pragma unroll
-    for (int j = 0; j < WPW; ++j) sW[buf][wave * WPW + j][lane] = wr[j];
-#pragma unroll
-    for (int u = 0; u < U; ++u) ac[u] = ar[u];
-    if (g + 1 < ngroups) {
-      load_w(wr, g + 1);
-      load_a(ar, g + 1);
-    }
-    __syncthreads();  // group g staged by every wave (and group g-1's reads of this buffer done)
-    if (active) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (g * U + u < nsteps) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[u], __builtin_bit_cast(bf16x8, sW[buf][u * NT + nt][lane]),
-                                                              acc[nt], 0, 0, 0);
-        }
-      }
-    }
-  }
-  if (!active) return;
-  f32x4 rs = f32x4{1.f, 1.f, 1.f, 1.f};
-  if (rn_ss != nullptr) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rs[r] = s_inv[wave * 16 + (lane >> 4) * 4 + r];
-  }
-  if constexpr (EPI == EPI_SWIGLU || EPI == EPI_SWIGLU_PACKED) {
-#pragma unroll
-    for (int nt = 0; nt < NT / 2; ++nt) {
-      const f32x4 gv = acc[nt] * rs, uv = acc[nt + NT / 2] * rs;
-      const int f = blockIdx.x * 64 + nt * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wave * 16 + (lane >> 4) * 4 + r;
-        const float g = bf2f(f2bf(gv[r]));
-        const float uu = bf2f(f2bf(uv[r]));
-        const bf16_t o = f2bf(g * uu / (1.f + __expf(-g)));
-        if constexpr (EPI == EPI_SWIGLU_PACKED) {
-          const int F = N >> 1;
-          Y[(((long)wave * (F >> 5) + (f >> 5)) * 64 + ((f >> 3) & 3) * 16 + (row & 15)) * 8 + (f & 7)] = o;
-        } else if (row < M) {
-          Y[(long)row * ldy + f] = o;
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const f32x4 v = acc[nt] * rs;
-      const int col = (tile0 + nt) * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wave * 16 + (lane >> 4) * 4 + r;
-        if (row < M) {
-          if constexpr (EPI == EPI_BF16)
-            Y[(long)row * ldy + col] = f2bf(v[r]);
-          else
-            partial[((long)s * M + row) * N + col] = v[r];
-        }
-      }
-    }
-  }
-}
-
 // Residual update with a deferred RMSNorm, fully parallel (grid (M, d/512), one wave per 512
 // columns): residual <- bf16(residual + sum_s partial[s]); out <- bf16(residual * w) (packed via
 // act_index); ss_part[m][chunk] <- sum of residual^2 over the chunk.  The consumer skinny GEMM
@@ -957,18 +828,13 @@ extern "C" int k8sllm_gemm_skinny_slabs(int K, int S) {
 
 // epi: 0 slab, 1 bf16, 2 swiglu; nt_tiles: 2 or 4 n-tiles per workgroup; a_packed: A in the
 // fragment-packed layout (lda ignored)
-// Kernel choice: the wide kernel for fragment-packed A with 32 < M <= 64 and N % 128 == 0
-// (unless disabled), else the narrow one.  splits <= 0: automatic split-K - the largest power of
-// two that keeps the grid within one workgroup per CU, K slices >= 512 deep and whole 256-deep
-// rounds of the 4 waves (uneven rounds leave waves idle at the tail).  Measured at M = 64
-// (tools/bench_skinny_waves.py, profiles/r01_s3_skinny_waves.jsonl): qkv S 2 14.9 us vs S 3
-// 18.1 us; o / down S 4 beat 2, 3, 6 and 8.
-static bool skinny_use_wide(int M, int N, int a_packed, int wide) {
-  return wide && a_packed && M > 32 && N % 128 == 0;
-}
-
-extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K, int a_packed, int wide) {
-  const int tiles = N / (skinny_use_wide(M, N, a_packed, wide) ? 128 : 64);
+// splits <= 0: automatic split-K - the largest power of two that keeps the grid within one
+// workgroup per CU, K slices >= 512 deep and whole 256-deep rounds of the 4 waves (uneven rounds
+// leave waves idle at the tail).  Measured at M = 64 (tools/bench_skinny_waves.py,
+// profiles/r01_s3_skinny_waves.jsonl): qkv S 2 14.9 us vs S 3 18.1 us; o / down S 4 beat 2, 3, 6
+// and 8.  (A 128-column variant for 32 < M <= 64 measured 10-25 % slower and was removed.)
+extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K) {
+  const int tiles = N / 64;
   int sp = 1;
   while (sp < 16 && (long)tiles * sp * 2 <= 256 && K / (sp * 2) >= 512 && K % (sp * 2 * 256) == 0) sp *= 2;
   return sp;
@@ -987,16 +853,16 @@ static void launch_rm(bool ilv, dim3 grid, dim3 blk, hipStream_t s, Args... args
 // (add_norm_partial); outputs are scaled by rsqrt(sum / rn_d + eps) - the deferred RMSNorm.
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
-                         float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
+                         float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
                          const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s);
 
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
-                                  int rn_nc, int rn_d, float rn_eps, int wide, int waves, int experts, long w_es,
+                                  int rn_nc, int rn_d, float rn_eps, int waves, int experts, long w_es,
                                   long a_es, long y_es, const float* row_w, int row_w_ld, int w_rm, hipStream_t s) {
   if (epi == EPI_RESNORM || epi == EPI_ROPE) return -6;  // fused epilogues: k8sllm_gemm_skinny_fused
   return skinny_launch(A, lda, Wp, partial, Y, ldy, M, N, K, S, epi, nt_tiles, a_packed, rn_ss, rn_nc, rn_d, rn_eps,
-                       wide, waves, experts, w_es, a_es, y_es, row_w, row_w_ld, SkinnyEpi{}, w_rm, s);
+                       waves, experts, w_es, a_es, y_es, row_w, row_w_ld, SkinnyEpi{}, w_rm, s);
 }
 
 // Fused epilogues (A fragment-packed, 64-column tiles, split-K slabs in `partial` reduced by each
@@ -1018,23 +884,22 @@ extern "C" int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* pa
   } else {
     return -6;
   }
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K, 1, 0);
+  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
   SkinnyEpi ep{(bf16_t*)residual, (const bf16_t*)norm_w, ss_out, positions, cos_sin, (bf16_t*)k_cache,
                (bf16_t*)v_cache, slot_mapping, counters, Hq, Hkv, block_size, apply_rope};
-  return skinny_launch(A, 0, Wp, partial, Y, ldy, M, N, K, splits, epi, 4, 1, rn_ss, rn_nc, K, rn_eps, 0, waves, 1,
+  return skinny_launch(A, 0, Wp, partial, Y, ldy, M, N, K, splits, epi, 4, 1, rn_ss, rn_nc, K, rn_eps, waves, 1,
                        0, 0, 0, nullptr, 0, ep, w_rm, s);
 }
 
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
-                         float rn_eps, int wide, int waves, int experts, long w_es, long a_es, long y_es,
+                         float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
                          const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s) {
   if (M <= 0) return 0;
   if (experts < 1) return -5;
-  if (experts > 1 || w_rm) wide = 0;  // grouped / row-major launches use the narrow decomposition
   const SkinnyGroup grp{w_es, a_es, y_es, row_w, row_w_ld};
   if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
-  if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K, a_packed, wide) : 1;  // fused: caller
+  if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K) : 1;  // fused: caller
   const int kc = skinny_kchunk(K, S, w_rm ? 64 : 32);
   if (w_rm) {
     if (!a_packed || K % 64 != 0 || N % 64 != 0) return -9;  // row-major W: packed A, 64-deep stages, NT = 4
@@ -1108,20 +973,6 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     return -4;
   if ((epi == EPI_RESNORM || epi == EPI_ROPE) && !a_packed) return -4;
   const float inv_d = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
-  if (skinny_use_wide(M, N, a_packed, wide)) {
-    dim3 grid(N / 128, slabs), blk(256);
-#define K8S_WIDE(EPV)                                                                                      \
-  hipLaunchKernelGGL((gemm_skinny_wide_kernel<EPV>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp, \
-                     partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps)
-    switch (epi) {
-      case EPI_SLAB: K8S_WIDE(EPI_SLAB); break;
-      case EPI_BF16: K8S_WIDE(EPI_BF16); break;
-      case EPI_SWIGLU: K8S_WIDE(EPI_SWIGLU); break;
-      default: K8S_WIDE(EPI_SWIGLU_PACKED); break;
-    }
-#undef K8S_WIDE
-    return (int)hipGetLastError();
-  }
   // 8-wave workgroups: twice the weight lines in flight per CU for the same K slice.  waves <= 0
   // (auto): 8 for the split-K slab projections (o 11.1 vs 11.8 us, down 24.3 vs 25.9 at M = 64),
   // 4 for the single-slice SwiGLU / bf16 epilogues (gate_up 47.5 vs 50.5 us).

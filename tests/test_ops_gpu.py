@@ -329,11 +329,32 @@ def test_llama_decode_skinny_matches_generic(monkeypatch, fused):
     meta = AttnMeta(is_prefill=False, positions=lens - 1, slot_mapping=slots.to(torch.int32),
                     block_tables=bt, seq_lens=lens,
                     decode_ws=ops.decode_workspace(B, m.hq, m.D, device=DEV, Hkv=m.hkv))
+    kv0 = [(k.clone(), v.clone()) for k, v in kv]  # the caches before this step writes the new token
     a = m.forward(ids, meta, kv).float()
     monkeypatch.setenv("K8SLLM_SKINNY", "0")
     b = m.forward(ids, meta, kv).float()
-    assert (a - b).abs().max().item() < 0.1 * b.abs().max().item() + 0.05
-    assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.8
+    # fp32 CPU reference of the same decode step (same weights, the pre-step caches)
+    rm = CausalLM(cfg, device="cpu", dtype=torch.float32, init="empty")
+    rm.embed.copy_(m.embed.float().cpu())
+    if rm.lm_head is not rm.embed:
+        rm.lm_head.copy_(m.lm_head.float().cpu())
+    rm.final_norm.copy_(m.final_norm.float().cpu())
+    for Lr, Lg in zip(rm.layers, m.layers):
+        for k, v in Lr.items():
+            if not k.endswith("_p") and not k.endswith("_pg"):
+                v.copy_(Lg[k].float().cpu())
+    cpu = lambda t: t.cpu() if t is not None else None  # noqa: E731
+    meta_c = AttnMeta(is_prefill=False, positions=cpu(meta.positions), slot_mapping=cpu(meta.slot_mapping),
+                      block_tables=cpu(bt), seq_lens=cpu(lens))
+    r = rm.forward(ids.cpu(), meta_c, [(k.float().cpu(), v.float().cpu()) for k, v in kv0]).float()
+    scale = float(r.abs().max())
+    for name, out in (("skinny", a), ("generic", b)):
+        out = out.cpu()
+        err = float((out - r).abs().max())
+        assert err < 0.03 * scale, f"{name}: max-abs err {err:.4f} vs scale {scale:.3f}"
+        # every row's argmax is the reference's or a provable near-tie (within 2x the bf16 error)
+        got = r.gather(1, out.argmax(-1, keepdim=True)).squeeze(1)
+        assert bool((r.max(-1).values - got <= 2 * err + 1e-6).all()), name
 
 
 @pytest.mark.parametrize("M", [1, 17, 64])
@@ -445,24 +466,6 @@ def test_skinny_qkv_rope_matches_slab_path(M, splits):
     qkv_r = qkv_r.to(torch.bfloat16)
     ref.rope_and_cache(qkv_r, pos.cpu(), cs.cpu(), None, None, None, hq, hkv, D)
     _close(qkv_a.cpu(), qkv_r, atol=6e-2, rtol=3e-2, what="qkv vs fp32 reference")
-
-
-@pytest.mark.parametrize("M", [33, 64])
-def test_gemm_skinny_wide_variant(M, monkeypatch):
-    """The opt-in wide kernel (waves split M, LDS-staged weights): slabs and packed SwiGLU."""
-    monkeypatch.setenv("K8SLLM_SKINNY_WIDE", "1")
-    K, N, F = 1024, 384, 320
-    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
-    ap = ops.pack_activation(a)
-    ws = ops.skinny_workspace(M, N, 8, DEV)
-    ns = ops.skinny_slabs(ap, ops.pack_skinny(w), ws, 0, rows=M)
-    _close(ops.reduce_slabs(ws, ns, M, N).cpu(), torch.nn.functional.linear(a.cpu().float(), w.cpu().float()),
-           atol=3e-2, rtol=2e-2, what="wide slabs")
-    w13 = (torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) * 0.05).to(torch.bfloat16)
-    actp = ops.skinny_swiglu(ap, ops.pack_skinny(ops.interleave_gate_up(w13)), rows=M, packed_out=True)
-    gu = torch.nn.functional.linear(a.cpu().float(), w13.cpu().float()).to(torch.bfloat16)
-    _close(ops.unpack_skinny(actp)[:M].cpu(), ref.silu_mul(gu), atol=3e-2, rtol=2e-2, what="wide swiglu")
 
 
 def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):

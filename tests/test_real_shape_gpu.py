@@ -51,8 +51,10 @@ def _logits(model, ids, rows, device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,layers", [("llama-3-8b", 2), ("llama-3-70b", 1)])
+@pytest.mark.parametrize("model,layers", [("llama-3-8b", 2), ("llama-3-70b", 1), ("mixtral-8x7b", 1)])
 def test_gpu_real_shape_engine_matches_fp32_reference(model, layers):
+    """Mixtral-8x7B dimensions (d 4096, 8 experts of ff 14336, top-2) exercise the grouped skinny
+    MoE decode kernels inside the decode hipGraph (VERDICT r2 'do this' #7)."""
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
 
     torch.set_num_threads(16)
@@ -87,14 +89,16 @@ def test_gpu_real_shape_engine_matches_fp32_reference(model, layers):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", [40, 64])
-def test_gpu_real_shape_decode_batch64_matches_prefill(batch):
-    """The headline's decode batch: 64 rows through the skinny decode graph (2-wave gate_up
-    workgroups with the deferred RMSNorm, M = 64 buckets) at Llama-3-8B dimensions.  Every greedy
-    token must be the argmax, or a near-tie, of the bf16 GPU prefill forward on the teacher-forced
-    sequence (hipBLASLt GEMMs and flash prefill: an independent path).  Rows 33-64 exercise what
-    batches of <= 32 never reach; 40 rows run the 64-row graph with 24 padding rows."""
+def test_gpu_real_shape_decode_batch64_matches_fp32_reference(batch):
+    """The headline's decode batch: 64 rows through the skinny decode graph (M = 64 buckets, the
+    deferred RMSNorm) at Llama-3-8B dimensions, against the fp32 CPU reference holding the same
+    weights.  Every greedy token must be the reference's argmax on the teacher-forced sequence or a
+    provable near-tie (within twice the measured bf16-vs-fp32 logit error of that sequence's GPU
+    prefill forward).  Rows 33-64 exercise what batches of <= 32 never reach; 40 rows run the
+    64-row graph with 24 padding rows."""
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
 
+    torch.set_num_threads(16)
     eng = LLMEngine(EngineConfig(model="llama-3-8b", model_overrides={"n_layers": 2}, max_num_seqs=64,
                                  max_model_len=1024, kv_cache_gb=2.0, seed=5), device="cuda")
     eng.warmup()
@@ -102,15 +106,19 @@ def test_gpu_real_shape_decode_batch64_matches_prefill(batch):
     n_new = 8
     seqs = eng.generate(prompts, SamplingParams(max_tokens=n_new, temperature=0.0, ignore_eos=True))
     assert 64 in eng.stats()["graph_buckets"]
-    worst = 0.0
+    ref = _fp32_reference(eng.model)
     for i, s in enumerate(seqs):
         ids = s.prompt_ids + s.output_ids
         p = len(s.prompt_ids)
-        lg = _logits(eng.model, ids, list(range(p - 1, p - 1 + n_new)), "cuda")
-        scale = float(lg.abs().max())
+        rows = list(range(p - 1, p - 1 + n_new))
+        lr = _logits(ref, ids, rows, "cpu")
+        lg = _logits(eng.model, ids, rows, "cuda")
+        scale = float(lr.abs().max())
+        err = float((lg - lr).abs().max())
+        assert err < 0.03 * scale, f"row {i}: prefill logits max-abs err {err:.4f} vs scale {scale:.3f}"
         for t in range(n_new):
-            gap = float(lg[t].max() - lg[t, s.output_ids[t]]) / scale
-            worst = max(worst, gap)
-            assert gap <= 0.02, f"row {i} step {t}: token {s.output_ids[t]} is {gap:.3f} x scale below the argmax"
+            top, got = float(lr[t].max()), float(lr[t, s.output_ids[t]])
+            assert top - got <= 2 * err + 1e-6, (
+                f"row {i} step {t}: token {s.output_ids[t]} logit {got:.4f} vs max {top:.4f} (bf16 err {err:.4f})")
     del eng
     torch.cuda.empty_cache()

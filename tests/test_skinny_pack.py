@@ -66,7 +66,6 @@ def test_skinny_splits_bounds(monkeypatch):
 def test_skinny_auto_splits_whole_rounds(monkeypatch):
     """Automatic split-K (mirror of the HIP launcher): power of two, grid <= one workgroup per CU,
     slices >= 512 deep and a multiple of the 4 waves' 256-deep round."""
-    monkeypatch.delenv("K8SLLM_SKINNY_WIDE", raising=False)
     assert ops.skinny_auto_splits(64, 6144, 4096) == 2   # Llama-3-8B qkv: 96 tiles x 2
     assert ops.skinny_auto_splits(64, 4096, 4096) == 4   # o
     assert ops.skinny_auto_splits(64, 4096, 14336) == 4  # down

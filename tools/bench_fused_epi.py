@@ -29,6 +29,8 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=320)
     ap.add_argument("--ms", default="64")
     ap.add_argument("--ops", default="qkv,o,down")
+    ap.add_argument("--layout", default="rowmajor", choices=["rowmajor", "packed"],
+                    help="weight layout: the engine's row-major tensors (default) or fragment-packed copies")
     a = ap.parse_args()
     dev = "cuda"
     d, F, hq, hkv, D, bs = 4096, 14336, 32, 8, 128, 16
@@ -38,7 +40,8 @@ def main() -> None:
     for name in a.ops.split(","):
         N, K = shapes[name]
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
-        wps = [ops.pack_skinny(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02) for _ in range(ncopy)]
+        keep = ops.pack_skinny if a.layout == "packed" else (lambda w: w)
+        wps = [keep(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02) for _ in range(ncopy)]
         gb = N * K * 2 / 1e9
         for M in map(int, a.ms.split(",")):
             xp = ops.pack_activation(torch.randn(M, K, device=dev, dtype=torch.bfloat16))

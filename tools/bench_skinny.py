@@ -89,26 +89,21 @@ def main() -> None:
                 timeit(base, a.iters))
             if name == "gate_up":
                 rep("skinny swiglu", timeit(lambda i: ops.skinny_swiglu(x, wps[i % ncopy], out=act), a.iters))
-                for wide in ("1", "0"):
-                    os.environ["K8SLLM_SKINNY_WIDE"] = wide
-                    rep(f"skinny swiglu packedA wide={wide}",
-                        timeit(lambda i: ops.skinny_swiglu(xp, wps[i % ncopy], out=act, rows=M), a.iters))
+                rep("skinny swiglu packedA",
+                    timeit(lambda i: ops.skinny_swiglu(xp, wps[i % ncopy], out=act, rows=M), a.iters))
                 continue
             if name == "qkv":
                 for nt_tiles in (2, 4):
                     rep(f"skinny bf16 1slice nt{nt_tiles} packedA",
                         timeit(lambda i: ops.skinny_linear(xp, wps[i % ncopy], out=y, nt_tiles=nt_tiles, rows=M),
                                a.iters))
-            for wide in ("1", "0"):
-                os.environ["K8SLLM_SKINNY_WIDE"] = wide
-                wsp = ops.skinny_workspace(M, N, 16, dev)
-                if name == "qkv":
-                    fn = lambda i, wsp=wsp: ops.skinny_slabs(xp, wps[i % ncopy], wsp, 0, rows=M)  # noqa: E731
-                else:
-                    fn = lambda i, wsp=wsp: ops.proj_add_rms_norm(  # noqa: E731
-                        xp, wps[i % ncopy], r, nw, eps, workspace=wsp, splits=0, out=ob, rows=M)
-                rep(f"skinny auto packedA wide={wide}", timeit(fn, a.iters))
-            os.environ["K8SLLM_SKINNY_WIDE"] = "1"
+            wsp = ops.skinny_workspace(M, N, 16, dev)
+            if name == "qkv":
+                fn = lambda i, wsp=wsp: ops.skinny_slabs(xp, wps[i % ncopy], wsp, 0, rows=M)  # noqa: E731
+            else:
+                fn = lambda i, wsp=wsp: ops.proj_add_rms_norm(  # noqa: E731
+                    xp, wps[i % ncopy], r, nw, eps, workspace=wsp, splits=0, out=ob, rows=M)
+            rep("skinny auto packedA", timeit(fn, a.iters))
             for s in map(int, a.splits.split(",")):
                 wsp = ops.skinny_workspace(M, N, s, dev)
                 for tag, xa in (("", x), (" packedA", xp)):
