@@ -249,14 +249,7 @@ class CausalLM:
         partial, ns = None, 0
         T = rows if rows is not None else x.shape[0]
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
-        if slabs is not None and self._fuse_rope:
-            # qkv GEMM + RoPE + KV-cache write in one launch (gemm_skinny ROPE epilogue)
-            qkv = torch.empty(T, ops.skinny_wdims(L["wqkv_p"])[0], dtype=self.dtype, device=self.device)
-            ops.skinny_qkv_rope(x, L["wqkv_p"], qkv, meta.positions, cs, k_cache, v_cache,
-                                meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, rows=T,
-                                apply_rope=c.arch == "llama", rownorm=rownorm, workspace=slabs[0],
-                                splits=slabs[1])
-        elif slabs is not None:
+        if slabs is not None:
             ws, splits = slabs
             ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T, rownorm=rownorm)
             if self._attn_rope and not meta.is_prefill and k_cache is not None and c.arch == "llama":
@@ -271,10 +264,9 @@ class CausalLM:
             qkv = F.linear(x, L["wqkv"], L["bqkv"])
         else:
             qkv = ops.prefill_linear(x, L["wqkv"])
-        if not (slabs is not None and self._fuse_rope):
-            ops.rope_and_cache(qkv, meta.positions, cs, k_cache, v_cache,
-                               meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, self.D,
-                               apply_rope=c.arch == "llama", partial=partial, nslabs=ns)
+        ops.rope_and_cache(qkv, meta.positions, cs, k_cache, v_cache,
+                           meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, self.D,
+                           apply_rope=c.arch == "llama", partial=partial, nslabs=ns)
         if meta.is_prefill:
             qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
             paged = None
@@ -570,25 +562,19 @@ class CausalLM:
                 del w
             self._w13_il = True
         self._w13_il = getattr(self, "_w13_il", False)
-        # opt-in fused epilogues (K8SLLM_FUSED_EPI=1): RoPE + KV write in the qkv GEMM (head_dim
-        # 128, any TP); residual add + norm producer in the o / down GEMMs (TP=1 dense: the
-        # row-parallel sums need the all-reduce first), each reduced in-launch by the tile's last
-        # K-slice workgroup.  Measured on MI355X at M = 64 (tools/bench_fused_epi.py,
-        # profiles/r01_s5_fused_epilogues.jsonl) 1-2 us per layer-op SLOWER than the slab GEMM +
-        # separate reduce kernel: the agent-scope release / ticket / acquire round trip of the
-        # last arriver costs more than the launch boundary it saves, so the default keeps the pair.
-        fuse = os.environ.get("K8SLLM_FUSED_EPI", "0") == "1"
-        self._fuse_rope = fuse and self.D == 128
+        # (In-launch split-K epilogues - RoPE + KV write in the qkv GEMM, residual add + norm
+        # producer in the o / down GEMMs, reduced by each tile's last-arriving workgroup - measured
+        # 5-6 us per layer-op SLOWER than the slab GEMM + separate reduce kernel on the row-major
+        # kernel too (profiles/r03/fused_epilogues_rowmajor.jsonl) and were removed.)
         # decode RoPE + KV write inside the attention kernel (paged_decode_fused), reading the qkv
         # GEMM's split-K slabs directly: one launch per layer fewer (K8SLLM_ATTN_ROPE=0 disables)
-        self._attn_rope = not self._fuse_rope and self.D == 128 and os.environ.get("K8SLLM_ATTN_ROPE", "1") != "0"
-        self._fuse_resnorm = fuse and self.tp == 1 and not c.is_moe and c.d_model % 64 == 0
+        self._attn_rope = self.D == 128 and os.environ.get("K8SLLM_ATTN_ROPE", "1") != "0"
         if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0" or not self._w13_il:
-            self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
+            self._attn_rope = False
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
         if d % 64 or nq % 64 or (self.hq * self.D) % 32:
-            self._fuse_rope = self._fuse_resnorm = self._attn_rope = False
+            self._attn_rope = False
             return
         rowmajor = os.environ.get("K8SLLM_SKINNY_LAYOUT", "rowmajor") != "packed" and (self.hq * self.D) % 64 == 0
         self.skinny_layout = "rowmajor" if rowmajor else "packed"
@@ -612,8 +598,6 @@ class CausalLM:
         n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d,
                 (self.e_hi - self.e_lo) * ops.skinny_nslabs(ff, 1) * d if c.is_moe else most(d, ff) * d)
         self._skinny_ws = torch.empty(n * ops.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
-        if self.device.type == "cuda" and (self._fuse_rope or self._fuse_resnorm):
-            ops.fused_counters(self.device)  # allocated (zeroed) before any hipGraph capture
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list]) -> torch.Tensor:
@@ -628,14 +612,6 @@ class CausalLM:
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
-            if self._fuse_resnorm:  # o / down GEMMs add into the residual and produce the next norm
-                xw, ss = ops.skinny_resnorm(op, L["wo_p"], residual, L["mlp_norm"], rows=M, workspace=ws,
-                                            splits=self._split_o)
-                act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=(ss, eps))
-                nw = self.layers[i + 1]["attn_norm"] if i + 1 < n else self.final_norm
-                xw, ss = ops.skinny_resnorm(act, L["w2_p"], residual, nw, rows=M, workspace=ws, splits=self._split_d)
-                rn = (ss, eps)
-                continue
             ns = ops.skinny_slabs(op, L["wo_p"], ws, self._split_o, rows=M)
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
                 # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated
@@ -660,9 +636,6 @@ class CausalLM:
             if i + 1 < n:
                 xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
         # final norm feeds the LM head (hipBLASLt): complete, row-major
-        if self._fuse_resnorm:
-            x = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, None, 0, self.final_norm, eps)
-            return self._logits(x)
         x = self._tp_tail(ws, ns, residual, self.final_norm, packed=False)
         if x is not None:
             return self._logits(x)

@@ -338,76 +338,6 @@ def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], 
     return out, ss_part
 
 
-_COUNTERS: dict = {}
-
-
-def fused_counters(device, n: int = 4096) -> torch.Tensor:
-    """Zeroed int32 split-K tile tickets shared by the fused skinny epilogues on ``device`` (the
-    launches are stream-ordered and every launch leaves them zero again).  Allocated outside any
-    hipGraph capture by the first call (the model calls it at init)."""
-    key = str(torch.device(device))
-    t = _COUNTERS.get(key)
-    if t is None or t.numel() < n:
-        t = _COUNTERS[key] = torch.zeros(n, dtype=torch.int32, device=device)
-    return t
-
-
-def _fused_ws(workspace: Optional[torch.Tensor], M: int, N: int, splits: int, device) -> torch.Tensor:
-    return workspace if workspace is not None else skinny_workspace(M, N, max(splits, 16), device)
-
-
-def skinny_resnorm(a: torch.Tensor, wp: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, rows: int,
-                   out: Optional[torch.Tensor] = None, ss: Optional[torch.Tensor] = None,
-                   workspace: Optional[torch.Tensor] = None, splits: int = 0) -> tuple:
-    """The o / down projection with the residual add and the deferred-RMSNorm producer fused in
-    (gemm_skinny RESNORM: split-K slabs reduced by each 64-column tile's last-arriving workgroup):
-    ``residual <- bf16(residual + a @ W^T)``; returns ``(residual * norm_w`` fragment-packed,
-    ``ss [M, N/64])`` - per-row sums of squares of each tile - for a consumer skinny GEMM called
-    with ``rownorm=(ss, eps)``.  Replaces skinny_slabs + add_norm_partial (one launch fewer)."""
-    M, N = rows, skinny_wdims(wp)[0]
-    nc = N // 64
-    if ss is None:
-        ss = torch.empty(M, nc, dtype=torch.float32, device=residual.device)
-    if out is None:
-        out = packed_empty(M, N, residual.dtype, residual.device)
-    if not _gpu(a):
-        y = _cpu_a(a, rows).float() @ _cpu_w(wp).t()
-        residual.copy_((residual.float() + y).to(residual.dtype))
-        v = residual.float()
-        ss.copy_((v * v).view(M, nc, 64).sum(-1))
-        out.copy_(pack_activation((v * norm_w.float()).to(residual.dtype)))
-        return out, ss
-    native().gemm_skinny_resnorm(a, wp, M, residual, norm_w, out, ss, _fused_ws(workspace, M, N, splits, a.device),
-                                 fused_counters(a.device), splits, skinny_waves())
-    return out, ss
-
-
-def skinny_qkv_rope(a: torch.Tensor, wp: torch.Tensor, qkv: torch.Tensor, positions: torch.Tensor,
-                    cos_sin: torch.Tensor, k_cache: Optional[torch.Tensor], v_cache: Optional[torch.Tensor],
-                    slot_mapping: Optional[torch.Tensor], Hq: int, Hkv: int, rows: int, apply_rope: bool = True,
-                    rownorm: Optional[tuple] = None, workspace: Optional[torch.Tensor] = None,
-                    splits: int = 0) -> torch.Tensor:
-    """The decode qkv projection with RoPE and the paged KV-cache write fused in (gemm_skinny ROPE,
-    head_dim 128, split-K slabs reduced by each tile's last-arriving workgroup): ``qkv[:rows]``
-    receives the rotated rows (q is read from there by paged_decode), k / v land in the cache at
-    ``slot_mapping``.  Replaces skinny_slabs + rope_and_cache (one launch fewer)."""
-    if not _gpu(a):
-        skinny_linear(a, wp, out=qkv[:rows], rows=rows, rownorm=rownorm)
-        ref.rope_and_cache(qkv[:rows], positions[:rows], cos_sin, k_cache, v_cache,
-                           slot_mapping[:rows] if slot_mapping is not None else None, Hq, Hkv, 128, apply_rope)
-        return qkv
-    empty = _empty_i32(qkv.device)
-    rn_ss, rn_eps = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
-    N = skinny_wdims(wp)[0]
-    native().gemm_skinny_qkv_rope(a, wp, rows, qkv, positions, cos_sin,
-                                  k_cache if k_cache is not None else empty,
-                                  v_cache if v_cache is not None else empty,
-                                  slot_mapping if slot_mapping is not None else empty,
-                                  Hq, Hkv, apply_rope, rn_ss, rn_eps, _fused_ws(workspace, rows, N, splits, a.device),
-                                  fused_counters(a.device), splits, skinny_waves())
-    return qkv
-
-
 def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=torch.bfloat16,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sum of ``nslabs`` split-K slabs [nslabs, M, N] -> [M, N] in ``dtype`` (TP>1 tails, before

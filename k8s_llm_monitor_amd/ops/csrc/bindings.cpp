@@ -47,11 +47,6 @@ int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, 
                        int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                        float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
                        const float* row_w, int row_w_ld, int w_rm, hipStream_t s);
-int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* partial, int splits, int* counters, void* Y,
-                             long ldy, int M, int N, int K, int epi, const float* rn_ss, int rn_nc, float rn_eps,
-                             int waves, void* residual, const void* norm_w, float* ss_out, const int* positions,
-                             const float* cos_sin, void* k_cache, void* v_cache, const int* slot_mapping, int Hq,
-                             int Hkv, int block_size, int apply_rope, int w_rm, hipStream_t s);
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
@@ -377,7 +372,7 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  if (algo == 0 || algo == 2) {
+  if (algo == 0 || algo == 2 || (algo >= 40 && algo <= 45)) {
     TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
                 "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
   } else {
@@ -556,97 +551,6 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
   return epi == 0 ? (int64_t)E * S : 1;
 }
 
-// Split-K workspace + tile counters of the fused epilogues: partial fp32 >= S * M * N (S = the
-// launcher's split), counters int32 >= N / 64, zero between launches (the kernel resets them).
-static void fused_ws_check(const torch::Tensor& partial, const torch::Tensor& counters, int64_t S, int M, int N) {
-  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == torch::kFloat32 && partial.is_contiguous() &&
-                  partial.numel() >= S * M * N, "fused skinny: partial must be fp32 with room for S * M * N");
-  dev_i32(counters, "counters");
-  TORCH_CHECK(counters.numel() >= N / 64, "fused skinny: counters must hold N / 64 ints");
-}
-
-// Fused o / down projection + residual add + deferred-RMSNorm producer (epi 4, RESNORM):
-// residual [M, N] += a . W^T (bf16 residual stream); out = packed residual * norm_w
-// [ceil(M/16), N/32, 64, 8]; ss_out [M, N / 64] = per-tile row sums of squares.  Returns S.
-int64_t gemm_skinny_resnorm(torch::Tensor a, torch::Tensor wp, int64_t rows, torch::Tensor residual,
-                            torch::Tensor norm_w, torch::Tensor out, torch::Tensor ss_out, torch::Tensor partial,
-                            torch::Tensor counters, int64_t splits, int64_t waves) {
-  dev_bf16(a, "a"); dev_bf16(wp, "wp"); dev_bf16(residual, "residual"); dev_bf16(norm_w, "norm_w");
-  dev_bf16(out, "out");
-  int N, K;
-  const int w_rm = skinny_weight_dims(wp, 0, N, K, "resnorm");
-  const int M = (int)rows;
-  TORCH_CHECK(N % 64 == 0, "resnorm: N % 64 != 0");
-  TORCH_CHECK(M > 0 && M <= 64, "resnorm: 1..64 rows");
-  TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(0) * 16 >= M && a.size(1) * 32 == K && a.size(2) == 64 &&
-                  a.size(3) == 8, "resnorm: a must be fragment-packed [ceil(M/16), K/32, 64, 8]");
-  TORCH_CHECK(residual.dim() == 2 && residual.is_contiguous() && residual.size(0) == M && residual.size(1) == N,
-              "resnorm: residual must be [M, N]");
-  TORCH_CHECK(norm_w.numel() == N && norm_w.is_contiguous(), "resnorm: norm_w [N]");
-  TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == (M + 15) / 16 && out.size(1) * 32 == N &&
-                  out.size(2) == 64 && out.size(3) == 8, "resnorm: out must be packed [ceil(M/16), N/32, 64, 8]");
-  TORCH_CHECK(ss_out.is_cuda() && ss_out.scalar_type() == torch::kFloat32 && ss_out.is_contiguous() &&
-                  ss_out.dim() == 2 && ss_out.size(0) == M && ss_out.size(1) == N / 64,
-              "resnorm: ss_out must be [M, N / 64] fp32");
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
-  const int S = k8sllm_gemm_skinny_slabs(K, (int)splits);
-  fused_ws_check(partial, counters, S, M, N);
-  check(k8sllm_gemm_skinny_fused(a.data_ptr(), wp.data_ptr(), partial.data_ptr<float>(), (int)splits,
-                                 counters.data_ptr<int>(), out.data_ptr(), 0, M, N, K, 4, nullptr, 0, 0.f, (int)waves,
-                                 residual.data_ptr(), norm_w.data_ptr(), ss_out.data_ptr<float>(), nullptr, nullptr,
-                                 nullptr, nullptr, nullptr, 0, 0, 0, 0, w_rm, cur()),
-        "gemm_skinny_resnorm");
-  return S;
-}
-
-// Fused qkv projection + RoPE + paged KV-cache write (epi 5, head_dim 128): qkv [M, (Hq+2Hkv)*128]
-// receives the rotated rows; with a slot_mapping the k / v heads also land in the cache.  Returns S.
-int64_t gemm_skinny_qkv_rope(torch::Tensor a, torch::Tensor wp, int64_t rows, torch::Tensor qkv,
-                             torch::Tensor positions, torch::Tensor cos_sin, torch::Tensor k_cache,
-                             torch::Tensor v_cache, torch::Tensor slot_mapping, int64_t Hq, int64_t Hkv,
-                             bool apply_rope, c10::optional<torch::Tensor> rn_ss, double rn_eps,
-                             torch::Tensor partial, torch::Tensor counters, int64_t splits, int64_t waves) {
-  dev_bf16(a, "a"); dev_bf16(wp, "wp"); dev_bf16(qkv, "qkv"); dev_i32(positions, "positions");
-  int N, K;
-  const int w_rm = skinny_weight_dims(wp, 0, N, K, "qkv_rope");
-  const int M = (int)rows;
-  TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "qkv_rope: N must be (Hq + 2 Hkv) * 128");
-  TORCH_CHECK(M > 0 && M <= 64, "qkv_rope: 1..64 rows");
-  TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(0) * 16 >= M && a.size(1) * 32 == K && a.size(2) == 64 &&
-                  a.size(3) == 8, "qkv_rope: a must be fragment-packed [ceil(M/16), K/32, 64, 8]");
-  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.stride(0) % 4 == 0 && qkv.size(0) >= M &&
-                  qkv.size(1) == N, "qkv_rope: qkv [M, N]");
-  TORCH_CHECK(positions.numel() >= M, "qkv_rope: positions");
-  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == torch::kFloat32 && cos_sin.is_contiguous() &&
-                  cos_sin.size(1) == 128, "qkv_rope: cos_sin [max_pos, 128] fp32");
-  const bool has_cache = slot_mapping.numel() > 0;
-  int block_size = 0;
-  if (has_cache) {
-    dev_i32(slot_mapping, "slot_mapping"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
-    TORCH_CHECK(slot_mapping.numel() >= M, "qkv_rope: slot_mapping");
-    TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == Hkv && k_cache.size(2) == 16 && k_cache.size(4) == 8,
-                "qkv_rope: k_cache [NB, Hkv, 16, BS, 8]");
-    TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == Hkv && v_cache.size(2) == 128 &&
-                    v_cache.size(3) == k_cache.size(3), "qkv_rope: v_cache [NB, Hkv, 128, BS]");
-    block_size = (int)k_cache.size(3);
-  }
-  const float* rp = nullptr;
-  int rn_nc = 0;
-  rownorm_args(rn_ss, M, K, rp, rn_nc);
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
-  const int S = k8sllm_gemm_skinny_slabs(K, (int)splits);
-  fused_ws_check(partial, counters, S, M, N);
-  check(k8sllm_gemm_skinny_fused(a.data_ptr(), wp.data_ptr(), partial.data_ptr<float>(), (int)splits,
-                                 counters.data_ptr<int>(), qkv.data_ptr(), qkv.stride(0), M, N, K, 5, rp, rn_nc,
-                                 (float)rn_eps, (int)waves, nullptr, nullptr, nullptr, positions.data_ptr<int>(),
-                                 cos_sin.data_ptr<float>(), has_cache ? k_cache.data_ptr() : nullptr,
-                                 has_cache ? v_cache.data_ptr() : nullptr,
-                                 has_cache ? slot_mapping.data_ptr<int>() : nullptr, (int)Hq, (int)Hkv, block_size,
-                                 apply_rope ? 1 : 0, w_rm, cur()),
-        "gemm_skinny_qkv_rope");
-  return S;
-}
-
 // residual += sum of S slabs; out = residual * w (row-major or fragment-packed); ss_part[m][c] =
 // sum of residual^2 over columns [512 c, 512 c + 512) - the deferred-RMSNorm producer.
 void add_norm_partial(torch::Tensor out, torch::Tensor residual, c10::optional<torch::Tensor> partial, int64_t S,
@@ -801,8 +705,6 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
-  m.def("gemm_skinny_resnorm", &gemm_skinny_resnorm);
-  m.def("gemm_skinny_qkv_rope", &gemm_skinny_qkv_rope);
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);

@@ -35,29 +35,7 @@ namespace k8sllm {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2, EPI_SWIGLU_PACKED = 3, EPI_RESNORM = 4, EPI_ROPE = 5 };
-
-// Operands of the fused epilogues, applied by the last-arriving K-slice workgroup of each 64-column
-// tile to the sum of the tile's split-K slabs (skinny_fused_tail), so the launch-boundary reduce
-// kernels disappear from the decode step:
-//   RESNORM - residual[m][n] <- bf16(residual + y); Y (fragment-packed, the next projection's A)
-//             <- bf16(residual * norm_w); ss_out[m][tile] <- sum of residual^2 over the tile's 64
-//             columns: the add_norm_partial pass folded into the o / down projection.
-//   ROPE    - the qkv projection with RoPE (neox pairs p, p + 64 of a 128-dim head: the SwiGLU
-//             tile pairing puts both in one workgroup) and the paged KV-cache write; Y = the
-//             rotated qkv rows (row-major, q read by paged_decode): the rope_cache pass folded in.
-struct SkinnyEpi {
-  bf16_t* residual;
-  const bf16_t* norm_w;
-  float* ss_out;
-  const int* positions;
-  const float* cos_sin;  // [max_pos][128]: cos | sin
-  bf16_t* k_cache;       // [NB][Hkv][16][BS][8]
-  bf16_t* v_cache;       // [NB][Hkv][128][BS]
-  const int* slot_mapping;
-  int* counters;  // [tiles] split-K tickets, zero between launches (the last arriver resets)
-  int Hq, Hkv, block_size, apply_rope;
-};
+enum { EPI_SLAB = 0, EPI_BF16 = 1, EPI_SWIGLU = 2, EPI_SWIGLU_PACKED = 3 };
 
 // Grouped (MoE expert) launches: grid.z = experts; expert x reads weights Wp + x * w_es, activations
 // A + x * a_es (0: every expert reads the same A), writes Y + x * y_es / slabs [x * S + s], and
@@ -75,7 +53,7 @@ struct SkinnyGroup {
 // matching up tiles, so every output column has its gate and up value in the same workgroup.
 template <int EPI, int NT>
 __device__ __forceinline__ int swiglu_tile(int ntile0, int nt) {
-  if constexpr (EPI == 2 || EPI == 3 || EPI == 5) {
+  if constexpr (EPI == 2 || EPI == 3) {
     const int bx = ntile0 / NT;
     return (bx >> 1) * 8 + (bx & 1) * 2 + (nt & 1) + (nt >> 1) * 4;
   } else {
@@ -89,137 +67,6 @@ struct SkinnyBatch {
   u32x4 b[U][NT];
   bf16x8 a[U][MT];
 };
-
-// Split-K tail of the fused epilogues (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item
-// 2, the counter form of the Guideline 16 hand-off): every K-slice workgroup has stored its fp32
-// slab with plain stores; it drains them, releases at agent scope and draws a ticket on the
-// tile's counter; the workgroup drawing S - 1 acquires, resets the counter (graph replays) and
-// reduces the S slabs of its 64-column tile, applying the epilogue.  Correct for any placement of
-// a tile's slices over CUs / XCDs; saves the separate reduce launch (add_norm_partial /
-// rope_cache) and its HBM round trip of the reduced values.
-template <int MT, int EPI, int WAVES>
-__device__ __forceinline__ void skinny_fused_tail(const float* __restrict__ partial, bf16_t* __restrict__ Y, long ldy,
-                                                  int M, int N, const SkinnyEpi& ep) {
-  __shared__ int s_last;
-  const int S = gridDim.y, tile = blockIdx.x;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(ep.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == S - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ep.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const long slab = (long)M * N;
-  // every slab load of a thread is issued before the first use (fixed trip counts, clamped
-  // indices, zero weights for the unused slots - no branch around a load: §5 item 4(c))
-  constexpr int NTH = 64 * WAVES, MAXS = 4;
-  auto slab_sum4 = [&](long off) {
-    float4 a = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int z = 0; z < MAXS; ++z) {
-      const float4 b = *reinterpret_cast<const float4*>(partial + min(z, S - 1) * slab + off);
-      const float f = z < S ? 1.f : 0.f;
-      a.x += b.x * f; a.y += b.y * f; a.z += b.z * f; a.w += b.w * f;
-    }
-    for (int z = MAXS; z < S; ++z) {
-      const float4 b = *reinterpret_cast<const float4*>(partial + z * slab + off);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-    return a;
-  };
-  if constexpr (EPI == EPI_RESNORM) {
-    // 64 columns x MT*16 rows as float4 chunks: 16 lanes per row, so a row's sum of squares is a
-    // 16-lane butterfly (padding rows read row M-1 and contribute 0)
-    constexpr int ITEMS = (MT * 256 + NTH - 1) / NTH;
-    float4 acc[ITEMS];
-    uint2 rv[ITEMS];
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int it = threadIdx.x + k * NTH;
-      const int row = min(it >> 4, M - 1), col = tile * 64 + (it & 15) * 4;
-      acc[k] = slab_sum4((long)row * N + col);
-      rv[k] = *reinterpret_cast<const uint2*>(ep.residual + (long)row * N + col);
-    }
-    const uint2 wv = *reinterpret_cast<const uint2*>(ep.norm_w + tile * 64 + (threadIdx.x & 15) * 4);
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int it = threadIdx.x + k * NTH;
-      if (it >= MT * 256) break;  // wave-uniform (NTH and MT * 256 are multiples of 64)
-      const int row = it >> 4, col = tile * 64 + (it & 15) * 4;
-      const float4 a = acc[k];
-      // the residual stream is bf16 (HF semantics): round, then norm
-      const float x0 = bf2f(f2bf(lo_bf(rv[k].x) + a.x)), x1 = bf2f(f2bf(hi_bf(rv[k].x) + a.y));
-      const float x2 = bf2f(f2bf(lo_bf(rv[k].y) + a.z)), x3 = bf2f(f2bf(hi_bf(rv[k].y) + a.w));
-      float sq = 0.f;
-      if (row < M) {
-        *reinterpret_cast<uint2*>(ep.residual + (long)row * N + col) = uint2{pack2(x0, x1), pack2(x2, x3)};
-        // 4 consecutive columns (col % 4 == 0) are contiguous in the fragment-packed layout
-        *reinterpret_cast<uint2*>(Y + act_index(row, col, -(long)(N >> 5))) =
-            uint2{pack2(x0 * lo_bf(wv.x), x1 * hi_bf(wv.x)), pack2(x2 * lo_bf(wv.y), x3 * hi_bf(wv.y))};
-        sq = x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3;
-      }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sq += __shfl_xor(sq, o, kWave);
-      if (row < M && (it & 15) == 0) ep.ss_out[(long)row * gridDim.x + tile] = sq;
-    }
-  } else {
-    // ROPE: head h = tile / 2 holds dims p = (tile & 1) * 32 + [0, 32) and p + 64 (neox pairs)
-    const int h = tile >> 1, pb = (tile & 1) * 32;
-    const bool rot = ep.apply_rope && h < ep.Hq + ep.Hkv;
-    for (int it = threadIdx.x; it < M * 8; it += NTH) {
-      const int row = it >> 3, p = pb + (it & 7) * 4;
-      const long c1 = (long)row * N + h * 128 + p;
-      const float4 a = slab_sum4(c1), b = slab_sum4(c1 + 64);
-      // rounded to bf16 first, as the unfused GEMM output -> rope_cache path is
-      float x1[4] = {bf2f(f2bf(a.x)), bf2f(f2bf(a.y)), bf2f(f2bf(a.z)), bf2f(f2bf(a.w))};
-      float x2[4] = {bf2f(f2bf(b.x)), bf2f(f2bf(b.y)), bf2f(f2bf(b.z)), bf2f(f2bf(b.w))};
-      if (rot) {
-        const float* cs = ep.cos_sin + (long)ep.positions[row] * 128;
-        const float4 c = *reinterpret_cast<const float4*>(cs + p);
-        const float4 sn = *reinterpret_cast<const float4*>(cs + 64 + p);
-        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float o1 = x1[j] * cc[j] - x2[j] * ss[j], o2 = x2[j] * cc[j] + x1[j] * ss[j];
-          x1[j] = o1;
-          x2[j] = o2;
-        }
-      }
-      const uint2 lo = uint2{pack2(x1[0], x1[1]), pack2(x1[2], x1[3])};
-      const uint2 hi = uint2{pack2(x2[0], x2[1]), pack2(x2[2], x2[3])};
-      bf16_t* yr = Y + (long)row * ldy + h * 128 + p;
-      *reinterpret_cast<uint2*>(yr) = lo;
-      *reinterpret_cast<uint2*>(yr + 64) = hi;
-      const int slot = ep.slot_mapping != nullptr && h >= ep.Hq ? ep.slot_mapping[row] : -1;
-      if (slot >= 0) {
-        const int bs = ep.block_size, blk = slot / bs, off = slot - blk * bs;
-        if (h < ep.Hq + ep.Hkv) {  // key: dims p..p+3 live in 16-dim piece p / 8 at inner offset p % 8
-          bf16_t* kb = ep.k_cache + ((long)blk * ep.Hkv + (h - ep.Hq)) * (128 * bs);
-          *reinterpret_cast<uint2*>(kb + ((p >> 3) * bs + off) * 8 + (p & 7)) = lo;
-          *reinterpret_cast<uint2*>(kb + (((p + 64) >> 3) * bs + off) * 8 + (p & 7)) = hi;
-        } else {  // value: V^T per block, [dim][token]
-          bf16_t* vb = ep.v_cache + ((long)blk * ep.Hkv + (h - ep.Hq - ep.Hkv)) * (128 * bs) + v_perm(off);
-          const uint32_t w[4] = {lo.x, lo.y, hi.x, hi.y};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int d = (j < 2 ? p : p + 64) + 2 * (j & 1);
-            vb[(long)d * bs] = (bf16_t)(w[j] & 0xffff);
-            vb[(long)(d + 1) * bs] = (bf16_t)(w[j] >> 16);
-          }
-        }
-      }
-    }
-  }
-}
 
 // Cross-wave combine of the per-wave accumulators and the epilogue (shared by the packed and the
 // row-major kernels), one m-tile per round.  red: [WAVES][NT][64][4] floats.  s_inv: the A rows'
@@ -275,7 +122,7 @@ __device__ __forceinline__ void skinny_epilogue(const f32x4 (&acc)[MT][NT], floa
             Y[(long)row * ldy + f] = o;
           }
         }
-      } else {  // SLAB / BF16; the fused epilogues write their split-K slab here too (reduced after)
+      } else {  // SLAB / BF16
         const int col = swiglu_tile<EPI, NT>(ntile0, nt) * 16 + (l & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -298,8 +145,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t
                                                           const bf16_t* __restrict__ Wp, float* __restrict__ partial,
                                                           bf16_t* __restrict__ Y, long ldy, int M, int N, int K,
                                                           int kchunk, const float* __restrict__ rn_ss, int rn_nc,
-                                                          float rn_inv_d, float rn_eps, SkinnyGroup grp,
-                                                          SkinnyEpi ep) {
+                                                          float rn_inv_d, float rn_eps, SkinnyGroup grp) {
   // U k-steps per wave group; two groups in flight per wave (register double buffer)
   constexpr int U = MT <= 2 ? 4 : 2;
   __shared__ __attribute__((aligned(16))) float red[WAVES][NT][64][4];  // one m-tile at a time: 16 KiB per 4 waves
@@ -399,7 +245,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t
 
   skinny_epilogue<MT, NT, EPI, WAVES>(acc, &red[0][0][0][0], rn_ss != nullptr ? s_inv : nullptr, partial, Y, ldy, M,
                                       N, ntile0, s, ex, grp);
-  if constexpr (EPI == EPI_RESNORM || EPI == EPI_ROPE) skinny_fused_tail<MT, EPI, WAVES>(partial, Y, ldy, M, N, ep);
 }
 
 // Row-major weights, LDS-DMA staged: the SAME decomposition, epilogues and fragment-packed A as
@@ -513,7 +358,7 @@ template <int MT, int NT, int EPI, int WAVES, bool ILV>
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, long ldw, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
-    float rn_inv_d, float rn_eps, SkinnyGroup grp, SkinnyEpi ep) {
+    float rn_inv_d, float rn_eps, SkinnyGroup grp) {
   using G = SkinnyRmGeom<MT, NT, EPI, WAVES>;
   constexpr int U = G::U;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -647,7 +492,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
   }
   skinny_epilogue_rows<MT, NT, EPI, WAVES>(acc, reinterpret_cast<float*>(smem), rn_ss != nullptr ? s_inv : nullptr,
                                            partial, Y, ldy, M, N, ntile0, s, ex, grp);
-  if constexpr (EPI == EPI_RESNORM || EPI == EPI_ROPE) skinny_fused_tail<MT, EPI, WAVES>(partial, Y, ldy, M, N, ep);
 }
 
 // residual[m] <- bf16(residual[m] + sum_s partial[s][m]); out[m] <- rmsnorm(residual[m]) * w
@@ -854,57 +698,30 @@ static void launch_rm(bool ilv, dim3 grid, dim3 blk, hipStream_t s, Args... args
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                          float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
-                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s);
+                         const float* row_w, int row_w_ld, int w_rm, hipStream_t s);
 
 extern "C" int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M,
                                   int N, int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss,
                                   int rn_nc, int rn_d, float rn_eps, int waves, int experts, long w_es,
                                   long a_es, long y_es, const float* row_w, int row_w_ld, int w_rm, hipStream_t s) {
-  if (epi == EPI_RESNORM || epi == EPI_ROPE) return -6;  // fused epilogues: k8sllm_gemm_skinny_fused
   return skinny_launch(A, lda, Wp, partial, Y, ldy, M, N, K, S, epi, nt_tiles, a_packed, rn_ss, rn_nc, rn_d, rn_eps,
-                       waves, experts, w_es, a_es, y_es, row_w, row_w_ld, SkinnyEpi{}, w_rm, s);
-}
-
-// Fused epilogues (A fragment-packed, 64-column tiles, split-K slabs in `partial` reduced by each
-// tile's last-arriving workgroup; splits <= 0: the automatic split).  epi 4 RESNORM: Y = packed
-// residual * norm_w [ceil(M/16)][N/32][64][8], residual [M][N] updated in place, ss_out
-// [M][N / 64].  epi 5 ROPE (head_dim 128): Y = rotated qkv rows [M][ldy]; k / v heads written to
-// the paged cache at slot_mapping (nullptr: no cache write).  counters: >= N / 64 zeroed ints.
-extern "C" int k8sllm_gemm_skinny_fused(const void* A, const void* Wp, float* partial, int splits, int* counters,
-                                        void* Y, long ldy, int M, int N, int K, int epi, const float* rn_ss,
-                                        int rn_nc, float rn_eps, int waves, void* residual, const void* norm_w,
-                                        float* ss_out, const int* positions, const float* cos_sin, void* k_cache,
-                                        void* v_cache, const int* slot_mapping, int Hq, int Hkv, int block_size,
-                                        int apply_rope, int w_rm, hipStream_t s) {
-  if (partial == nullptr || counters == nullptr || N % 64 != 0) return -7;
-  if (epi == EPI_RESNORM) {
-    if (residual == nullptr || norm_w == nullptr || ss_out == nullptr) return -7;
-  } else if (epi == EPI_ROPE) {
-    if (N != (Hq + 2 * Hkv) * 128 || (slot_mapping != nullptr && block_size <= 0)) return -8;
-  } else {
-    return -6;
-  }
-  if (splits <= 0) splits = k8sllm_gemm_skinny_auto_splits(M, N, K);
-  SkinnyEpi ep{(bf16_t*)residual, (const bf16_t*)norm_w, ss_out, positions, cos_sin, (bf16_t*)k_cache,
-               (bf16_t*)v_cache, slot_mapping, counters, Hq, Hkv, block_size, apply_rope};
-  return skinny_launch(A, 0, Wp, partial, Y, ldy, M, N, K, splits, epi, 4, 1, rn_ss, rn_nc, K, rn_eps, waves, 1,
-                       0, 0, 0, nullptr, 0, ep, w_rm, s);
+                       waves, experts, w_es, a_es, y_es, row_w, row_w_ld, w_rm, s);
 }
 
 static int skinny_launch(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N,
                          int K, int S, int epi, int nt_tiles, int a_packed, const float* rn_ss, int rn_nc, int rn_d,
                          float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
-                         const float* row_w, int row_w_ld, const SkinnyEpi& ep, int w_rm, hipStream_t s) {
+                         const float* row_w, int row_w_ld, int w_rm, hipStream_t s) {
   if (M <= 0) return 0;
   if (experts < 1) return -5;
   const SkinnyGroup grp{w_es, a_es, y_es, row_w, row_w_ld};
   if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
-  if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K) : 1;  // fused: caller
+  if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K) : 1;
   const int kc = skinny_kchunk(K, S, w_rm ? 64 : 32);
   if (w_rm) {
     if (!a_packed || K % 64 != 0 || N % 64 != 0) return -9;  // row-major W: packed A, 64-deep stages, NT = 4
     const int slabs_rm = (K + kc - 1) / kc;
-    if (epi != EPI_SLAB && epi != EPI_RESNORM && epi != EPI_ROPE && slabs_rm != 1) return -3;
+    if (epi != EPI_SLAB && slabs_rm != 1) return -3;
     const float inv_d_rm = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
     const char* ilv_env = getenv("K8SLLM_SKINNY_ILV");
     const bool ilv = ilv_env == nullptr || atoi(ilv_env) != 0;
@@ -927,7 +744,7 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
 #define K8S_RM3(MTV)                                                                                              \
   launch_rm<MTV, 3, EPI_SLAB, 4>(ilv, grid3, blk3, s, (const bf16_t*)A,            \
                      (const bf16_t*)Wp, (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, \
-                     grp, ep)
+                     grp)
       switch (MT) {
         case 1: K8S_RM3(1); break;
         case 2: K8S_RM3(2); break;
@@ -944,10 +761,10 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
 #define K8S_RM(MTV, EPV)                                                                                             \
   if (rw == 4)                                                                                                       \
     launch_rm<MTV, 4, EPV, 4>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
-                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep);     \
+                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp);         \
   else                                                                                                               \
     launch_rm<MTV, 4, EPV, 2>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
-                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp, ep)
+                       (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp)
 #define K8S_RM_M(EPV)                  \
   switch (MT) {                        \
     case 1: K8S_RM(1, EPV); break;     \
@@ -959,29 +776,25 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
       case EPI_SLAB: K8S_RM_M(EPI_SLAB) break;
       case EPI_BF16: K8S_RM_M(EPI_BF16) break;
       case EPI_SWIGLU: K8S_RM_M(EPI_SWIGLU) break;
-      case EPI_SWIGLU_PACKED: K8S_RM_M(EPI_SWIGLU_PACKED) break;
-      case EPI_RESNORM: K8S_RM_M(EPI_RESNORM) break;
-      default: K8S_RM_M(EPI_ROPE) break;
+      default: K8S_RM_M(EPI_SWIGLU_PACKED) break;
     }
 #undef K8S_RM_M
 #undef K8S_RM
     return (int)hipGetLastError();
   }
   const int slabs = (K + kc - 1) / kc;
-  if (epi != EPI_SLAB && epi != EPI_RESNORM && epi != EPI_ROPE && slabs != 1) return -3;
-  if ((epi == EPI_SWIGLU || epi == EPI_SWIGLU_PACKED || epi == EPI_ROPE || epi == EPI_RESNORM) && nt_tiles != 4)
-    return -4;
-  if ((epi == EPI_RESNORM || epi == EPI_ROPE) && !a_packed) return -4;
+  if (epi != EPI_SLAB && slabs != 1) return -3;
+  if ((epi == EPI_SWIGLU || epi == EPI_SWIGLU_PACKED) && nt_tiles != 4) return -4;
   const float inv_d = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
   // 8-wave workgroups: twice the weight lines in flight per CU for the same K slice.  waves <= 0
   // (auto): 8 for the split-K slab projections (o 11.1 vs 11.8 us, down 24.3 vs 25.9 at M = 64),
   // 4 for the single-slice SwiGLU / bf16 epilogues (gate_up 47.5 vs 50.5 us).
-  const int nwaves = waves == 8 || (waves <= 0 && (epi == EPI_SLAB || epi == EPI_RESNORM || epi == EPI_ROPE)) ? 8 : 4;
+  const int nwaves = waves == 8 || (waves <= 0 && epi == EPI_SLAB) ? 8 : 4;
   dim3 grid(N / (16 * nt_tiles), slabs, experts), blk(64 * nwaves);
   const int MT = (M + 15) / 16;
 #define K8S_SK(MTV, NTV, EPV, APKV, WV)                                                                        \
   hipLaunchKernelGGL((gemm_skinny_kernel<MTV, NTV, EPV, APKV, WV>), grid, blk, 0, s, (const bf16_t*)A, lda,   \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps, grp, ep)
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d, rn_eps, grp)
 #define K8S_SK_W(MTV, NTV, EPV, NTLV)                                       \
   if (nwaves == 8) { K8S_SK(MTV, NTV, EPV, NTLV, 8); }                      \
   else { K8S_SK(MTV, NTV, EPV, NTLV, 4); }
@@ -998,11 +811,7 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
   } else {                    \
     K8S_SK_M(NTV, EPV, false) \
   }
-  if (epi == EPI_RESNORM) {
-    K8S_SK_M(4, EPI_RESNORM, true)
-  } else if (epi == EPI_ROPE) {
-    K8S_SK_M(4, EPI_ROPE, true)
-  } else if (epi == EPI_SWIGLU) {
+  if (epi == EPI_SWIGLU) {
     K8S_SK_NTL(4, EPI_SWIGLU)
   } else if (epi == EPI_SWIGLU_PACKED) {
     K8S_SK_NTL(4, EPI_SWIGLU_PACKED)

@@ -325,8 +325,16 @@ __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// CPX / CPW: cache-policy bits of the X / W DMA loads (17 = sc0 sc1: bypass the CU's L1)
-template <int EPI, bool GROUPED, int ABL = 0, int CPX = 0, int CPW = 0>  // ABL (diagnosis): 1 no MFMA, 2 no in-loop DMA
+// CPX / CPW: cache-policy bits of the X / W DMA loads (17 = sc0 sc1: bypass the CU's L1).
+// SCH: 0 = one barrier per k-tile, A_{t+2} DMA'd during (t, 0) and B_{t+2} during (t, 1);
+//      1 = two barriers per k-tile: the mid-(t, 0) barrier (every wave has tile t's k-half-1
+//      fragments in registers) frees BOTH of tile t's half-slots, so B_{t+2} and A_{t+3} are
+//      DMA'd from there on - every piece gets >= ~120 MFMAs to land instead of ~64.
+// SWZ: 1 = XOR-swizzled 16-B chunks (permuted DMA source, conflict-free reads); 0 = linear rows
+// (sequential DMA source, bank-conflicted fragment reads) - diagnosis.
+// WST (SCH = 1): wave w issues its DMA pieces w MFMAs later than wave 0, so the four waves' pieces
+// reach the texture-address unit one MFMA (16 cycles) apart instead of together.
+template <int EPI, bool GROUPED, int ABL = 0, int CPX = 0, int CPW = 0, int SCH = 0, int SWZ = 1, int WST = 0>  // ABL (diagnosis): 1 no MFMA, 2 no in-loop DMA
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     const int rl = (p * 4 + wave) * 8 + (lane >> 3);
-    const int cl = (lane & 7) ^ ((rl >> 1) & 7);
+    const int cl = SWZ ? (lane & 7) ^ ((rl >> 1) & 7) : (lane & 7);
     soff[0][p] = (uint32_t)(((long)min(rl, mrows - 1) * K + cl * 8) * 2);  // rows past the end: clamped, never stored
     soff[1][p] = (uint32_t)(((long)min(rl, nrows - 1) * K + cl * 8) * 2);
   }
@@ -411,7 +419,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   // fragment read: lane row lane & 15 of a 16-row block, 16-B chunk 4 ks + (lane >> 4)
   int rd[2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) rd[ks] = (lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+  for (int ks = 0; ks < 2; ++ks)
+    rd[ks] = (lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ (SWZ ? ((lane >> 1) & 7) : 0)) << 4);
   auto frag = [&](int slot, int ks, int o, int blk) -> bf16x8 {
     const char* b = smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + rd[ks];
     return *reinterpret_cast<const bf16x8*>(b);
@@ -459,6 +468,82 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     }
   };
 
+  if constexpr (SCH == 1) {
+    // piece i (0..15) of iteration t: B_{t+2} pieces 0..7 into A_t's half-slot, then A_{t+3}
+    // pieces 0..7 into B_t's (both free once the mid-(t, 0) barrier has passed)
+    auto piece16 = [&](int i, int t) {
+      if (i < 8)
+        piece(1, i, t + 2, (2 * t) % 5);
+      else
+        piece(0, i - 8, t + 3, (2 * t + 1) % 5);
+    };
+    // PH 0 = (t, 0): fragment reads of k-half 1 of tile t on MFMAs 0-15, lgkmcnt(0) + barrier after
+    // MFMA 19, pieces 0-6 on MFMAs 22, 28, ..., 58.  PH 1 = (t, 1): reads of k-half 0 of tile t+1
+    // on MFMAs 0-15, pieces 7-15 on MFMAs 19, 24, ..., 59.
+    auto sub1 = [&](auto ph, auto wo, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], int sa,
+                    int sb, int nks, int t) {
+      constexpr int PH = decltype(ph)::value, WO = decltype(wo)::value;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = g * 8 + j;
+          if constexpr (ABL == 1) {
+            asm volatile("" ::"v"(cb[j]), "v"(ca[g]));
+          } else {
+            acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
+          }
+          if (n < 8) {
+            nb[n] = frag(sb, nks, 1, n);
+          } else if (n < 16) {
+            na[n - 8] = frag(sa, nks, 0, n - 8);
+          } else if (PH == 0 && n == 19) {
+            lgkm_wait0();
+            __builtin_amdgcn_s_barrier();
+          } else if (PH == 0 && n >= 22 + WO && (n - 22 - WO) % 6 == 0 && (n - 22 - WO) / 6 < 7) {
+            if constexpr (ABL != 2) piece16((n - 22 - WO) / 6, t);
+          } else if (PH == 1 && n >= 19 + WO && (n - 19 - WO) % 5 == 0 && (n - 19 - WO) / 5 < 9) {
+            if constexpr (ABL != 2) piece16(7 + (n - 19 - WO) / 5, t);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    // prologue: A_0 B_0 A_1 B_1 A_2 in flight (all five half-slots); tile 0 landed -> its k-half 0
+    issue_half(0, 0);
+    issue_half(1, 0);
+    issue_half(0, 1);
+    issue_half(1, 1);
+    issue_half(0, 2);
+    vm_wait_n<24>();
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      fa0[g] = frag(0, 0, 0, g);
+      fb0[g] = frag(1, 0, 1, g);
+    }
+    auto kloop = [&](auto wo) {
+      for (int t = 0; t < nk; ++t) {
+        // the previous sub-step's reads landed long ago; saying so keeps hipcc from waiting for the
+        // first read of this one before the first MFMA
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) as a real instruction the waitcnt pass sees
+        sub1(std::integral_constant<int, 0>{}, wo, fa0, fb0, fa1, fb1, (2 * t) % 5, (2 * t + 1) % 5, 1, t);
+        vm_wait_n<15>();  // B_{t+1} landed (younger: A_{t+2}'s 8 pieces and this tile's first 7)
+        __builtin_amdgcn_s_barrier();
+        sub1(std::integral_constant<int, 1>{}, wo, fa1, fb1, fa0, fb0, (2 * t + 2) % 5, (2 * t + 3) % 5, 0, t);
+      }
+    };
+    if constexpr (WST) {
+      if (wave == 0) kloop(std::integral_constant<int, 0>{});
+      else if (wave == 1) kloop(std::integral_constant<int, 1>{});
+      else if (wave == 2) kloop(std::integral_constant<int, 2>{});
+      else kloop(std::integral_constant<int, 3>{});
+    } else {
+      kloop(std::integral_constant<int, 0>{});
+    }
+    vm_wait_n<0>();
+  } else {
   // prologue: A_0 B_0 A_1 B_1 in flight; tile 0 landed -> read its first k-half
   issue_half(0, 0);
   issue_half(1, 0);
@@ -484,6 +569,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     sub(fa1, fb1, fa0, fb0, sa1, sb1, 0, 1, t + 2, (2 * t + 5) % 5);
   }
   vm_wait_n<0>();
+  }
 
   // ---- epilogue: acc[i][j][r] = Y[m][n], m = wm*128 + i*16 + (lane & 15),
   // n = wn*128 + j*16 + 4 (lane >> 4) + r.  Staged through LDS (the ring is idle now): each wave
@@ -762,7 +848,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
   if (M <= 0) return 0;
   const bool grouped = offsets != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
-  if (algo == 0 || algo == 2) {
+  if (algo == 0 || algo == 2 || (algo >= 40 && algo <= 45)) {
     if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
   } else if (N % 256 != 0 || K % 64 != 0 || K < 64) {
     return -1;
@@ -791,6 +877,36 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
     K8_TILE_EPI(gemm_w4p_kernel, 256)
   } else if (algo == 0 || algo == 2) {
     K8_TILE_EPI(gemm_w4_kernel, 256)
+  } else if (algo == 40 || algo == 41) {  // two-barrier schedule of the 4-wave kernel (SCH = 1); 41: no swizzle
+    if (grouped) return -1;
+#define K8_SCH(SW_)                                                                                                  \
+  if (epi == TILE_EPI_SWIGLU)                                                                                        \
+    hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_SWIGLU, false, 0, 0, 0, 1, SW_>), grid, dim3(256), 0, s,              \
+                       (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);        \
+  else                                                                                                               \
+    hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 0, 0, 0, 1, SW_>), grid, dim3(256), 0, s,                \
+                       (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+    if (algo == 40) { K8_SCH(1); } else { K8_SCH(0); }
+#undef K8_SCH
+  } else if (algo >= 42 && algo <= 44) {  // SCH = 1 with sc1 (device-scope: L1 bypass) DMA loads
+    if (grouped) return -1;
+#define K8_SC1(CX, CW)                                                                                               \
+  if (epi == TILE_EPI_SWIGLU)                                                                                        \
+    hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_SWIGLU, false, 0, CX, CW, 1, 1>), grid, dim3(256), 0, s,             \
+                       (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);        \
+  else                                                                                                               \
+    hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 0, CX, CW, 1, 1>), grid, dim3(256), 0, s,               \
+                       (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+    if (algo == 42) { K8_SC1(16, 16); } else if (algo == 43) { K8_SC1(16, 0); } else { K8_SC1(0, 16); }
+#undef K8_SC1
+  } else if (algo == 45) {  // SCH = 1 with per-wave staggered DMA issue (WST)
+    if (grouped) return -1;
+    if (epi == TILE_EPI_SWIGLU)
+      hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_SWIGLU, false, 0, 0, 0, 1, 1, 1>), grid, dim3(256), 0, s,
+                         (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);
+    else
+      hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 0, 0, 0, 1, 1, 1>), grid, dim3(256), 0, s,
+                         (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);
   } else if (algo >= 20 && algo <= 23) {  // cache-policy variants of the 4-wave kernel (dense, bf16 out)
     if (grouped || epi != TILE_EPI_BF16) return -1;
 #define K8_CP(CX, CW)                                                                                             \

@@ -78,35 +78,6 @@ def test_rm_deferred_rmsnorm(M):
     _close(y.cpu(), y_ref, atol=3e-2, rtol=3e-2, what="rm deferred norm")
 
 
-@pytest.mark.parametrize("M,splits", [(1, 1), (64, 4)])
-def test_rm_resnorm_and_qkv_rope(M, splits):
-    K, d = 1024, 4096
-    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = _w(d, K)
-    r = torch.randn(M, d, device=DEV, dtype=torch.bfloat16)
-    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
-    r_ref = (r.cpu().float() + F_.linear(a.cpu().float(), w.cpu().float())).to(torch.bfloat16)
-    xw, ss = ops.skinny_resnorm(ops.pack_activation(a), w, r, nw, rows=M, splits=splits)
-    assert int(ops.fused_counters(DEV).abs().sum()) == 0
-    _close(r.cpu(), r_ref, atol=3e-2, rtol=1e-2, what="rm resnorm residual")
-    _close(ss.sum(1).cpu(), (r_ref.float() ** 2).sum(1), atol=1.0, rtol=2e-3, what="rm resnorm ss")
-    hq, hkv, D, bs = 8, 2, 128, 16
-    ncol = (hq + 2 * hkv) * D
-    wq = _w(ncol, K)
-    pos = torch.randint(0, 500, (M,), dtype=torch.int32, device=DEV)
-    cs = ref.rope_cos_sin(2048, D, 500000.0, None, device=DEV)
-    nb = (M + bs - 1) // bs + 2
-    slots = torch.randperm(nb * bs, device=DEV)[:M].to(torch.int32)
-    kc = torch.zeros(nb, hkv, D // 8, bs, 8, device=DEV, dtype=torch.bfloat16)
-    vc = torch.zeros(nb, hkv, D, bs, device=DEV, dtype=torch.bfloat16)
-    qkv = torch.empty(M, ncol, device=DEV, dtype=torch.bfloat16)
-    ops.skinny_qkv_rope(ops.pack_activation(a), wq, qkv, pos, cs, kc, vc, slots, hq, hkv, rows=M, splits=splits)
-    qkv_r = F_.linear(a.cpu().float(), wq.cpu().float()).to(torch.bfloat16)
-    ref.rope_and_cache(qkv_r, pos.cpu(), cs.cpu(), None, None, None, hq, hkv, D)
-    qk = (hq + hkv) * D
-    _close(qkv[:, :qk].cpu(), qkv_r[:, :qk], atol=6e-2, rtol=3e-2, what="rm qkv rope")
-
-
 @pytest.mark.parametrize("M,E", [(1, 4), (64, 2)])
 def test_rm_grouped_moe(M, E):
     K, F, d = 512, 448, 256

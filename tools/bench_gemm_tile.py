@@ -44,6 +44,12 @@ def main() -> None:
         cases.append((name, 2 * T * N * K, {
             "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
             "w4p": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=2)),
+            "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=40)),
+            "w4s_lin": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=41)),
+            "w4s_sc1": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=42)),
+            "w4s_sc1x": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=43)),
+            "w4s_sc1w": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=44)),
+            "w4s_wst": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=45)),
             "w4_cpx": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=20)),
             "w4_cpw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=21)),
             "w4_cpxw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=22)),
@@ -59,6 +65,10 @@ def main() -> None:
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
         "w4p": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2)),
+        "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=40)),
+        "w4s_lin": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=41)),
+        "w4s_sc1": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=42)),
+        "w4s_wst": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=45)),
         "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
         "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
         "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
