@@ -334,7 +334,12 @@ __device__ __forceinline__ void vm_wait_n() {
 // (sequential DMA source, bank-conflicted fragment reads) - diagnosis.
 // WST (SCH = 1): wave w issues its DMA pieces w MFMAs later than wave 0, so the four waves' pieces
 // reach the texture-address unit one MFMA (16 cycles) apart instead of together.
-template <int EPI, bool GROUPED, int ABL = 0, int CPX = 0, int CPW = 0, int SCH = 0, int SWZ = 1, int WST = 0>  // ABL (diagnosis): 1 no MFMA, 2 no in-loop DMA
+// STG (SCH = 0): 1 = register-staged refill instead of LDS-DMA: each piece is a buffer_load_dwordx4
+// into VGPRs issued one k-tile ahead and a ds_write_b128 of the previous one (an LDS-DMA piece
+// holds its wave's issue for ~60-185 cycles among MFMAs; a VGPR load and an LDS store ride the
+// MFMA shadow like the fragment reads).
+template <int EPI, bool GROUPED, int ABL = 0, int CPX = 0, int CPW = 0, int SCH = 0, int SWZ = 1, int WST = 0,
+          int STG = 0, int LGK = 0>  // ABL (diagnosis): 1 no MFMA, 2 no in-loop DMA
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
@@ -415,6 +420,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
 #pragma unroll
     for (int p = 0; p < 8; ++p) piece(o, p, kt, (2 * kt + o) % 5);
   };
+  // register staging (STG): piece p of half-tile (o, kt) into st[o][p]; written lane-linear into
+  // the same LDS bytes the DMA piece would fill
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  u32x4s st[2][8];
+  auto st_load = [&](int o, int p, int kt) {
+    if (o)
+      st[o][p] = __builtin_amdgcn_raw_buffer_load_b128(wr, soff[1][p], min(kt, nk - 1) * 128, CPW);
+    else
+      st[o][p] = __builtin_amdgcn_raw_buffer_load_b128(xr, soff[0][p], min(kt, nk - 1) * 128, CPX);
+  };
+  auto st_write = [&](int o, int p, int slot) {
+    *reinterpret_cast<u32x4s*>(smem + slot * HS + (p * 4 + wave) * 1024 + lane * 16) = st[o][p];
+  };
 
   // fragment read: lane row lane & 15 of a 16-row block, 16-B chunk 4 ks + (lane >> 4)
   int rd[2];
@@ -457,7 +475,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
         }
         const int q = n - (n > 4) - (n > 12);  // read index: skips the DMA slots 4 and 12
         if (j == 4) {
-          if constexpr (ABL != 2) piece(o, g, kt, ds);
+          if constexpr (STG) {
+            st_write(o, g, ds);   // half-tile (o, kt) piece g, loaded one k-tile ago
+            st_load(o, g, kt + 1);
+          } else if constexpr (ABL != 2) {
+            piece(o, g, kt, ds);
+          }
         } else if (q < 8) {
           nb[q] = frag(sb, nks, 1, q);
         } else if (q < 16) {
@@ -549,7 +572,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   issue_half(1, 0);
   issue_half(0, 1);
   issue_half(1, 1);
-  vm_wait_n<16>();
+  if constexpr (STG) {
+    // A_2, B_2 into the staging registers; they are written to LDS during (0, 0) / (0, 1)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) st_load(0, p, 2);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) st_load(1, p, 2);
+    vm_wait_n<32>();  // tile 0 landed (tile 1 and the 16 staged loads younger)
+  } else {
+    vm_wait_n<16>();
+  }
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
@@ -560,10 +592,17 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   for (int t = 0; t < nk; ++t) {
     const int sa = (2 * t) % 5, sb = (2 * t + 1) % 5;            // tile t's half-slots
     const int sa1 = (2 * t + 2) % 5, sb1 = (2 * t + 3) % 5;      // tile t+1's
+    // the previous sub-step's fragment reads landed long ago; an explicit lgkmcnt(0) here keeps
+    // hipcc from merging that wait with the first read of this sub-step (a full LDS latency before
+    // the first MFMA of every k-tile)
+    if constexpr (LGK) __builtin_amdgcn_s_waitcnt(0xc07f);
     // (t, 0): MFMAs on k-half 0; read k-half 1 of tile t; DMA A_{t+2}
     sub(fa0, fb0, fa1, fb1, sa, sb, 1, 0, t + 2, (2 * t + 4) % 5);
     lgkm_wait0();
-    vm_wait_n<8>();  // B_{t+1} landed (only A_{t+2} younger)
+    if constexpr (STG)
+      vm_wait_n<24>();  // t = 0: B_1 (DMA) landed - younger: B_2, A_2... staged loads (<= 24); later a no-op
+    else
+      vm_wait_n<8>();  // B_{t+1} landed (only A_{t+2} younger)
     __builtin_amdgcn_s_barrier();
     // (t, 1): MFMAs on k-half 1; read k-half 0 of tile t+1 (garbage past the end, never used); DMA B_{t+2}
     sub(fa1, fb1, fa0, fb0, sa1, sb1, 0, 1, t + 2, (2 * t + 5) % 5);
@@ -848,7 +887,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
   if (M <= 0) return 0;
   const bool grouped = offsets != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
-  if (algo == 0 || algo == 2 || (algo >= 40 && algo <= 45)) {
+  if ((algo >= 0 && algo <= 5 && algo != 1) || (algo >= 40 && algo <= 45)) {
     if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
   } else if (N % 256 != 0 || K % 64 != 0 || K < 64) {
     return -1;
@@ -877,6 +916,32 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
     K8_TILE_EPI(gemm_w4p_kernel, 256)
   } else if (algo == 0 || algo == 2) {
     K8_TILE_EPI(gemm_w4_kernel, 256)
+  } else if (algo == 4 || algo == 5) {  // explicit loop-top lgkmcnt(0) (LGK = 1); 5: + no in-loop DMA (diagnosis)
+    if (algo == 5) {
+      if (grouped || epi != TILE_EPI_BF16) return -1;
+      hipLaunchKernelGGL((gemm_w4_kernel<TILE_EPI_BF16, false, 2, 0, 0, 0, 1, 0, 0, 1>), grid, dim3(256), 0, s,
+                         (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt);
+    } else {
+#define K8_LGK(EPI_, G_)                                                                                             \
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, 0, 0, 0, 0, 1, 0, 0, 1>), grid, dim3(256), 0, s, (const bf16_t*)X,    \
+                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+      if (grouped) {
+        if (epi == TILE_EPI_SWIGLU) K8_LGK(TILE_EPI_SWIGLU, true); else K8_LGK(TILE_EPI_BF16, true);
+      } else {
+        if (epi == TILE_EPI_SWIGLU) K8_LGK(TILE_EPI_SWIGLU, false); else K8_LGK(TILE_EPI_BF16, false);
+      }
+#undef K8_LGK
+    }
+  } else if (algo == 3) {  // register-staged refill (STG = 1)
+#define K8_STG(EPI_, G_)                                                                                             \
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, 0, 0, 0, 0, 1, 0, 1>), grid, dim3(256), 0, s, (const bf16_t*)X,       \
+                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+    if (grouped) {
+      if (epi == TILE_EPI_SWIGLU) K8_STG(TILE_EPI_SWIGLU, true); else K8_STG(TILE_EPI_BF16, true);
+    } else {
+      if (epi == TILE_EPI_SWIGLU) K8_STG(TILE_EPI_SWIGLU, false); else K8_STG(TILE_EPI_BF16, false);
+    }
+#undef K8_STG
   } else if (algo == 40 || algo == 41) {  // two-barrier schedule of the 4-wave kernel (SCH = 1); 41: no swizzle
     if (grouped) return -1;
 #define K8_SCH(SW_)                                                                                                  \

@@ -44,6 +44,9 @@ def main() -> None:
         cases.append((name, 2 * T * N * K, {
             "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
             "w4p": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=2)),
+            "w4r": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=3)),
+            "w4l": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=4)),
+            "w4l_nodma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=5)),
             "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=40)),
             "w4s_lin": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=41)),
             "w4s_sc1": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=42)),
@@ -65,6 +68,8 @@ def main() -> None:
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
         "w4p": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2)),
+        "w4r": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=3)),
+        "w4l": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=4)),
         "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=40)),
         "w4s_lin": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=41)),
         "w4s_sc1": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=42)),
@@ -102,6 +107,7 @@ def main() -> None:
     cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=0)),
         "w4p": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=2)),
+        "w4r": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=3)),
         "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
         "hipblaslt_loop": loop13,
@@ -109,6 +115,7 @@ def main() -> None:
     cases.append(("moe_w2", 2 * rows * d * F, {
         "w4": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=0)),
         "w4p": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=2)),
+        "w4r": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=3)),
         "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
         "hipblaslt_loop": loop2,

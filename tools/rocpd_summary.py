@@ -25,12 +25,36 @@ def short(name: str, n: int = 90) -> str:
     return name if len(name) <= n else name[: n - 3] + "..."
 
 
+def decode_steps(db: str) -> None:
+    """Median kernel-busy time of pure decode steps (the sampler's final kernel ends every step)."""
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    marks = [i for i, r in enumerate(rows) if "sample_final" in r[0]]
+    spans = []
+    for a, b in zip(marks, marks[1:]):
+        ks = rows[a + 1:b + 1]
+        if any("paged_decode" in r[0] for r in ks) and not any("flash_prefill" in r[0] for r in ks):
+            spans.append((sum(r[2] - r[1] for r in ks), ks[-1][2] - rows[a][2]))
+    spans.sort()
+    if not spans:
+        print("no pure decode steps found")
+        return
+    n = len(spans)
+    med = spans[n // 2]
+    print(f"decode steps {n}: median kernel-busy {med[0] / 1e6:.3f} ms, wall {med[1] / 1e6:.3f} ms (between step ends)")
+    print(f"mean busy {sum(s[0] for s in spans) / n / 1e6:.3f} ms, mean wall {sum(s[1] for s in spans) / n / 1e6:.3f} ms")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--title", default="")
+    ap.add_argument("--decode-steps", action="store_true", help="print decode-step kernel-busy statistics only")
     a = ap.parse_args()
+    if a.decode_steps:
+        decode_steps(a.db)
+        return
     rows, total = summarise(a.db, a.top)
     if a.title:
         print(f"# {a.title}\n")
