@@ -693,7 +693,7 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
     if N % 256 == 0 and K % 64 == 0 and N * K * 2 < (1 << 31):
         # the 256 x 256 tile kernel (gemm_tile.hip): 1.12-1.15 PF/s on Mixtral's expert shapes
         # against 0.86-0.94 for the 128-tile kernel below (profiles/r02/gemm_tile_vs_hipblaslt.jsonl)
-        native().gemm_tile(out, x.contiguous(), w, offsets.contiguous(), swiglu)
+        native().gemm_tile(out, x.contiguous(), w, offsets.contiguous(), swiglu, TILE_ALGO)
     else:
         native().moe_grouped_gemm(out, x.contiguous(), w, offsets.contiguous(), swiglu)
     return out
@@ -731,11 +731,14 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
 
 
 # Prefill projections (qkv / o / gate_up + SwiGLU / down) on the hand-written 4-wave MFMA GEMM
-# (csrc/gemm_tile.hip gemm_w4_kernel) or hipBLASLt (torch F.linear).  K8SLLM_PREFILL_GEMM=tile|blas
-# forces one; the default routes the shapes where the tile kernel measured at least at parity
-# (profiles/r03/README.md).
+# (csrc/gemm_tile.hip, two-barrier schedule) or hipBLASLt (torch F.linear).  K8SLLM_PREFILL_GEMM=
+# tile|blas forces one; the default ("auto") takes the tile kernel where it measured at least at
+# parity with hipBLASLt on the same box: the fused gate_up + SwiGLU (1.46 vs 1.43 PF/s including
+# hipBLASLt's separate silu_mul pass); qkv / o / down stay on hipBLASLt, 6-12 % faster there
+# (profiles/r03/gemm_schedules.jsonl).
 PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "auto")
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
+TILE_ALGO = 1  # refill schedule: two barriers per k-tile
 
 
 def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
@@ -750,7 +753,7 @@ def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
                and (not swiglu or N % 256 == 0) and N * K * 2 < (1 << 31))
     use_tile = tile_ok and (mode == "tile" or (mode == "auto" and swiglu))
     if use_tile:
-        return gemm_tile(x, w, swiglu=swiglu, out=out, algo=0)
+        return gemm_tile(x, w, swiglu=swiglu, out=out, algo=TILE_ALGO)
     y = torch.nn.functional.linear(x, w)
     if swiglu:
         return silu_mul(y, out=out, interleaved=True)

@@ -372,12 +372,9 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  if ((algo >= 0 && algo <= 5 && algo != 1) || (algo >= 40 && algo <= 45)) {
-    TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
-                "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
-  } else {
-    TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "gemm_tile: N % 256 == 0, K % 64 == 0");
-  }
+  TORCH_CHECK(algo == 0 || algo == 1, "gemm_tile: algo 0 (one barrier per k-tile) or 1 (two)");
+  TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
+              "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
   TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (swiglu ? N / 2 : N), "gemm_tile: y shape");
   const int* op = nullptr;
   if (grouped) {

@@ -196,7 +196,7 @@ def test_service_coalesces_a_burst_into_one_prefill():
     from k8s_llm_monitor_amd.engine import EngineService
 
     eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=16, max_model_len=256, num_blocks=128,
-                                 use_graphs=False, admit_gap_ms=5.0, admit_window_ms=200.0), device="cpu")
+                                 use_graphs=False, admit_gap_ms=50.0, admit_window_ms=400.0), device="cpu")
     eng.trace = []
     svc = EngineService(eng)
     futs = []

@@ -1,4 +1,4 @@
-"""Prefill GEMMs on MI355X: the 256 x 256 MFMA tile kernel (ops/csrc/gemm_tile.hip) against
+"""Prefill GEMMs on MI355X: the 256 x 256 MFMA tile kernel (w4: one barrier per k-tile, w4s: two) (ops/csrc/gemm_tile.hip) against
 hipBLASLt (torch F.linear), at the Llama-3-8B prefill-chunk shapes (16384 tokens) and the
 Mixtral-8x7B grouped expert shapes (top-2 of 8).  Random operands, interleaved rounds, hipGraph
 replay of back-to-back calls; the SwiGLU rows compare the fused epilogue with F.linear + silu_mul.
@@ -43,23 +43,7 @@ def main() -> None:
         y = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
         cases.append((name, 2 * T * N * K, {
             "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
-            "w4p": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=2)),
-            "w4r": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=3)),
-            "w4l": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=4)),
-            "w4l_nodma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=5)),
-            "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=40)),
-            "w4s_lin": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=41)),
-            "w4s_sc1": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=42)),
-            "w4s_sc1x": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=43)),
-            "w4s_sc1w": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=44)),
-            "w4s_wst": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=45)),
-            "w4_cpx": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=20)),
-            "w4_cpw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=21)),
-            "w4_cpxw": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=22)),
-            "w4_nt": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=23)),
-            "w4_nomfma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=10)),
-            "w4_nodma": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=11)),
-            "tile": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
+            "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
             "hipblaslt": (lambda i, xin=xin, w=w, y=y: torch.matmul(xin, w.t(), out=y)),
         }))
     w13 = ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02).contiguous()
@@ -67,14 +51,7 @@ def main() -> None:
     act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
-        "w4p": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2)),
-        "w4r": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=3)),
-        "w4l": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=4)),
-        "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=40)),
-        "w4s_lin": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=41)),
-        "w4s_sc1": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=42)),
-        "w4s_wst": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=45)),
-        "tile": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
+        "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
         "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
         "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
     }))
@@ -106,17 +83,13 @@ def main() -> None:
 
     cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=0)),
-        "w4p": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=2)),
-        "w4r": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=3)),
-        "tile": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
+        "w4s": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
         "hipblaslt_loop": loop13,
     }))
     cases.append(("moe_w2", 2 * rows * d * F, {
         "w4": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=0)),
-        "w4p": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=2)),
-        "w4r": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=3)),
-        "tile": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
+        "w4s": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
         "hipblaslt_loop": loop2,
     }))

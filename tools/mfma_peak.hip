@@ -30,7 +30,10 @@ __global__ __launch_bounds__(256, 1) void mfma32_loop(float* out, int iters) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // issue order as written (no accumulator rotation)
+      }
   }
   long t1 = clock64();
   float s = 0.f;
@@ -59,7 +62,10 @@ __global__ __launch_bounds__(256, 1) void mfma_loop(float* out, int iters) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
   }
   long t1 = clock64();
   float s = 0.f;
