@@ -536,8 +536,8 @@ class CausalLM:
         whole 128-B lines by LDS-DMA - within 1-3 % of the old fragment-packed duplicate at every
         decode batch (tools/bench_skinny_rm.py, profiles/r02/skinny_rm_vs_packed.jsonl), so
         Llama-3-8B holds 16 GB of weights, not 32, and 70B fits one GPU on the skinny path.
-        ``K8SLLM_SKINNY_LAYOUT=packed`` (or a shape the row-major kernel does not take: N or K not
-        a multiple of 64) keeps fragment-packed copies instead.
+        A shape the row-major kernel does not take (N or K not a multiple of 64) keeps
+        fragment-packed copies instead.
 
         w13 is stored gate/up-interleaved per 128 rows ([64 gate | 64 up], the SwiGLU epilogue's
         pairing): called on canonical [gate; up] tensors (after _build or load_checkpoint), it
@@ -576,7 +576,7 @@ class CausalLM:
         if d % 64 or nq % 64 or (self.hq * self.D) % 32:
             self._attn_rope = False
             return
-        rowmajor = os.environ.get("K8SLLM_SKINNY_LAYOUT", "rowmajor") != "packed" and (self.hq * self.D) % 64 == 0
+        rowmajor = (self.hq * self.D) % 64 == 0
         self.skinny_layout = "rowmajor" if rowmajor else "packed"
         keep = (lambda w: w) if rowmajor else ops.pack_skinny
         for L in self.layers:

@@ -492,9 +492,8 @@ extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv,
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
-  const bool v1_only = getenv("K8SLLM_PREFILL_V1") != nullptr && atoi(getenv("K8SLLM_PREFILL_V1")) == 1;
   // bt_stride = the block-table width = most blocks a sequence can hold: <= 2048 - 3 fit the LDS copy
-  if (ctx_start != nullptr && !v1_only && (G == 2 || G == 4 || G == 8) && bt_stride <= 2045) {
+  if (ctx_start != nullptr && (G == 2 || G == 4 || G == 8) && bt_stride <= 2045) {
     // v2: q-blocks of 128 rows split into 128 / QR workgroups (QR = 256 / G rows each)
     const int z = 128 / (256 / G);
 #define K8S_FP2(GG)                                                                                                 \

@@ -354,7 +354,7 @@ struct SkinnyRmGeom {
   static constexpr int NLOAD = NT * 2 + MT * U;      // DMA instructions per stage
 };
 
-template <int MT, int NT, int EPI, int WAVES, bool ILV>
+template <int MT, int NT, int EPI, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, long ldw, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
@@ -459,7 +459,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers: the slot is free
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(refill)::value) issue(slot, wave + (i + 2) * WAVES);
-    if constexpr (!ILV) __builtin_amdgcn_sched_barrier(0);  // the pre-interleave order: DMAs, then MFMAs
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -467,7 +466,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][mt], bw[u][nt], acc[mt][nt], 0, 0, 0);
-    if constexpr (ILV && decltype(refill)::value) {
+    if constexpr (decltype(refill)::value) {
       constexpr int PER = (U * MT * NT + G::NLOAD - 1) / G::NLOAD;
 #pragma unroll
       for (int k = 0; k < G::NLOAD; ++k) {
@@ -634,8 +633,7 @@ extern "C" int k8sllm_add_norm_partial(void* out, long out_stride, void* residua
 #define K8S_ANP(SCV)                                                                                         \
   hipLaunchKernelGGL((add_norm_partial_kernel<SCV>), grid, blk, 0, s, (bf16_t*)out, out_stride, (bf16_t*)residual, \
                      partial, S, M, (const bf16_t*)w, d, ss_part)
-  static const bool dyn = getenv("K8SLLM_ANP_STATIC") != nullptr && atoi(getenv("K8SLLM_ANP_STATIC")) == 0;
-  switch (dyn ? -1 : S) {
+  switch (S) {
     case 1: K8S_ANP(1); break;
     case 2: K8S_ANP(2); break;
     case 3: K8S_ANP(3); break;
@@ -684,13 +682,9 @@ extern "C" int k8sllm_gemm_skinny_auto_splits(int M, int N, int K) {
   return sp;
 }
 
-// K8SLLM_SKINNY_ILV=0 launches the row-major kernel without the DMA / MFMA interleave (A/B knob)
 template <int MT, int NT, int EPI, int WAVES, typename... Args>
-static void launch_rm(bool ilv, dim3 grid, dim3 blk, hipStream_t s, Args... args) {
-  if (ilv)
-    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MT, NT, EPI, WAVES, true>), grid, blk, 0, s, args...);
-  else
-    hipLaunchKernelGGL((gemm_skinny_rm_kernel<MT, NT, EPI, WAVES, false>), grid, blk, 0, s, args...);
+static void launch_rm(dim3 grid, dim3 blk, hipStream_t s, Args... args) {
+  hipLaunchKernelGGL((gemm_skinny_rm_kernel<MT, NT, EPI, WAVES>), grid, blk, 0, s, args...);
 }
 
 // rn_ss (optional): per-row partial sums of squares [M][rn_nc] of the un-normalised A rows
@@ -723,8 +717,6 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     const int slabs_rm = (K + kc - 1) / kc;
     if (epi != EPI_SLAB && slabs_rm != 1) return -3;
     const float inv_d_rm = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
-    const char* ilv_env = getenv("K8SLLM_SKINNY_ILV");
-    const bool ilv = ilv_env == nullptr || atoi(ilv_env) != 0;
     const int MT = (M + 15) / 16;
     // 4 waves per workgroup unless the grid then needs more than one round of workgroups: each
     // wave's ring holds two 16-KiB stages at M = 64, so LDS caps residency (4 waves: 1 workgroup
@@ -742,7 +734,7 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     if (nt3) {
       dim3 grid3(N / 48, slabs_rm, experts), blk3(256);
 #define K8S_RM3(MTV)                                                                                              \
-  launch_rm<MTV, 3, EPI_SLAB, 4>(ilv, grid3, blk3, s, (const bf16_t*)A,            \
+  launch_rm<MTV, 3, EPI_SLAB, 4>(grid3, blk3, s, (const bf16_t*)A,            \
                      (const bf16_t*)Wp, (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, \
                      grp)
       switch (MT) {
@@ -760,10 +752,10 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
     dim3 grid(N / 64, slabs_rm, experts), blk(64 * rw);
 #define K8S_RM(MTV, EPV)                                                                                             \
   if (rw == 4)                                                                                                       \
-    launch_rm<MTV, 4, EPV, 4>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+    launch_rm<MTV, 4, EPV, 4>(grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
                        (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp);         \
   else                                                                                                               \
-    launch_rm<MTV, 4, EPV, 2>(ilv, grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
+    launch_rm<MTV, 4, EPV, 2>(grid, blk, s, (const bf16_t*)A, (const bf16_t*)Wp, \
                        (long)K, partial, (bf16_t*)Y, ldy, M, N, K, kc, rn_ss, rn_nc, inv_d_rm, rn_eps, grp)
 #define K8S_RM_M(EPV)                  \
   switch (MT) {                        \

@@ -23,7 +23,6 @@ def main() -> None:
     ap.add_argument("--seqs", type=int, default=10)
     ap.add_argument("--len", type=int, default=1609)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", choices=["all", "v1", "v2"], default="all", help="paged kernel(s) to time (PMC runs)")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     T = a.seqs * a.len
@@ -46,7 +45,7 @@ def main() -> None:
         us = e0.elapsed_time(e1) / a.iters * 1e3
         print(json.dumps({"seqs": a.seqs, "len": a.len, "kernel": "plain", "us": round(us, 1),
                           "PFps": round(flops / us / 1e9, 3)}))
-    # paged (the engine's path): keys / values from a block-permuted cache, v1 vs v2 interleaved
+    # paged (the engine's path): keys / values from a block-permuted cache, the v2 kernel
     bs = 16
     nb = a.seqs * ((a.len + bs - 1) // bs)
     kc = torch.zeros(nb + 4, Hkv, D // 8, bs, 8, device="cuda", dtype=torch.bfloat16)
@@ -61,10 +60,7 @@ def main() -> None:
     cst = torch.zeros(a.seqs, dtype=torch.int32, device="cuda")
     res: dict = {}
     for _ in range(3):
-        for tag, v1 in (("paged_v1", "1"), ("paged_v2", "0")):
-            if a.only != "all" and not tag.endswith(a.only):
-                continue
-            os.environ["K8SLLM_PREFILL_V1"] = v1
+        for tag in ("paged_v2",):
             for _ in range(3):
                 ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out, paged=(cst, kc, vc, bt))
             torch.cuda.synchronize()
@@ -74,7 +70,6 @@ def main() -> None:
             e1.record()
             torch.cuda.synchronize()
             res.setdefault(tag, []).append(e0.elapsed_time(e1) / a.iters * 1e3)
-    os.environ.pop("K8SLLM_PREFILL_V1", None)
     for tag, ts in res.items():
         us = min(ts)
         print(json.dumps({"seqs": a.seqs, "len": a.len, "kernel": tag, "us": round(us, 1),
