@@ -517,6 +517,15 @@ class EngineService:
         if not self.healthy:
             fut.set_exception(EngineUnavailable(f"engine unhealthy: {self._error!r}"))
             return fut
+        if isinstance(prompt, str):
+            # tokenize on the caller's thread: the native BPE releases the GIL, so a burst's HTTP
+            # handler threads encode in parallel instead of the engine thread encoding the whole
+            # burst serially while the GPU waits for the first prefill
+            try:
+                prompt = self.engine.tokenizer.encode(prompt)
+            except Exception as e:  # noqa: BLE001 - reject this request only
+                fut.set_exception(e)
+                return fut
         if self.pending() >= self.max_queue:
             self.rejected += 1
             fut.set_exception(EngineOverloaded(f"request queue full ({self.max_queue} waiting)"))
