@@ -211,12 +211,12 @@ def run_rank(a) -> None:
     params = SamplingParams(max_tokens=a.max_new_tokens, temperature=0.1, ignore_eos=True)
     rng = random.Random(1234 + ps.dp_rank)
 
-    def post(items, offsets=None):
+    def post(w, items, offsets=None):
         from k8s_llm_monitor_amd.monitor.app import post_queries
 
         kw = dict(offsets_s=offsets, allow_errors=a.production or a.mode == "poisson")
         if loadgen:
-            return loadgen.post_queries(port, items, a.max_new_tokens, slim=True, **kw)
+            return loadgen.post_queries(port, None, a.max_new_tokens, slim=True, staged=w, **kw)
         return post_queries(port, items, a.max_new_tokens, **kw)
 
     # the clients' synthetic payloads are generated up front: building them is load-generator
@@ -226,6 +226,9 @@ def run_rank(a) -> None:
     payload = {}
     if a.path == "http":
         payload = {w: [synthetic_context(sd)[::-1] for sd in seeds_of[w]] for w in seeds_of}  # (question, context)
+        if loadgen:  # the clients hold their payloads before the clock starts: per wave only a key crosses the pipe
+            for w, items in payload.items():
+                loadgen.stage(w, items)
     elif a.path == "engine":
         payload = {w: [synthetic_cluster_prompt(sd) for sd in seeds_of[w]] for w in seeds_of}
 
@@ -238,8 +241,8 @@ def run_rank(a) -> None:
                 for _ in items:
                     t += rng.expovariate(a.rate)
                     offs.append(t)
-                return post(items, offs)
-            return post(items)
+                return post(w, items, offs)
+            return post(w, items)
         if a.path == "podcomm":
             from k8s_llm_monitor_amd.monitor.app import bench_pod_pairs, post_pod_communication
 
@@ -402,6 +405,14 @@ def _print_trace(trace: list, t0: float) -> None:
         if prev and nxt:
             print(f"[trace] boundary: last decode -> first add {(w[0][0] - prev[-1]) * 1e3:.1f} ms, "
                   f"first add -> first prefill {(nxt[0] - w[0][0]) * 1e3:.1f} ms", file=sys.stderr)
+            # where the boundary goes: answers resolved (detokenized) on the engine thread ->
+            # first new request submitted by an HTTP handler -> added by the engine thread
+            res = [e[0] for e in ev if e[1] == "resolved" and prev[-1] <= e[0] < w[0][0]]
+            sub = [e[0] for e in ev if e[1] == "submit" and prev[-1] <= e[0] <= w[0][0]]
+            if res and sub:
+                print(f"[trace]   last decode -> answers resolved {(res[-1] - prev[-1]) * 1e3:.1f} ms, "
+                      f"-> first submit {(sub[0] - res[-1]) * 1e3:.1f} ms, -> first add {(w[0][0] - sub[0]) * 1e3:.1f} ms",
+                      file=sys.stderr)
         gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
         print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"
               + (f" median gap {gaps[len(gaps) // 2] * 1e3:.2f} ms max gap {gaps[-1] * 1e3:.2f} ms" if gaps else ""),

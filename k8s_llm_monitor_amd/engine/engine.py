@@ -722,6 +722,8 @@ class EngineService:
             if isinstance(fut, Future) and not fut.done():
                 self.latencies_ms.append(seq.timings()["latency_ms"])
                 fut.set_result((eng.decode_text(seq), seq))
+        if finished and eng.trace is not None:
+            eng.trace.append((time.perf_counter(), "resolved", len(finished), 0))
 
     def _on_failure(self, e: BaseException) -> None:
         """A step raised: fail the requests in flight, reset the batch, maybe go unhealthy."""

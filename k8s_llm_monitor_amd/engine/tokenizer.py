@@ -36,6 +36,7 @@ class ByteBPETokenizer:
         for a, b in self.merges:
             self._bytes.append(self._bytes[a] + self._bytes[b])
         self._cache: dict[str, list[int]] = {}
+        self._dec_tables: dict[bool, list[bytes]] = {}
         self._native = None
         try:
             from ..runtime import native_runtime
@@ -77,20 +78,26 @@ class ByteBPETokenizer:
             out.extend(ids)
         return out
 
-    def decode(self, ids: Iterable[int], skip_special: bool = True) -> str:
-        buf = bytearray()
+    def _token_bytes(self, t: int, skip_special: bool) -> bytes:
+        if t < 0 or (skip_special and t in (self.bos_id, self.eos_id)):
+            return b""
         nb = self.n_base
-        for t in ids:
-            if t in (self.bos_id, self.eos_id) and skip_special:
-                continue
-            if t < 0:
-                continue
-            if t < nb:
-                buf += self._bytes[t]
-            elif nb > 256:  # uncovered id from a random-init model: fold onto the merge range
-                buf += self._bytes[256 + (t - nb) % (nb - 256)]
-            else:
-                buf += self._bytes[t % 256]
+        if t < nb:
+            return self._bytes[t]
+        if nb > 256:  # uncovered id from a random-init model: fold onto the merge range
+            return self._bytes[256 + (t - nb) % (nb - 256)]
+        return self._bytes[t % 256]
+
+    def decode(self, ids: Iterable[int], skip_special: bool = True) -> str:
+        # one bytes object per vocabulary id, built on first use: a whole answer is then one
+        # list lookup per token and one join (an engine step's finished answers are decoded on the
+        # engine thread)
+        tbl = self._dec_tables.get(skip_special)
+        if tbl is None:
+            tbl = [self._token_bytes(t, skip_special) for t in range(self.vocab_size)]
+            self._dec_tables[skip_special] = tbl
+        n = len(tbl)
+        buf = b"".join([tbl[t] if 0 <= t < n else self._token_bytes(t, skip_special) for t in ids])
         return buf.decode("utf-8", errors="replace")
 
     # --------------------------------------------------------------- persistence

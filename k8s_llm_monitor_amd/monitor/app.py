@@ -182,6 +182,94 @@ def build_app_for_bench(engine_service, host: str = "127.0.0.1", port: int = 0, 
     return srv, srv.server_address[1]
 
 
+class QueryClient:
+    """Concurrent /api/v1/query client with persistent state across waves: one worker thread per
+    concurrent request, each keeping its HTTP/1.1 keep-alive connection to the server (the REST
+    server speaks HTTP/1.1), so a benchmark wave costs no thread spawns and no TCP handshakes on
+    either side - as long-lived clients behave."""
+
+    def __init__(self, host: str = "127.0.0.1", workers: int = 64):
+        import concurrent.futures as cf
+        import threading
+
+        self.host = host
+        self.ex = cf.ThreadPoolExecutor(max_workers=workers, thread_name_prefix="client")
+        self.workers = workers
+        self._tls = threading.local()
+
+    def _conn(self, port: int, fresh: bool = False):
+        import http.client
+        import socket
+
+        c = getattr(self._tls, "conn", None)
+        if fresh or c is None or getattr(self._tls, "port", None) != port:
+            if c is not None:
+                c.close()
+            c = http.client.HTTPConnection(self.host, port, timeout=900)
+            c.connect()
+            c.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)  # no Nagle wait on keep-alive
+            self._tls.conn, self._tls.port = c, port
+        return c
+
+    def _request(self, port: int, path: str, body: bytes):
+        import http.client
+
+        for attempt in range(2):  # a keep-alive connection the server closed meanwhile: reconnect once
+            conn = self._conn(port, fresh=attempt > 0)
+            try:
+                conn.request("POST", path, body, {"Content-Type": "application/json"})
+                r = conn.getresponse()
+                data = r.read()
+                if r.getheader("Connection", "").lower() == "close":
+                    conn.close()
+                    self._tls.conn = None
+                return r.status, data
+            except (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError,
+                    http.client.CannotSendRequest):
+                conn.close()
+                self._tls.conn = None
+                if attempt:
+                    raise
+        raise RuntimeError("unreachable")
+
+    def post_queries(self, port: int, items: list, max_new_tokens: int, offsets_s: Optional[list] = None,
+                     allow_errors: bool = False) -> list:
+        t_start = time.perf_counter()
+
+        def one(i):
+            q, ctx = items[i]
+            if offsets_s is not None:
+                delay = t_start + offsets_s[i] - time.perf_counter()
+                if delay > 0:
+                    time.sleep(delay)
+            body = json.dumps({"question": q, "max_tokens": max_new_tokens, "ignore_eos": True,
+                               "context": {"cluster_state": ctx}}).encode()
+            t0 = time.perf_counter()
+            status, raw = self._request(port, "/api/v1/query", body)
+            data = json.loads(raw)
+            lat = (time.perf_counter() - t0) * 1e3
+            if status != 200 or data.get("status") != "success":
+                if allow_errors:
+                    return {"http_status": status, "error": data.get("error"), "http_latency_ms": lat,
+                            "t_send_s": t0 - t_start}
+                raise RuntimeError(f"query failed: HTTP {status}: {data}")
+            res = data["result"]
+            res["http_status"] = status
+            res["http_latency_ms"] = lat
+            res["t_send_s"] = t0 - t_start
+            return res
+
+        if len(items) > self.workers:
+            raise ValueError(f"{len(items)} concurrent requests > {self.workers} client workers")
+        return list(self.ex.map(one, range(len(items))))
+
+    def close(self) -> None:
+        self.ex.shutdown(wait=True)
+
+
+_CLIENTS: dict = {}
+
+
 def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0.0.1",
                  concurrency: Optional[int] = None, offsets_s: Optional[list] = None,
                  allow_errors: bool = False) -> list:
@@ -189,40 +277,14 @@ def post_queries(port: int, items: list, max_new_tokens: int, host: str = "127.0
     per-request result dicts (answer, timings, ``http_latency_ms``).  ``offsets_s``: open-loop
     arrivals - request i is sent ``offsets_s[i]`` seconds after the call starts (``t_send_s``
     records when it went out).  ``allow_errors``: a non-200 answer becomes
-    ``{"http_status": code, "error": ...}`` instead of raising (overload / admission studies)."""
-    import concurrent.futures as cf
-    import http.client
-
-    t_start = time.perf_counter()
-
-    def one(i):
-        q, ctx = items[i]
-        if offsets_s is not None:
-            delay = t_start + offsets_s[i] - time.perf_counter()
-            if delay > 0:
-                time.sleep(delay)
-        body = json.dumps({"question": q, "max_tokens": max_new_tokens, "ignore_eos": True,
-                           "context": {"cluster_state": ctx}}).encode()
-        conn = http.client.HTTPConnection(host, port, timeout=900)
-        t0 = time.perf_counter()
-        conn.request("POST", "/api/v1/query", body, {"Content-Type": "application/json"})
-        r = conn.getresponse()
-        data = json.loads(r.read())
-        conn.close()
-        lat = (time.perf_counter() - t0) * 1e3
-        if r.status != 200 or data.get("status") != "success":
-            if allow_errors:
-                return {"http_status": r.status, "error": data.get("error"), "http_latency_ms": lat,
-                        "t_send_s": t0 - t_start}
-            raise RuntimeError(f"query failed: HTTP {r.status}: {data}")
-        res = data["result"]
-        res["http_status"] = r.status
-        res["http_latency_ms"] = lat
-        res["t_send_s"] = t0 - t_start
-        return res
-
-    with cf.ThreadPoolExecutor(max_workers=concurrency or len(items)) as ex:
-        return list(ex.map(one, range(len(items))))
+    ``{"http_status": code, "error": ...}`` instead of raising (overload / admission studies).
+    Calls with the same (host, concurrency) share one persistent :class:`QueryClient`."""
+    n = concurrency or len(items)
+    key = (host, n)
+    cl = _CLIENTS.get(key)
+    if cl is None:
+        cl = _CLIENTS[key] = QueryClient(host, n)
+    return cl.post_queries(port, items, max_new_tokens, offsets_s=offsets_s, allow_errors=allow_errors)
 
 
 def post_pod_communication(port: int, pairs: list, max_new_tokens: int, host: str = "127.0.0.1") -> list:

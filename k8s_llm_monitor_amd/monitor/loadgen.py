@@ -11,6 +11,8 @@ Protocol: one JSON request per stdin line, one JSON reply per stdout line.
     {"op": "query", "port": P, "items": [[question, context], ...], "max_new_tokens": N,
      "offsets_s": [...] (optional, open-loop arrival times), "allow_errors": bool (optional),
      "slim": bool (optional: only the timing / token-count fields travel back)}
+    {"op": "stage", "key": K, "items": [[question, context], ...]}   (kept for later "query"s)
+    {"op": "query", "port": P, "staged": K, ...}   (the staged items: only the key crosses the pipe)
     {"op": "podcomm", "port": P, "pairs": [[pod_a, pod_b], ...], "max_new_tokens": N}
     -> {"ok": true, "results": [...]}   (post_queries / post_pod_communication result dicts)
     -> {"ok": false, "error": "..."}
@@ -33,14 +35,19 @@ def serve(stdin=None, stdout=None) -> None:
 
     stdin = stdin or sys.stdin
     stdout = stdout or sys.stdout
+    staged: dict = {}
     for line in stdin:
         line = line.strip()
         if not line:
             continue
         try:
             req = json.loads(line)
-            if req["op"] == "query":
-                res = post_queries(req["port"], [tuple(x) for x in req["items"]], req["max_new_tokens"],
+            if req["op"] == "stage":
+                staged[str(req["key"])] = [tuple(x) for x in req["items"]]
+                res = []
+            elif req["op"] == "query":
+                items = staged[str(req["staged"])] if req.get("staged") is not None else [tuple(x) for x in req["items"]]
+                res = post_queries(req["port"], items, req["max_new_tokens"],
                                    offsets_s=req.get("offsets_s"), allow_errors=bool(req.get("allow_errors")))
                 if req.get("slim"):
                     res = [{k: r[k] for k in _SLIM if k in r} for r in res]
@@ -75,11 +82,20 @@ class LoadGen:
             raise RuntimeError(f"load generator: {rep['error']}")
         return rep["results"]
 
-    def post_queries(self, port: int, items: list, max_new_tokens: int, offsets_s: list | None = None,
-                     allow_errors: bool = False, slim: bool = False) -> list:
-        return self._call({"op": "query", "port": port, "items": [list(x) for x in items],
-                           "max_new_tokens": max_new_tokens, "offsets_s": offsets_s, "allow_errors": allow_errors,
-                           "slim": slim})
+    def stage(self, key, items: list) -> None:
+        """Hand ``items`` to the child once (outside any timed region); later post_queries(staged=key)
+        send only the key."""
+        self._call({"op": "stage", "key": str(key), "items": [list(x) for x in items]})
+
+    def post_queries(self, port: int, items: list | None, max_new_tokens: int, offsets_s: list | None = None,
+                     allow_errors: bool = False, slim: bool = False, staged=None) -> list:
+        req = {"op": "query", "port": port, "max_new_tokens": max_new_tokens, "offsets_s": offsets_s,
+               "allow_errors": allow_errors, "slim": slim}
+        if staged is not None:
+            req["staged"] = str(staged)
+        else:
+            req["items"] = [list(x) for x in items]
+        return self._call(req)
 
     def post_pod_communication(self, port: int, pairs: list, max_new_tokens: int) -> list:
         return self._call({"op": "podcomm", "port": port, "pairs": [list(x) for x in pairs],

@@ -46,9 +46,34 @@ def test_query_path_from_loadgen_process(served):
         with pytest.raises(RuntimeError, match="unknown op"):
             lg._call({"op": "bogus"})  # errors come back to the parent; the child keeps serving
         assert len(lg.post_queries(port, items[:1], 2)) == 1
+        # staged payloads: only the key crosses the pipe; the same keep-alive client serves twice
+        lg.stage("w0", items)
+        for _ in range(2):
+            res = lg.post_queries(port, None, 3, staged="w0", slim=True)
+            assert [r["completion_tokens"] for r in res] == [3, 3, 3]
+            assert set(res[0]) <= {"http_status", "http_latency_ms", "t_send_s", "error", "prompt_tokens",
+                                   "completion_tokens", "ttft_ms", "latency_ms", "finish_reason", "type"}
     finally:
         lg.close()
     assert lg.proc.returncode == 0
+
+
+def test_query_client_keeps_connections(served):
+    """Consecutive waves reuse each worker's HTTP/1.1 connection (no reconnect per request)."""
+    from k8s_llm_monitor_amd.monitor.app import QueryClient
+
+    svc, port = served
+    cl = QueryClient(workers=2)
+    try:
+        items = [(q, ctx[:300]) for ctx, q in (synthetic_context(s) for s in range(20, 22))]
+        cl.post_queries(port, items, 2)
+        before = [cl.ex.submit(lambda: getattr(cl._tls, "conn", None)).result() for _ in range(4)]
+        cl.post_queries(port, items, 2)
+        after = [cl.ex.submit(lambda: getattr(cl._tls, "conn", None)).result() for _ in range(4)]
+        live = [c for c in before if c is not None]
+        assert live and {id(c) for c in live} & {id(c) for c in after if c is not None}
+    finally:
+        cl.close()
 
 
 def test_pod_communication_path(served):
