@@ -239,6 +239,7 @@ class BlockManager:
         seq.num_computed = 0
         seq.chunk = 0
         seq.prefilled = False
+        seq.pending_first = 0
 
     def usage(self) -> float:
         return 1.0 - self.pool.num_free / max(1, self.num_blocks)

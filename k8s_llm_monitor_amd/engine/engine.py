@@ -122,6 +122,9 @@ class LLMEngine:
                          "deadline_stops": 0, "step_failures": 0}
         self.is_leader = self.ps.tp_rank == 0
         self._inflight = None  # (seqs, DecodeHandle) of the enqueued, not yet read back decode step
+        # (plan, DecodeHandle, step id) of the enqueued, not yet read back prefill-only step
+        self._pf_inflight = None
+        self._pf_step_id = 0
         self.trace: Optional[list] = [] if os.environ.get("K8SLLM_TRACE") else None  # (t, kind, n, tokens)
         self._inflight_rows: dict = {}
         # TP: the step bus to the workers (shared-memory ring, parallel/step_bus.py) - collective
@@ -162,7 +165,7 @@ class LLMEngine:
         return seq
 
     def has_work(self) -> bool:
-        return self.sched.has_work() or self._inflight is not None
+        return self.sched.has_work() or self._inflight is not None or self._pf_inflight is not None
 
     PENDING = -1  # placeholder for a token sampled by the in-flight decode step
 
@@ -184,11 +187,27 @@ class LLMEngine:
             done += self._resolve()
         plan = s.schedule()
         self.counters["preemptions"] += len(plan.preempted)
+        if self._pf_inflight is not None:
+            if plan.is_prefill and not plan.decode:
+                # pipelined prefill: enqueue this step behind the in-flight one, then read that one
+                # back - the host's scheduling and input staging overlap the GPU's previous step
+                h = self._launch_prefill(plan)
+                done += self._resolve_prefill()
+                self._pf_inflight = h
+                return done
+            done += self._resolve_prefill()
+            if not plan.is_prefill:
+                # the decode rows left out the sequences whose first token was in flight: plan again
+                plan = s.schedule()
+                self.counters["preemptions"] += len(plan.preempted)
         if plan.empty:
             if self._inflight is not None:
                 done += self._resolve()
             return done
         if plan.is_prefill:
+            if not plan.decode and self._inflight is None:
+                self._pf_inflight = self._launch_prefill(plan)  # read back by the next step
+                return done
             return done + self._run_sync(plan)
         # length-limited sequences whose last token is already in flight stop on resolve: skip them
         seqs = [q for q in plan.seqs if not self._length_done(q)]
@@ -207,6 +226,48 @@ class LLMEngine:
         self._inflight_rows = {q.seq_id: i for i, q in enumerate(seqs)}
         if prev is not None:
             done += self._resolve_step(*prev)
+        return done
+
+    def _launch_prefill(self, plan) -> tuple:
+        """Enqueue a prefill-only step without reading its tokens back.  Chunk accounting happens
+        now; a sequence whose prompt this step completes waits in ``pending_first`` (neither
+        prefillable nor decodable) until :meth:`_resolve_prefill` appends its first token."""
+        if self.bus is not None:
+            self.bus.send_obj(self._pack(plan))
+        plan.chunks = [q.chunk for q in plan.seqs]  # for the trace (chunk_done clears them)
+        h = self.runner.prefill_launch(plan.seqs)
+        self._pf_step_id += 1
+        sid = self._pf_step_id
+        for seq in plan.seqs:
+            if self.sched.chunk_done(seq):
+                seq.prefilled = False
+                seq.pending_first = sid
+        return plan, h, sid
+
+    def _resolve_prefill(self) -> list[Sequence]:
+        plan, h, sid = self._pf_inflight
+        self._pf_inflight = None
+        toks = self.runner.decode_collect(h)
+        self._check_collectives()
+        self.counters["prefill_steps"] += 1
+        if self.trace is not None:
+            self.trace.append((time.perf_counter(), "prefill", len(plan.seqs), sum(plan.chunks)))
+        now = time.perf_counter()
+        done = []
+        for seq, tok in zip(plan.seqs, toks):
+            if seq.pending_first != sid:
+                continue  # a chunk short of the prompt's end, or freed (preempted / aborted) since
+            seq.pending_first = 0
+            seq.prefilled = True
+            seq.output_ids.append(int(tok))
+            self.counters["generated_tokens"] += 1
+            if seq.t_first_token is None:
+                seq.t_first_token = now
+            reason = self._stop_reason(seq, int(tok), now=now)
+            if reason:
+                seq.t_finish = now
+                self._finish(seq, reason)
+                done.append(seq)
         return done
 
     def _length_done(self, q: Sequence) -> bool:
@@ -321,6 +382,7 @@ class LLMEngine:
         sequence (their KV blocks return to the pool).  Returns the aborted sequences."""
         self._inflight = None
         self._inflight_rows = {}
+        self._pf_inflight = None
         if self.device.type == "cuda":
             try:
                 torch.cuda.synchronize(self.device)

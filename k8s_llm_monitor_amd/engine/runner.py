@@ -80,6 +80,10 @@ class ModelRunner:
         self._stage_i = 0
         self.h_out = [torch.zeros(B, dtype=torch.int32, pin_memory=self.is_gpu) for _ in range(2)]
         self._out_i = 0
+        self._pf_bufs = [None, None]  # pinned prefill-input staging (_pf_stage)
+        self._pf_i = 0
+        self._pf_out = [None, None]  # pinned sampled tokens of in-flight prefill steps
+        self._pf_oi = 0
         self.buckets = [b for b in DEFAULT_BUCKETS if b < B] + [B]
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -100,22 +104,56 @@ class ModelRunner:
 
     # --------------------------------------------------------------------- prefill
     def prefill(self, seqs: list[Sequence], decode: Optional[list] = None) -> list[int]:
-        """Run each sequence's scheduled prefill chunk: tokens [num_computed, num_computed + chunk)
-        of its prompt (+ any tokens generated before a preemption); the first num_computed tokens
-        already have their KV in the cache (prefix-cache hits, earlier chunks) and are attended
-        through the paged flash prefill.  ``decode`` (a mixed step): running sequences that also
-        get their next token in this forward - their rows come first and attend through
-        paged_decode.  Returns the sampled token of every decode row, then of every chunk (the
-        first output token of the sequences whose prompt this step completes)."""
+        """One prefill (or mixed) step, synchronous: see :meth:`prefill_launch`."""
+        return self.decode_collect(self.prefill_launch(seqs, decode))
+
+    def _pf_stage(self, n: int) -> torch.Tensor:
+        """Pinned int32 staging for one prefill step's inputs, alternating between two buffers
+        (the previous step's copy may still be queued behind the step before it); grown on demand."""
+        i = self._pf_i
+        self._pf_i ^= 1
+        buf = self._pf_bufs[i]
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(n, 1 << 16) * 5 // 4, dtype=torch.int32, pin_memory=self.is_gpu)
+            self._pf_bufs[i] = buf
+        return buf
+
+    def prefill_launch(self, seqs: list[Sequence], decode: Optional[list] = None) -> "DecodeHandle":
+        """Enqueue each sequence's scheduled prefill chunk - tokens [num_computed, num_computed +
+        chunk) of its prompt (+ any tokens generated before a preemption) - without waiting for it;
+        the first num_computed tokens already have their KV in the cache (prefix-cache hits,
+        earlier chunks) and are attended through the paged flash prefill.  ``decode`` (a mixed
+        step): running sequences that also get their next token in this forward - their rows come
+        first and attend through paged_decode.  The handle yields the sampled token of every decode
+        row, then of every chunk (the first output token of the sequences whose prompt this step
+        completes).  Every input goes over in ONE host-to-device copy from pinned memory, so a step
+        can be enqueued while the previous one still runs (pipelined prefill)."""
         dev = self.device
         decode = decode or []
         nd = len(decode)
         starts = [s.num_computed for s in seqs]
         lens = [s.chunk or (s.num_tokens - c) for s, c in zip(seqs, starts)]
         T = nd + sum(lens)
-        ids = np.empty(T, dtype=np.int32)
-        pos = np.empty(T, dtype=np.int32)
-        slots = np.empty(T, dtype=np.int32)
+        rows = list(decode) + list(seqs)
+        R = len(rows)
+        cu = np.zeros(len(seqs) + 1, dtype=np.int32)
+        cu[1:] = np.cumsum(lens)
+        qs, st = ops.prefill_qblocks(cu.tolist(), ctx_starts=starts)
+        nq = len(qs)
+        paged = any(starts)
+        W = max(len(s.block_table) for s in seqs) if paged else 0
+        Wd = max(len(q.block_table) for q in decode) if nd else 0
+        # layout of the staging buffer (int32 words; the float sampling parameters bit-cast)
+        sizes = dict(ids=T, pos=T, slots=T, cu=len(seqs) + 1, qs=nq, st=nq, lidx=R, temp=R, topk=R, topp=R,
+                     cst=len(seqs) if paged else 0, bt=len(seqs) * W, dbt=nd * Wd, dlen=nd)
+        off, o = {}, 0
+        for k, n in sizes.items():
+            off[k] = o
+            o += n
+        buf = self._pf_stage(o)
+        h = buf.numpy()
+        v = {k: h[off[k]:off[k] + n] for k, n in sizes.items()}
+        ids, pos, slots = v["ids"], v["pos"], v["slots"]
         for i, q in enumerate(decode):  # the token being fed is the last generated one
             p = q.num_tokens - 1
             ids[i] = q.last_token
@@ -130,44 +168,58 @@ class ModelRunner:
             bt = np.asarray(s.block_table, dtype=np.int32)
             slots[o:o + n] = bt[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
             o += n
-        cu = np.zeros(len(seqs) + 1, dtype=np.int32)
-        cu[1:] = np.cumsum(lens)
-        qs, st = ops.prefill_qblocks(cu.tolist(), ctx_starts=starts)
-        t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dt, non_blocking=True)
-        logits_idx = np.concatenate([np.arange(nd, dtype=np.int64), nd + cu[1:].astype(np.int64) - 1])
-        meta = AttnMeta(is_prefill=True, positions=t(pos), slot_mapping=t(slots), cu_seqlens=t(cu),
-                        qb_seq=t(np.asarray(qs, dtype=np.int32)), qb_start=t(np.asarray(st, dtype=np.int32)),
-                        logits_idx=t(logits_idx, torch.int64))
-        if any(starts):
-            W = max(len(s.block_table) for s in seqs)
-            bt = np.zeros((len(seqs), W), dtype=np.int32)
+        v["cu"][:] = cu
+        v["qs"][:] = qs
+        v["st"][:] = st
+        v["lidx"][:nd] = np.arange(nd, dtype=np.int32)
+        v["lidx"][nd:] = nd + cu[1:] - 1
+        v["temp"].view(np.float32)[:] = [s.params.temperature for s in rows]
+        v["topk"][:] = [s.params.top_k for s in rows]
+        v["topp"].view(np.float32)[:] = [s.params.top_p for s in rows]
+        if paged:
+            v["cst"][:] = starts
+            bt2 = v["bt"].reshape(len(seqs), W)
+            bt2[:] = 0
             for i, s in enumerate(seqs):
-                bt[i, : len(s.block_table)] = s.block_table
-            meta.ctx_start = t(np.asarray(starts, dtype=np.int32))
-            meta.block_tables = t(bt)
+                bt2[i, : len(s.block_table)] = s.block_table
         if nd:
-            W = max(len(q.block_table) for q in decode)
-            bt = np.zeros((nd, W), dtype=np.int32)
+            dbt = v["dbt"].reshape(nd, Wd)
+            dbt[:] = 0
             for i, q in enumerate(decode):
-                bt[i, : len(q.block_table)] = q.block_table
+                dbt[i, : len(q.block_table)] = q.block_table
+            v["dlen"][:] = [q.num_tokens for q in decode]
+        d = buf[: sum(sizes.values())].to(dev, non_blocking=True)
+        dv = {k: d[off[k]:off[k] + n] for k, n in sizes.items()}
+        meta = AttnMeta(is_prefill=True, positions=dv["pos"], slot_mapping=dv["slots"], cu_seqlens=dv["cu"],
+                        qb_seq=dv["qs"], qb_start=dv["st"], logits_idx=dv["lidx"].long())
+        if paged:
+            meta.ctx_start = dv["cst"]
+            meta.block_tables = dv["bt"].view(len(seqs), W)
+        if nd:
             meta.num_decode = nd
-            meta.dec_block_tables = t(bt)
-            meta.dec_seq_lens = t(np.asarray([q.num_tokens for q in decode], dtype=np.int32))
+            meta.dec_block_tables = dv["dbt"].view(nd, Wd)
+            meta.dec_seq_lens = dv["dlen"]
             meta.decode_ws = self.decode_ws
             self.n_steps["mixed"] = self.n_steps.get("mixed", 0) + 1
         # tokens attended from the paged cache instead of recomputed (prefix hits + earlier chunks)
         self.n_steps["prefill_context_tokens"] = self.n_steps.get("prefill_context_tokens", 0) + sum(starts)
         self.n_steps["prefill_tokens"] = self.n_steps.get("prefill_tokens", 0) + T
-        logits = self.model.forward(t(ids), meta, self.kv)
-        rows = list(decode) + list(seqs)
-        temp = torch.tensor([s.params.temperature for s in rows], dtype=torch.float32).to(dev)
-        topk = torch.tensor([s.params.top_k for s in rows], dtype=torch.int32).to(dev)
-        topp = torch.tensor([s.params.top_p for s in rows], dtype=torch.float32).to(dev)
-        tok = self._sample(logits, temp, topk, topp)
+        logits = self.model.forward(dv["ids"], meta, self.kv)
+        tok = self._sample(logits, dv["temp"].view(torch.float32), dv["topk"], dv["topp"].view(torch.float32))
         self.n_steps["prefill"] += 1
         if self.on_launched is not None:  # TP: the custom-AR error flag, read back with the tokens
             self.on_launched()
-        return tok[: len(rows)].cpu().tolist()
+        if not self.is_gpu:
+            return DecodeHandle(R, None, tok[:R].tolist())
+        j = self._pf_oi
+        self._pf_oi ^= 1  # two in flight at most: step N+1 is launched before step N is read back
+        if self._pf_out[j] is None or self._pf_out[j].numel() < R:
+            self._pf_out[j] = torch.empty(max(R, 2 * self.B), dtype=torch.int32, pin_memory=True)
+        out = self._pf_out[j]
+        out[:R].copy_(tok[:R], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return DecodeHandle(R, ev, out)
 
     # --------------------------------------------------------------------- decode
     def _decode_body(self, b: int) -> None:

@@ -58,6 +58,7 @@ class StepPlan:
     seqs: list[Sequence] = field(default_factory=list)
     preempted: list[Sequence] = field(default_factory=list)
     decode: list[Sequence] = field(default_factory=list)
+    chunks: list[int] = field(default_factory=list)  # per-seq chunk sizes, kept for the trace
 
     @property
     def is_mixed(self) -> bool:
@@ -105,12 +106,12 @@ class Scheduler:
     def prefill_pending(self) -> bool:
         """Would the next schedule() be a prefill step?"""
         return bool(self.waiting and len(self.running) < self.cfg.max_num_seqs) or any(
-            not q.prefilled for q in self.running)
+            not q.prefilled and not q.pending_first for q in self.running)
 
     def prefill_backlog(self) -> int:
         """Prompt tokens still to prefill: partially prefilled running sequences plus the waiting
         requests that fit the free sequence slots."""
-        n = sum(q.num_tokens - q.num_computed for q in self.running if not q.prefilled)
+        n = sum(q.num_tokens - q.num_computed for q in self.running if not q.prefilled and not q.pending_first)
         free = self.cfg.max_num_seqs - len(self.running)
         for i, q in enumerate(self.waiting):
             if i >= free:
@@ -138,7 +139,9 @@ class Scheduler:
             budget = self.cfg.max_prefill_tokens
             if mix:
                 budget = min(budget, self.cfg.mixed_prefill_tokens)
-            for seq in [q for q in self.running if not q.prefilled]:
+            # (a sequence whose last chunk is in flight - pending_first - has nothing left to prefill
+            # and cannot decode before its first token is read back)
+            for seq in [q for q in self.running if not q.prefilled and not q.pending_first]:
                 if budget <= 0:
                     break
                 self._take_chunk(seq, budget, plan)

@@ -52,6 +52,10 @@ class Sequence:
     num_computed: int = 0
     chunk: int = 0
     prefilled: bool = False
+    # pipelined prefill: id of the in-flight prefill step whose sampled token will be this
+    # sequence's first output token (its prompt is fully computed, the token not yet read back);
+    # 0 = none.  Reset whenever the sequence's blocks are freed (preemption, abort, finish).
+    pending_first: int = 0
     user: object = None  # opaque payload for the caller (future, callback, ...)
     deadline: Optional[float] = None  # time.perf_counter() by which the answer is due (engine.add_request)
 

@@ -27,6 +27,7 @@ prof_summary() {  # $1 = rocprofv3 output dir, $2 = tag, $3 = title
   f=$(find "$1" -name "*results.db" | head -1)
   python3 tools/rocpd_summary.py "$f" --top 40 --title "$3" > "gpurun_out/prof_$2_summary.md"
   python3 tools/rocpd_summary.py "$f" --decode-steps > "gpurun_out/prof_$2_steps.txt" || true
+  python3 tools/rocpd_summary.py "$f" --gaps 5.4 >> "gpurun_out/prof_$2_steps.txt" || true
   cat "gpurun_out/prof_$2_steps.txt"
   rm -rf "$1"
 }

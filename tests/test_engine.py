@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+from k8s_llm_monitor_amd.engine.sequence import SeqStatus
 from k8s_llm_monitor_amd.models import AttnMeta
 
 
@@ -272,3 +273,27 @@ def test_decode_staging_layout_and_resolve_ids_cpu():
     src = torch.tensor([-1, 2, -1, 0], dtype=torch.int32)
     prev = torch.tensor([100, 101, 102, 103], dtype=torch.int32)
     assert ops.resolve_ids(ids, src, prev).tolist() == [10, 102, 12, 100]
+
+
+def test_pipelined_prefill_matches_sync_engine():
+    """Prefill-only steps are enqueued before the previous one is read back (pending_first): a
+    burst prefilled over several pipelined steps (chunked prompts, a mid-burst abort) yields the
+    same greedy tokens as the synchronous engine, and no KV block leaks."""
+    prompts = [f"pod-{i} CrashLoopBackOff on node-{i:03d}, restarts={i * 7}; " * (3 + i % 3) for i in range(6)]
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for pipe in (True, False):
+        eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=8, max_model_len=512, num_blocks=256,
+                                     use_graphs=False, seed=3, dtype="float32", prefix_caching=False,
+                                     max_prefill_tokens=48, pipeline=pipe), device="cpu")
+        seqs = [eng.add_request(p, sp) for p in prompts]
+        extra = eng.add_request("aborted while its prefill is in flight " * 4, sp)
+        eng.step()
+        eng.step()
+        eng.abort(extra)
+        while eng.has_work():
+            eng.step()
+        assert all(s.status == SeqStatus.FINISHED and len(s.output_ids) == 5 for s in seqs)
+        assert eng.blocks.num_free == 256
+        outs[pipe] = [s.output_ids for s in seqs]
+    assert outs[True] == outs[False]

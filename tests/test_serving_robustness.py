@@ -57,7 +57,9 @@ def test_mixed_step_keeps_decodes_running_and_matches_unmixed():
                                      mixed_prefill_tokens=mixed, max_prefill_tokens=32,
                                      max_decode_stall_steps=0), device="cpu")
         a = eng.add_request(prompts[0], sp)
-        for _ in range(3):  # a is chunked over 2 prefills then decodes one step
+        for _ in range(8):  # a is chunked over 3 prefill steps (pipelined: read back one step later)
+            if a.prefilled:
+                break
             eng.step()
         assert a.prefilled and len(a.output_ids) >= 1
         b = eng.add_request(prompts[1], sp)
@@ -183,7 +185,7 @@ def test_cancel_frees_blocks():
 def test_step_failure_fails_only_inflight_then_unhealthy():
     eng = _tiny_engine()
     svc = EngineService(eng, max_failures=2)
-    real = eng.runner.prefill
+    real = eng.runner.prefill_launch  # every prefill path (pipelined and mixed) goes through it
     boom = {"n": 1}
 
     def flaky(*a, **k):
@@ -192,7 +194,7 @@ def test_step_failure_fails_only_inflight_then_unhealthy():
             raise RuntimeError("injected HIP fault")
         return real(*a, **k)
 
-    eng.runner.prefill = flaky
+    eng.runner.prefill_launch = flaky
     sp = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True)
     try:
         with pytest.raises(RuntimeError, match="injected"):

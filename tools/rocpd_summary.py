@@ -45,13 +45,46 @@ def decode_steps(db: str) -> None:
     print(f"mean busy {sum(s[0] for s in spans) / n / 1e6:.3f} ms, mean wall {sum(s[1] for s in spans) / n / 1e6:.3f} ms")
 
 
+def gaps(db: str, window_s: float = 5.4, min_us: float = 20.0) -> None:
+    """GPU idle time in the last ``window_s`` seconds of the trace (the timed waves): total idle,
+    idle gaps longer than ``min_us`` grouped by the kernels around them, and the busy fraction."""
+    import collections
+
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    t1 = max(r[2] for r in rows)
+    win0 = t1 - int(window_s * 1e9)
+    be, idle, small = rows[0][2], 0, 0
+    by, cnt = collections.Counter(), collections.Counter()
+    for (n0, s0, e0), (n1, s1, e1) in zip(rows, rows[1:]):
+        be = max(be, e0)
+        if s1 < win0 or s1 <= be:
+            continue
+        g = s1 - be
+        idle += g
+        if g > min_us * 1e3:
+            k = (n0.split("(")[0][-45:], n1.split("(")[0][-45:])
+            by[k] += g
+            cnt[k] += 1
+        else:
+            small += g
+    print(f"last {window_s:.1f} s: idle {idle / 1e6:.1f} ms ({100 * idle / (window_s * 1e9):.1f} %), "
+          f"of which gaps <= {min_us:.0f} us {small / 1e6:.1f} ms")
+    for (a, b), g in by.most_common(12):
+        print(f"{g / 1e6:8.2f} ms  x{cnt[(a, b)]:5d}  after {a}  before {b}")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--title", default="")
     ap.add_argument("--decode-steps", action="store_true", help="print decode-step kernel-busy statistics only")
+    ap.add_argument("--gaps", type=float, default=0.0, help="print GPU idle gaps of the last GAPS seconds only")
     a = ap.parse_args()
+    if a.gaps > 0:
+        gaps(a.db, a.gaps)
+        return
     if a.decode_steps:
         decode_steps(a.db)
         return
