@@ -76,7 +76,12 @@ class ModelRunner:
             if self.is_gpu else None
         # pinned host staging, double-buffered: with pipelined decode the host fills step N+1's
         # inputs while step N's host-to-device copies may still be queued
-        self.stage = [_Staging(B, self.max_blocks_per_seq, self.is_gpu) for _ in range(2)]
+        self.stage = [_Staging(B, self.max_blocks_per_seq, self.is_gpu, idx=i) for i in range(2)]
+        # the staging copy as the first node of each decode graph (one graph per staging buffer and
+        # bucket): a replay then starts with its own inputs instead of a separate copy in front of it
+        # (removes a ~100 us launch gap per decode step between the copy and the graph's first
+        # kernel; profiles/r03/README.md)
+        self.graph_h2d = True
         self._stage_i = 0
         self.h_out = [torch.zeros(B, dtype=torch.int32, pin_memory=self.is_gpu) for _ in range(2)]
         self._out_i = 0
@@ -85,7 +90,7 @@ class ModelRunner:
         self._pf_out = [None, None]  # pinned sampled tokens of in-flight prefill steps
         self._pf_oi = 0
         self.buckets = [b for b in DEFAULT_BUCKETS if b < B] + [B]
-        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graphs: dict[int, list] = {}  # bucket -> [graph] (or one graph per staging buffer)
         self.graph_pool = None
         self.n_steps = {"prefill": 0, "decode": 0}
         self.on_launched = None  # hook after every step's launch (TP: enqueue the custom-AR error readback)
@@ -249,10 +254,16 @@ class ModelRunner:
         torch.cuda.synchronize()
         self.graph_pool = torch.cuda.graph_pool_handle()
         for b in sorted(buckets or self.buckets, reverse=True):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
-                self._decode_body(b)
-            self.graphs[b] = g
+            n_el = _Staging.prefix(self.B, self.max_blocks_per_seq, b)
+            gs = []
+            for st in (self.stage if self.graph_h2d else [None]):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool):
+                    if st is not None:
+                        self.d_all[:n_el].copy_(st.h_all[:n_el], non_blocking=True)
+                    self._decode_body(b)
+                gs.append(g)
+            self.graphs[b] = gs
         torch.cuda.synchronize()
         self.rng.copy_(rng_state)
 
@@ -310,12 +321,15 @@ class ModelRunner:
         return self._launch_staged(st, n, b, n_el)
 
     def _launch_staged(self, st: "_Staging", n: int, b: int, n_el: int) -> "DecodeHandle":
-        self.d_all[:n_el].copy_(st.h_all[:n_el], non_blocking=True)
-        g = self.graphs.get(b)
-        if g is not None:
-            g.replay()
+        gs = self.graphs.get(b)
+        if gs is not None and self.graph_h2d:
+            gs[st.idx].replay()  # its first node copies this staging buffer (n_el = the bucket's prefix)
         else:
-            self._decode_body(b)
+            self.d_all[:n_el].copy_(st.h_all[:n_el], non_blocking=True)
+            if gs is not None:
+                gs[0].replay()
+            else:
+                self._decode_body(b)
         self.n_steps["decode"] += 1
         if self.on_launched is not None:
             self.on_launched()
@@ -370,9 +384,10 @@ class _Staging:
         bt = bt.view(B, max_blocks) if isinstance(buf, torch.Tensor) else bt.reshape(B, max_blocks)
         return (*f, bt)
 
-    def __init__(self, B: int, max_blocks: int, pin: bool):
+    def __init__(self, B: int, max_blocks: int, pin: bool, idx: int = 0):
         from ..parallel.step_bus import DECODE_HDR, KIND_DECODE
 
+        self.idx = idx
         # DECODE_HDR leading words hold the step-bus header, so a TP leader publishes
         # full[:DECODE_HDR + n_el] without a copy (parallel/step_bus.py)
         self.h_full = torch.zeros(DECODE_HDR + self.size(B, max_blocks), dtype=torch.int32, pin_memory=pin)

@@ -72,6 +72,18 @@ def gaps(db: str, window_s: float = 5.4, min_us: float = 20.0) -> None:
           f"of which gaps <= {min_us:.0f} us {small / 1e6:.1f} ms")
     for (a, b), g in by.most_common(12):
         print(f"{g / 1e6:8.2f} ms  x{cnt[(a, b)]:5d}  after {a}  before {b}")
+    # the kernels around the three largest gaps (start relative to the gap, duration)
+    big = []
+    be = rows[0][2]
+    for i in range(1, len(rows)):
+        be = max(be, rows[i - 1][2])
+        if rows[i][1] >= win0 and rows[i][1] - be > min_us * 1e3:
+            big.append((rows[i][1] - be, i, be))
+    for g, i, gs in sorted(big, reverse=True)[:3]:
+        print(f"-- gap {g / 1e6:.2f} ms:")
+        for j in range(max(0, i - 4), min(len(rows), i + 4)):
+            n, st, en = rows[j]
+            print(f"   {(st - gs) / 1e3:+10.1f} us  {(en - st) / 1e3:8.1f} us  {n.split('(')[0][-60:]}")
 
 
 def main() -> None:
