@@ -733,9 +733,9 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
 # Prefill projections (qkv / o / gate_up + SwiGLU / down) on the hand-written 4-wave MFMA GEMM
 # (csrc/gemm_tile.hip, two-barrier schedule) or hipBLASLt (torch F.linear).  K8SLLM_PREFILL_GEMM=
 # tile|blas forces one; the default ("auto") takes the tile kernel where it measured at least at
-# parity with hipBLASLt on the same box: the fused gate_up + SwiGLU (1.46 vs 1.43 PF/s including
-# hipBLASLt's separate silu_mul pass); qkv / o / down stay on hipBLASLt, 6-12 % faster there
-# (profiles/r03/gemm_schedules.jsonl).
+# parity with hipBLASLt on the same box: the fused gate_up + SwiGLU (1.50 vs 1.42 PF/s including
+# hipBLASLt's separate silu_mul pass); qkv / o / down stay on hipBLASLt, 4-8 % faster there
+# (profiles/r03/gemm_ring_addressing.jsonl).
 PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "auto")
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 TILE_ALGO = 1  # refill schedule: two barriers per k-tile

@@ -33,7 +33,12 @@
 //  1: two barriers per k-tile: the mid-(t, 0) barrier (every wave holds tile t's k-half-1
 //     fragments in registers) frees BOTH of tile t's half-slots, so B_{t+2} and A_{t+3} are DMA'd
 //     from there on and every piece gets >= ~120 MFMAs to land.  2-6 % faster than SCH 0 on the
-//     Llama-3-8B prefill shapes (profiles/r03/gemm_schedules.jsonl).
+//     Llama-3-8B prefill shapes (profiles/r03/gemm_schedules.jsonl).  Its ring addressing is
+//     scalar: the tile's five half-slot offsets advance in SGPRs (one conditional subtract) and each
+//     sub-step forms one A and one B fragment base VGPR (block reads = base + immediate).  With
+//     `(2t + i) % 5` written inline hipcc emitted ~25 mul-hi / per-read address instructions in
+//     front of every k-tile's first MFMA; removing them made the kernel 4-5 % faster on every
+//     shape (profiles/r03/gemm_ring_addressing.jsonl).
 // Measured and removed (profiles/r03): an 8-wave 128 x 64-per-wave kernel (0.375 reads per MFMA),
 // a persistent form (spilled), register-staged refill (8-10 % slower: ds_write_b128 costs more
 // than the DMA issue), the same tile on v_mfma_f32_32x32x16_bf16 (1-5 % slower), unswizzled rows
@@ -156,21 +161,24 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
   if constexpr (SCH == 1) {
-    // piece i (0..15) of iteration t: B_{t+2} pieces 0..7 into A_t's half-slot, then A_{t+3}
-    // pieces 0..7 into B_t's (both free once the mid-(t, 0) barrier has passed)
-    auto piece16 = [&](int i, int t) {
-      if (i < 8)
-        piece(1, i, t + 2, (2 * t) % 5);
-      else
-        piece(0, i - 8, t + 3, (2 * t + 1) % 5);
+    // Ring addressing: the five half-slot byte offsets of the current
+    // tile live in SGPRs and advance by one conditional subtract per tile (SCH 1 recomputes
+    // (2t + i) % 5 with mul-hi sequences), and each sub-step forms ONE A and ONE B fragment base
+    // VGPR (every block read is that base + an immediate), where hipcc built a base per read.
+    const uint32_t fbA0 = (uint32_t)(rd[0] + wm * 16384), fbA1 = (uint32_t)(rd[1] + wm * 16384);
+    const uint32_t fbB0 = (uint32_t)(rd[0] + wn * 16384), fbB1 = (uint32_t)(rd[1] + wn * 16384);
+    auto rd16 = [&](uint32_t base, int blk) -> bf16x8 {
+      return *reinterpret_cast<const bf16x8*>(smem + base + blk * 2048);
     };
-    // PH 0 = (t, 0): fragment reads of k-half 1 of tile t on MFMAs 0-15, lgkmcnt(0) + barrier after
-    // MFMA 19, pieces 0-6 on MFMAs 22, 28, ..., 58.  PH 1 = (t, 1): reads of k-half 0 of tile t+1
-    // on MFMAs 0-15, pieces 7-15 on MFMAs 19, 24, ..., 59.  One instruction in each MFMA's shadow
-    // (a sched_barrier after every MFMA).
-    auto sub = [&](auto ph, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], int sa, int sb,
-                   int nks, int t) {
+    auto pc = [&](int o, int p, int kt, uint32_t slot_bytes) {
+      char* dst = smem + slot_bytes + (p * 4 + wave) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], min(kt, nk - 1) * 128, 0, 0);
+    };
+    auto sub = [&](auto ph, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], uint32_t sa,
+                   uint32_t sb, uint32_t da, uint32_t db, int t) {
       constexpr int PH = decltype(ph)::value;
+      // sa / sb: half-slot bytes of the fragments read here; da / db: B_{t+2}'s / A_{t+3}'s targets
+      const uint32_t ba = sa + (PH == 0 ? fbA1 : fbA0), bb = sb + (PH == 0 ? fbB1 : fbB0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
@@ -179,22 +187,25 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
           const int n = g * 8 + j;
           acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
           if (n < 8) {
-            nb[n] = frag(sb, nks, 1, n);
+            nb[n] = rd16(bb, n);
           } else if (n < 16) {
-            na[n - 8] = frag(sa, nks, 0, n - 8);
+            na[n - 8] = rd16(ba, n - 8);
           } else if (PH == 0 && n == 19) {
             lgkm_wait0();
             __builtin_amdgcn_s_barrier();
           } else if (PH == 0 && n >= 22 && (n - 22) % 6 == 0 && (n - 22) / 6 < 7) {
-            piece16((n - 22) / 6, t);
+            pc(1, (n - 22) / 6, t + 2, da);
           } else if (PH == 1 && n >= 19 && (n - 19) % 5 == 0 && (n - 19) / 5 < 9) {
-            piece16(7 + (n - 19) / 5, t);
+            const int i = 7 + (n - 19) / 5;
+            if (i < 8)
+              pc(1, i, t + 2, da);
+            else
+              pc(0, i - 8, t + 3, db);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
     };
-    // prologue: A_0 B_0 A_1 B_1 A_2 in flight (all five half-slots); tile 0 landed -> its k-half 0
     issue_half(0, 0);
     issue_half(1, 0);
     issue_half(0, 1);
@@ -207,14 +218,18 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       fa0[g] = frag(0, 0, 0, g);
       fb0[g] = frag(1, 0, 1, g);
     }
+    // half-slot indices of tile t: s0 = 2t % 5 (A_t), s1 = (2t + 1) % 5 (B_t), s2, s3 = tile t+1's
+    int s0 = 0;
+    auto nx = [](int v, int d) { return v + d >= 5 ? v + d - 5 : v + d; };
     for (int t = 0; t < nk; ++t) {
-      // the previous sub-step's reads landed long ago; an explicit lgkmcnt(0) keeps hipcc from
-      // merging that wait with the first read of this sub-step (a full LDS latency per k-tile)
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      sub(std::integral_constant<int, 0>{}, fa0, fb0, fa1, fb1, (2 * t) % 5, (2 * t + 1) % 5, 1, t);
-      vm_wait_n<15>();  // B_{t+1} landed (younger: A_{t+2}'s 8 pieces and this tile's first 7)
+      const int s1 = nx(s0, 1), s2 = nx(s0, 2), s3 = nx(s0, 3);
+      const uint32_t S0 = (uint32_t)s0 * HS, S1 = (uint32_t)s1 * HS, S2 = (uint32_t)s2 * HS, S3 = (uint32_t)s3 * HS;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): see SCH 1
+      sub(std::integral_constant<int, 0>{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
+      vm_wait_n<15>();
       __builtin_amdgcn_s_barrier();
-      sub(std::integral_constant<int, 1>{}, fa1, fb1, fa0, fb0, (2 * t + 2) % 5, (2 * t + 3) % 5, 0, t);
+      sub(std::integral_constant<int, 1>{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+      s0 = s2;
     }
     vm_wait_n<0>();
   } else {
