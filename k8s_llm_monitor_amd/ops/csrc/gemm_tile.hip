@@ -161,10 +161,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
   if constexpr (SCH == 1) {
-    // Ring addressing: the five half-slot byte offsets of the current
-    // tile live in SGPRs and advance by one conditional subtract per tile (SCH 1 recomputes
-    // (2t + i) % 5 with mul-hi sequences), and each sub-step forms ONE A and ONE B fragment base
-    // VGPR (every block read is that base + an immediate), where hipcc built a base per read.
+    // Ring addressing: the half-slot byte offsets of the current tile live in SGPRs and rotate
+    // by one conditional subtract per tile, and each sub-step forms ONE A and ONE B fragment base
+    // VGPR (every block read is that base + an immediate).
     const uint32_t fbA0 = (uint32_t)(rd[0] + wm * 16384), fbA1 = (uint32_t)(rd[1] + wm * 16384);
     const uint32_t fbB0 = (uint32_t)(rd[0] + wn * 16384), fbB1 = (uint32_t)(rd[1] + wn * 16384);
     auto rd16 = [&](uint32_t base, int blk) -> bf16x8 {
@@ -218,18 +217,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       fa0[g] = frag(0, 0, 0, g);
       fb0[g] = frag(1, 0, 1, g);
     }
-    // half-slot indices of tile t: s0 = 2t % 5 (A_t), s1 = (2t + 1) % 5 (B_t), s2, s3 = tile t+1's
-    int s0 = 0;
-    auto nx = [](int v, int d) { return v + d >= 5 ? v + d - 5 : v + d; };
+    // half-slot bytes of tile t: S0 = (2t % 5) HS (A_t), S1 = ((2t + 1) % 5) HS (B_t), S2 / S3 =
+    // tile t+1's.  Tile t+1: S0' = S2, S1' = S3, S2' = ((2t + 4) % 5) HS, S3' = S0.
+    uint32_t S0 = 0, S1 = HS, S2 = 2 * HS, S3 = 3 * HS;
     for (int t = 0; t < nk; ++t) {
-      const int s1 = nx(s0, 1), s2 = nx(s0, 2), s3 = nx(s0, 3);
-      const uint32_t S0 = (uint32_t)s0 * HS, S1 = (uint32_t)s1 * HS, S2 = (uint32_t)s2 * HS, S3 = (uint32_t)s3 * HS;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): see SCH 1
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous sub-step's reads, explicitly
       sub(std::integral_constant<int, 0>{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
       vm_wait_n<15>();
       __builtin_amdgcn_s_barrier();
       sub(std::integral_constant<int, 1>{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
-      s0 = s2;
+      const uint32_t s4 = S0 == 0 ? 4 * HS : S0 - HS, s0 = S0;
+      S0 = S2;
+      S1 = S3;
+      S2 = s4;
+      S3 = s0;
     }
     vm_wait_n<0>();
   } else {
