@@ -79,11 +79,22 @@ def gaps(db: str, window_s: float = 5.4, min_us: float = 20.0) -> None:
         be = max(be, rows[i - 1][2])
         if rows[i][1] >= win0 and rows[i][1] - be > min_us * 1e3:
             big.append((rows[i][1] - be, i, be))
-    for g, i, gs in sorted(big, reverse=True)[:3]:
+    def show(g, i, gs, ctx=4):
         print(f"-- gap {g / 1e6:.2f} ms:")
-        for j in range(max(0, i - 4), min(len(rows), i + 4)):
+        for j in range(max(0, i - ctx), min(len(rows), i + ctx)):
             n, st, en = rows[j]
             print(f"   {(st - gs) / 1e3:+10.1f} us  {(en - st) / 1e3:8.1f} us  {n.split('(')[0][-60:]}")
+
+    for g, i, gs in sorted(big, reverse=True)[:3]:
+        show(g, i, gs)
+    # one example (the median-sized gap) of each of the four costliest (before, after) classes,
+    # with more context: where a recurring host stall sits in the step sequence
+    for (a, b), _ in by.most_common(4):
+        ex = sorted((g, i, gs) for g, i, gs in big
+                    if (rows[i - 1][0].split("(")[0][-45:], rows[i][0].split("(")[0][-45:]) == (a, b))
+        if ex:
+            print(f"== class {a} -> {b}: {len(ex)} gaps, median example")
+            show(*ex[len(ex) // 2], ctx=8)
 
 
 def main() -> None:
