@@ -213,6 +213,7 @@ class LLMEngine:
         seqs = [q for q in plan.seqs if not self._length_done(q)]
         if not seqs:
             return done + (self._resolve() if self._inflight is not None else [])
+        seqs = self._attention_row_order(seqs)
         prev_rows = self._inflight_rows
         src = [prev_rows.get(q.seq_id, -1) for q in seqs]
         handle = self.runner.decode_launch(seqs, src, publish=self._publish)
@@ -227,6 +228,26 @@ class LLMEngine:
         if prev is not None:
             done += self._resolve_step(*prev)
         return done
+
+    def _attention_row_order(self, seqs: list) -> list:
+        """Decode batch rows ordered for the paged-attention grid (one workgroup per (row, kv head),
+        two per CU): with a 64-row graph every XCD runs the 64 rows of one kv head and workgroups z
+        and z + 32 share a CU, so rows 0..31 take the 32 longest contexts (longest first) and rows
+        32..63 the rest shortest first - each CU gets one long and one short sequence and no CU
+        keeps two long ones running after the rest drained (ragged 1.3k-2.3k contexts: 72.7 vs
+        77.1 us per layer for an arbitrary order, profiles/r03/decode_row_order.jsonl).  Other
+        bucket sizes: longest first (74.6 us).  Row order is free: each row's input token is
+        located through ``src`` and every per-row result is keyed by the sequence.
+        ``K8SLLM_DECODE_ROW_ORDER=0`` keeps the scheduler's order."""
+        if not _ROW_ORDER or len(seqs) < 2:
+            return seqs
+        srt = sorted(seqs, key=lambda q: -q.num_tokens)
+        n = len(srt)
+        b = self.runner.bucket_for(n) if self.runner.graphs else n
+        half = b // 2
+        if b != 2 * _CUS_PER_XCD or n <= half:
+            return srt
+        return srt[:half] + srt[half:][::-1]
 
     def _launch_prefill(self, plan) -> tuple:
         """Enqueue a prefill-only step without reading its tokens back.  Chunk accounting happens
@@ -500,6 +521,10 @@ class TpotModel:
 
     def snapshot(self) -> dict:
         return {str(b): round(t, 3) for b, t in sorted(self.ew.items())}
+
+
+_ROW_ORDER = os.environ.get("K8SLLM_DECODE_ROW_ORDER", "1") != "0"
+_CUS_PER_XCD = 32  # MI355X: 256 CUs in 8 XCDs
 
 
 class EngineOverloaded(RuntimeError):
