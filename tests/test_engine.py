@@ -297,3 +297,27 @@ def test_pipelined_prefill_matches_sync_engine():
         assert eng.blocks.num_free == 256
         outs[pipe] = [s.output_ids for s in seqs]
     assert outs[True] == outs[False]
+
+
+def test_attention_row_order_pairs_long_and_short():
+    """64-row decode graph: rows 0..31 are the 32 longest contexts (longest first), rows 32..63
+    the rest shortest first, so rows z and z + 32 (one CU in the paged-attention grid) pair the
+    k-th longest with the k-th shortest; other bucket sizes are longest first."""
+    import random
+    import types
+
+    from k8s_llm_monitor_amd.engine.engine import LLMEngine
+
+    rng = random.Random(0)
+    seqs = [types.SimpleNamespace(num_tokens=rng.randint(1200, 2400), seq_id=i) for i in range(64)]
+    eng = types.SimpleNamespace(runner=types.SimpleNamespace(graphs={64: object()}, bucket_for=lambda n: 64))
+    out = LLMEngine._attention_row_order(eng, list(seqs))
+    assert sorted(q.seq_id for q in out) == list(range(64))
+    lens = [q.num_tokens for q in out]
+    srt = sorted(lens, reverse=True)
+    assert lens[:32] == srt[:32] and lens[32:] == srt[32:][::-1]
+    for z in range(32):  # the pair on one CU: k-th longest with k-th shortest
+        assert lens[z] == srt[z] and lens[z + 32] == srt[63 - z]
+    eng.runner.bucket_for = lambda n: 32
+    out = LLMEngine._attention_row_order(eng, list(seqs[:20]))
+    assert [q.num_tokens for q in out] == sorted((q.num_tokens for q in seqs[:20]), reverse=True)
