@@ -53,17 +53,34 @@ for name, od in orders.items():
     lens = torch.tensor([lens_list[i] for i in od], dtype=torch.int32)
     inputs[name] = (bt.to(DEV), lens.to(DEV))
 
+# the engine's fused form (qkv split-K slab reduce + RoPE + cache write of the new token in the
+# prologue): 2 slabs, positions = context - 1, no cache write (slot -1)
+ncol = (hq + 2 * hkv) * d
+slabs = torch.randn(2 * B * ncol, device=DEV, dtype=torch.float32)
+cs = torch.randn(maxlen, d, device=DEV, dtype=torch.float32)
+slots = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+fused_inputs = {k + "_fused": v for k, v in inputs.items() if k in ("random", "paired")}
+
+
+def run(name, bt, lens):
+    if name.endswith("_fused"):
+        ops.paged_decode_fused(slabs, 2, lens - 1, cs, slots, kc, vc, bt, lens, hq, hkv, d, 1 / math.sqrt(d),
+                               workspace=ws, out=out, splits=1)
+    else:
+        ops.paged_decode(q, kc, vc, bt, lens, hq, hkv, d, 1 / math.sqrt(d), workspace=ws, out=out, splits=1)
+
+
 res = {}
 for rnd in range(6):
-    for name, (bt, lens) in inputs.items():
+    for name, (bt, lens) in {**inputs, **fused_inputs}.items():
         for _ in range(3):
-            ops.paged_decode(q, kc, vc, bt, lens, hq, hkv, d, 1 / math.sqrt(d), workspace=ws, out=out, splits=1)
+            run(name, bt, lens)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
         e0.record()
         n = 30
         for _ in range(n):
-            ops.paged_decode(q, kc, vc, bt, lens, hq, hkv, d, 1 / math.sqrt(d), workspace=ws, out=out, splits=1)
+            run(name, bt, lens)
         e1.record()
         torch.cuda.synchronize()
         res.setdefault(name, []).append(e0.elapsed_time(e1) / n * 1e3)
