@@ -214,7 +214,7 @@ class CausalLM:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
         for L in self.layers:
             for k, v in L.items():
-                if k.endswith("_p"):  # decode-layout copies (_init_skinny) are not extra parameters
+                if k.endswith(("_p", "_d", "_pg")):  # decode-layout copies (_init_skinny) are not parameters
                     continue
                 if isinstance(v, tuple):
                     n += sum(t.numel() for t in v)
@@ -251,7 +251,7 @@ class CausalLM:
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
         if slabs is not None:
             ws, splits = slabs
-            ns = ops.skinny_slabs(x, L["wqkv_p"], ws, splits, rows=T, rownorm=rownorm)
+            ns = self._proj_slabs(L, "wqkv", x, T, splits, rownorm)
             if self._attn_rope and not meta.is_prefill and k_cache is not None and c.arch == "llama":
                 # the attention kernel reduces the slabs, applies RoPE and writes the new k / v
                 out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device)
@@ -259,7 +259,7 @@ class CausalLM:
                                               meta.block_tables, meta.seq_lens, self.hq, self.hkv, self.D, self.scale,
                                               workspace=meta.decode_ws, out=out)
             partial = ws
-            qkv = torch.empty(T, ops.skinny_wdims(L["wqkv_p"])[0], dtype=self.dtype, device=self.device)
+            qkv = torch.empty(T, L["wqkv"].shape[0], dtype=self.dtype, device=self.device)
         elif "bqkv" in L:
             qkv = F.linear(x, L["wqkv"], L["bqkv"])
         else:
@@ -516,8 +516,20 @@ class CausalLM:
                     x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
         return self._logits(x)
 
-    def _logits(self, x: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(x, self.lm_head)
+    def _logits(self, x: torch.Tensor, rows: Optional[int] = None) -> torch.Tensor:
+        """LM head (+ the TP all-gather of the vocab shards).  ``x``: the final-normed rows,
+        row-major, or fragment-packed with ``rows`` valid rows (decode).  With a decode copy of the
+        head (``lm_head_d``) up to 64 rows at a time go through gemm_decode.hip - the decode step's
+        and a prefill step's last-token logits alike; hipBLASLt otherwise."""
+        hd = self.lm_head_d
+        if x.dim() == 4:  # packed (decode): the decode copy exists by construction
+            logits = torch.empty(rows, hd.shape[0] * 16, dtype=self.dtype, device=self.device)
+            ops.dec_gemm(x, hd, 1, rows, out=logits)
+        elif hd is not None and x.is_cuda and x.shape[0] <= ops.SKINNY_MAX_M:
+            logits = torch.empty(x.shape[0], hd.shape[0] * 16, dtype=self.dtype, device=self.device)
+            ops.dec_gemm(ops.pack_activation(x), hd, 1, x.shape[0], out=logits)
+        else:
+            logits = F.linear(x, self.lm_head)
         logits = tp_all_gather_last(logits, self.ps)
         if self.vocab_padded != self.cfg.vocab_size:
             logits = logits[:, : self.cfg.vocab_size]
@@ -552,6 +564,10 @@ class CausalLM:
         On the CPU the same ops run as fp32 references with the kernels' split-K slicing, so the
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
+        self.lm_head_d = None
+        for L in self.layers:  # (re)built below from the current weights
+            for key in ("wqkv_d", "wo_d", "w13_d", "w2_d"):
+                L.pop(key, None)
         c = self.cfg
         ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
         if not getattr(self, "_w13_il", False) and c.arch == "llama" and ff % 64 == 0:
@@ -591,9 +607,12 @@ class CausalLM:
         env = os.environ.get("K8SLLM_SKINNY_SPLITS")
         split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split
+        self._init_dec()
 
         def most(N: int, K: int) -> int:
-            return split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
+            s_rm = split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
+            cfg = ops.dec_config(N, K, 0) if self.layers and any(k.endswith("_d") for k in self.layers[0]) else None
+            return max(s_rm, cfg[0] if cfg else 1)
 
         n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d,
                 (self.e_hi - self.e_lo) * ops.skinny_nslabs(ff, 1) * d if c.is_moe else most(d, ff) * d)
@@ -612,7 +631,7 @@ class CausalLM:
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
-            ns = ops.skinny_slabs(op, L["wo_p"], ws, self._split_o, rows=M)
+            ns = self._proj_slabs(L, "wo", op, M, self._split_o)
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
                 # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated
                 # MLP output comes back from _moe_a2a_decode
@@ -631,20 +650,29 @@ class CausalLM:
                 ns = self._moe_skinny(L, residual, ws, ns, M)
             else:
                 xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
-                act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
-                ns = ops.skinny_slabs(act, L["w2_p"], ws, self._split_d, rows=M)
+                if "w13_d" in L:
+                    act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
+                    ops.dec_gemm(xw, L["w13_d"], 2, M, out=act, rownorm=rn)
+                else:
+                    act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
+                ns = self._proj_slabs(L, "w2", act, M, self._split_d)
             if i + 1 < n:
                 xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
-        # final norm feeds the LM head (hipBLASLt): complete, row-major
-        x = self._tp_tail(ws, ns, residual, self.final_norm, packed=False)
-        if x is not None:
-            return self._logits(x)
-        x = self._row_parallel_sum(ws, ns, M, residual)
+        # final norm feeds the LM head: fragment-packed for the decode GEMM (gemm_decode.hip), or
+        # complete and row-major for hipBLASLt where no decode copy of the head exists
+        packed = self.lm_head_d is not None
+        x = self._tp_tail(ws, ns, residual, self.final_norm, packed=packed)
         if x is None:
-            x = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, self.final_norm, eps)
-        else:
-            x = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
-        return self._logits(x)
+            y = self._row_parallel_sum(ws, ns, M, residual)
+            if y is None:
+                out = (ops.packed_empty(M, residual.shape[1], residual.dtype, residual.device) if packed
+                       else torch.empty_like(residual))
+                x = ops.reduce_add_rms_norm(out, residual, ws, ns, self.final_norm, eps)
+            else:
+                x = ops.fused_add_rms_norm(y, residual, self.final_norm, eps)
+                if packed:
+                    x = ops.pack_activation(x)
+        return self._logits(x, rows=M)
 
     def _moe_skinny(self, L: dict, residual: torch.Tensor, ws, ns: int, M: int) -> int:
         """MoE decode MLP on the grouped skinny kernels: residual += the o
@@ -666,6 +694,55 @@ class CausalLM:
         wd = torch.zeros(M, c.n_experts, dtype=torch.float32, device=xn.device).scatter_(1, ids.long(), w)
         act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
+
+    def _proj_slabs(self, L: dict, key: str, x: torch.Tensor, rows: int, split: int,
+                    rownorm: Optional[tuple] = None) -> int:
+        """Split-K slabs of a decode projection into the shared workspace: the shared-A decode
+        GEMM over the packed copy ``L[key + "_d"]`` where one exists, else gemm_skinny over
+        ``L[key + "_p"]``.  Returns the slab count."""
+        wd = L.get(key + "_d")
+        if wd is not None:
+            return ops.dec_gemm(x, wd, 0, rows, workspace=self._skinny_ws, rownorm=rownorm)
+        return ops.skinny_slabs(x, L[key + "_p"], self._skinny_ws, split, rows=rows, rownorm=rownorm)
+
+    def _want_dec(self) -> bool:
+        """Decode-only fragment-packed weight copies for gemm_decode.hip (``K8SLLM_DECODE_GEMM`` =
+        auto | dec | rm).  auto: dense Llama whose weights take at most a quarter of the device
+        (Llama-3-8B: 16 GB of 288; 70B at TP=1 keeps the single row-major copy and gemm_skinny)."""
+        mode = os.environ.get("K8SLLM_DECODE_GEMM", "auto")
+        if mode in ("rm", "0", "off") or self.cfg.arch != "llama":
+            return False
+        if mode in ("dec", "1", "on"):
+            return True
+        if self.cfg.is_moe:
+            return False
+        if self.device.type != "cuda":
+            return True
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        return self.num_local_params() * 2 * 2 <= total // 2
+
+    def _init_dec(self) -> None:
+        """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
+        launch configuration for its shape (ops.dec_config): wqkv_d / wo_d / w2_d
+        ([N/16, K/32, 64, 8]), w13_d (gate/up interleaved per 16 rows as [8 gate | 8 up]), and the
+        LM head.  Prefill keeps reading the row-major tensors."""
+        self.lm_head_d = None
+        if not self._want_dec():
+            return
+        c = self.cfg
+        for L in self.layers:
+            for key in ("wqkv", "wo", "w2"):
+                N, K = L[key].shape
+                if ops.dec_available(N, K, 0):
+                    L[key + "_d"] = ops.pack_skinny(L[key])
+            if not c.is_moe:
+                w = ops.deinterleave_gate_up(L["w13"]) if self._w13_il else L["w13"]
+                if ops.dec_available(w.shape[0], w.shape[1], 2):
+                    L["w13_d"] = ops.pack_skinny(ops.interleave_gate_up8(w))
+                del w
+        N, K = self.lm_head.shape
+        if N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
+            self.lm_head_d = ops.pack_skinny(self.lm_head)
 
     def _tp_tail(self, ws, ns: int, residual: torch.Tensor, norm_w, packed: bool) -> Optional[torch.Tensor]:
         """TP>1 on the GPU with the IPC all-reduce: the row-parallel tail (slab sum, all-reduce,

@@ -313,6 +313,114 @@ def skinny_grouped_slabs(act: torch.Tensor, wp2: torch.Tensor, workspace: torch.
                                         skinny_waves())
 
 
+# ---------------------------------------------------------------- decode GEMM, shared-A design (gemm_decode.hip)
+
+def interleave_gate_up8(w13: torch.Tensor) -> torch.Tensor:
+    """[gate (F rows); up (F rows)] -> per 16-row n-tile [8 gate | 8 up] rows: the DEC_SWIGLU8
+    epilogue finds a feature's gate and up in lanes l and l ^ 8 of one accumulator."""
+    F2, K = w13.shape
+    F = F2 // 2
+    if F % 8:
+        raise ValueError("interleave_gate_up8: F must be a multiple of 8")
+    return w13.reshape(2, F // 8, 8, K).permute(1, 0, 2, 3).reshape(F2, K)
+
+
+def deinterleave_gate_up8(w: torch.Tensor) -> torch.Tensor:
+    F2, K = w.shape
+    return w.reshape(F2 // 16, 2, 8, K).permute(1, 0, 2, 3).reshape(F2, K)
+
+
+# (splits, n-tiles per wave, waves, weight ring depth) per decode projection shape (N, K) at
+# M <= 64: ~256 equal workgroups (measured: tools/bench_decode_gemm.py,
+# profiles/r04/decode_gemm_sweep.jsonl).  Shapes not listed get an automatic pick.
+DEC_TABLE: dict = {
+    # Llama-3-8B at TP=1 (profiles/r04/decode_gemm_sweep_v1.jsonl, M = 64 / M = 1 us):
+    (6144, 4096, 0): (4, 1, 8, 8),      # qkv      13.2 / 10.3   (row-major skinny 13.4 / 10.4)
+    (4096, 4096, 0): (8, 1, 8, 8),      # o         9.6 / 7.5    (10.2 / 7.5)
+    (28672, 4096, 2): (1, 1, 7, 8),     # gate_up  39.9 / 38.1   (47.9 / 40.0)
+    (4096, 14336, 0): (8, 1, 8, 8),     # down     22.3 / 19.0   (24.3 / 19.9)
+    (128256, 4096, 1): (1, 4, 8, 4),    # LM head 173.8 / 166.0  (hipBLASLt 202.2 / 176.2)
+}
+
+
+def dec_config(N: int, K: int, epi: int) -> Optional[tuple]:
+    """Launch configuration of gemm_dec for a weight [N, K]: (splits, ntw, waves, depth) or None
+    when no configuration tiles the shape (the caller keeps gemm_skinny).  ``K8SLLM_DEC_CFG`` =
+    "S,NTW,WAVES,DEPTH" forces one (tools)."""
+    env = os.environ.get("K8SLLM_DEC_CFG")
+    if env:
+        return tuple(int(v) for v in env.split(","))
+    hit = DEC_TABLE.get((N, K, epi))
+    if hit is not None:
+        return hit
+    ntiles, ksteps = N // 16, K // 32
+    cands = ([(1, 1, 7, 8), (1, 1, 7, 16), (1, 1, 8, 16), (1, 2, 4, 8)] if epi == 2 else
+             [(1, 4, 8, 4), (1, 3, 8, 8), (1, 2, 8, 8), (1, 4, 4, 8)] if epi == 1 else
+             [(s, ntw, w, d) for s in (1, 2, 4, 8, 16) for (ntw, w, d) in
+              ((1, 8, 8), (1, 4, 16), (1, 4, 8), (2, 4, 8), (2, 8, 8), (3, 4, 8), (3, 8, 8), (4, 4, 8),
+                               (4, 4, 4))])
+    best = None
+    for s, ntw, w, d in cands:
+        it = max(d, 8)
+        if (epi == 0 and ntiles % (ntw * w)) or K % s or (ksteps // s) % it or ksteps % s:
+            continue
+        wgs = -(-ntiles // (ntw * w)) * s
+        # ~256 workgroups; for split-K slabs 8-wave workgroups of one n-tile per wave were the
+        # fastest within 64 workgroups of that (the sweep), then fewer K splits (slab traffic)
+        far = abs(wgs - 256) if wgs <= 512 else 10_000 + wgs
+        key = ((far > 64, -w, far, s) if epi == 0 else (far, s))
+        if best is None or key < best[0]:
+            best = (key, (s, ntw, w, d))
+    return best[1] if best else None
+
+
+def dec_available(N: int, K: int, epi: int) -> bool:
+    return dec_config(N, K, epi) is not None
+
+
+def dec_gemm(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None, rownorm: Optional[tuple] = None,
+             cfg: Optional[tuple] = None) -> int:
+    """gemm_dec over a fragment-packed activation ``a`` and packed weight ``wp`` (decode-only copy).
+    epi 0: fp32 split-K slabs into ``workspace`` [S, M, N], returns S; epi 1: ``out`` [M, N] bf16;
+    epi 2: ``out`` packed SwiGLU [ceil(M/16), F/32, 64, 8] over an interleave_gate_up8 weight.
+    ``rownorm = (ss_part, eps)``: deferred RMSNorm of the A rows (add_norm_partial).  CPU: the fp32
+    reference with the same split-K slicing."""
+    N, K = skinny_wdims(wp)
+    M = rows
+    if cfg is None:
+        cfg = dec_config(N, K, epi)
+    if cfg is None:
+        raise ValueError(f"gemm_dec: no configuration for N={N} K={K} epi={epi}")
+    S, ntw, waves, depth = cfg
+    if not _gpu(a):
+        x = _cpu_a(a, rows).float()
+        w = _cpu_w(wp)
+        sc = _rn_scale(rownorm, M, K)
+        if epi == 0:
+            kc = K // S
+            slabs = workspace[: S * M * N].view(S, M, N)
+            for s in range(S):
+                y = x[:, s * kc:(s + 1) * kc] @ w[:, s * kc:(s + 1) * kc].t()
+                slabs[s] = y * sc if sc is not None else y
+            return S
+        y = x @ w.t()
+        if sc is not None:
+            y = y * sc
+        if epi == 1:
+            out[:M].copy_(y.to(out.dtype))
+            return 1
+        gu = deinterleave_gate_up8(y.to(a.dtype).float().t()).t()
+        g, u = gu[:, : N // 2], gu[:, N // 2:]
+        out.copy_(pack_activation((torch.nn.functional.silu(g) * u).to(a.dtype)))
+        return 1
+    rn = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
+    r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn)
+    if r < 0:
+        raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
+    return r
+
+
 def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int, norm_w: torch.Tensor,
                      out: Optional[torch.Tensor] = None, ss_part: Optional[torch.Tensor] = None,
                      packed: bool = True) -> tuple:

@@ -48,6 +48,9 @@ int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, 
                        float rn_eps, int waves, int experts, long w_es, long a_es, long y_es,
                        const float* row_w, int row_w_ld, int w_rm, hipStream_t s);
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
+int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K, int splits,
+                    int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc, int rn_d, float rn_eps,
+                    hipStream_t s);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
@@ -489,6 +492,54 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
   return S;
 }
 
+// Decode GEMM over a fragment-packed weight copy with A shared through LDS (gemm_decode.hip):
+// a packed [ceil(M/16), K/32, 64, 8] (`rows` valid), wp packed [N/16, K/32, 64, 8] (for epi 2 the
+// rows interleaved per 16-row n-tile as [8 gate | 8 up]).  epi 0: fp32 slabs partial[S][M][N],
+// returns S = splits; epi 1: y [M, N] bf16 (row stride y.stride(0)); epi 2: packed SwiGLU
+// y [ceil(M/16), N/64, 64, 8].  Returns the slab count (1 for epi 1/2); -1 if the configuration
+// is not available (the caller falls back to gemm_skinny).
+int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial, c10::optional<torch::Tensor> y,
+                 int64_t splits, int64_t epi, int64_t ntw, int64_t waves, int64_t depth, int64_t rows,
+                 c10::optional<torch::Tensor> rn_ss, double rn_eps) {
+  dev_bf16(a, "a"); dev_bf16(wp, "wp");
+  TORCH_CHECK(wp.dim() == 4 && wp.is_contiguous() && wp.size(2) == 64 && wp.size(3) == 8,
+              "gemm_dec: wp must be fragment-packed [N/16, K/32, 64, 8]");
+  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32, M = (int)rows;
+  TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(1) * 32 == K && a.size(2) == 64 && a.size(3) == 8,
+              "gemm_dec: a must be fragment-packed [ceil(M/16), K/32, 64, 8]");
+  TORCH_CHECK(M > 0 && M <= 64 && (M + 15) / 16 <= a.size(0), "gemm_dec: 1..64 rows within the packed a");
+  float* pp = nullptr;
+  void* yp = nullptr;
+  long ldy = 0;
+  if (epi == 0) {
+    TORCH_CHECK(partial.has_value() && partial->is_cuda() && partial->scalar_type() == torch::kFloat32 &&
+                    partial->is_contiguous() && partial->numel() >= splits * M * N,
+                "gemm_dec: partial must be contiguous fp32 with splits x M x N elements");
+    pp = partial->data_ptr<float>();
+  } else {
+    TORCH_CHECK(splits == 1, "gemm_dec: bf16 / SwiGLU epilogues need splits == 1");
+    TORCH_CHECK(y.has_value(), "gemm_dec: output tensor required");
+    dev_bf16(*y, "y");
+    if (epi == 2) {
+      TORCH_CHECK(y->dim() == 4 && y->is_contiguous() && y->size(0) == (M + 15) / 16 && y->size(1) * 64 == N &&
+                      y->size(2) == 64 && y->size(3) == 8,
+                  "gemm_dec: packed SwiGLU output must be [ceil(M/16), N/64, 64, 8]");
+    } else {
+      TORCH_CHECK(y->dim() == 2 && y->size(0) >= M && y->size(1) == N && y->stride(1) == 1, "gemm_dec: y [M, N]");
+      ldy = y->stride(0);
+    }
+    yp = y->data_ptr();
+  }
+  const float* rp = nullptr;
+  int rn_nc = 0;
+  rownorm_args(rn_ss, M, K, rp, rn_nc);
+  const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, ldy, M, N, K, (int)splits, (int)epi, (int)ntw,
+                                 (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, cur());
+  if (rc < 0) return -1;
+  check(rc, "gemm_dec");
+  return epi == 0 ? splits : 1;
+}
+
 // Grouped (MoE) skinny GEMM: wp [E, N/16, K/32, 64, 8] (one packed weight per local expert).
 // a: packed [MT, K/32, 64, 8] shared by every expert, or [E, MT, K/32, 64, 8] per expert.
 // epi 3: y = packed SwiGLU [E, MT, F/32, 64, 8]; epi 0: fp32 slabs partial[E * S'][M][N] with
@@ -702,6 +753,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
+  m.def("gemm_dec", &gemm_dec);
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);

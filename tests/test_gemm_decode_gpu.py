@@ -1,0 +1,99 @@
+"""The shared-A decode GEMM (gemm_decode.hip: packed weight streamed into registers, A staged in LDS
+once per workgroup and shared by waves that split the columns) against an fp32 reference of the
+same product, for every epilogue the decode path uses (split-K slabs, bf16 LM head, packed SwiGLU
+over the [8 gate | 8 up] weight), with and without the deferred RMSNorm row scale, at Llama-3-8B
+projection shapes and at every row count class (1 m-tile .. 4 m-tiles, ragged)."""
+import pytest
+import torch
+
+from k8s_llm_monitor_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+F_ = torch.nn.functional
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    ops.native()
+    torch.manual_seed(0)
+
+
+def _check(y, ref, what, tol=2.5e-2):
+    err = (y.float() - ref.float()).abs().max().item()
+    scale = ref.float().abs().max().item()
+    assert err <= tol * scale + 1e-3, f"{what}: max err {err:.4g} vs scale {scale:.4g}"
+
+
+def _w(N, K, s=0.02):
+    return (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * s).to(torch.bfloat16)
+
+
+CASES = [  # (N, K, cfg)  - the engine's picks plus ragged / edge configurations
+    (6144, 4096, (8, 3, 4, 8)),
+    (4096, 4096, (8, 1, 8, 8)),
+    (4096, 4096, (4, 1, 4, 16)),
+    (4096, 14336, (8, 2, 4, 8)),
+    (4096, 14336, (4, 1, 4, 16)),
+    (1024, 512, (2, 2, 8, 8)),
+    (384, 1024, (1, 4, 4, 8)),  # 24 n-tiles, 16 per workgroup: the second workgroup is ragged
+]
+
+
+@pytest.mark.parametrize("M", [1, 17, 40, 64])
+@pytest.mark.parametrize("N,K,cfg", CASES)
+def test_dec_slabs_match_fp32(M, N, K, cfg):
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = _w(N, K)
+    ws = torch.empty(cfg[0] * M * N, device=DEV, dtype=torch.float32)
+    s = ops.dec_gemm(ops.pack_activation(x), ops.pack_skinny(w), 0, M, workspace=ws, cfg=cfg)
+    assert s == cfg[0]
+    y = ws[: s * M * N].view(s, M, N).sum(0)
+    _check(y, x.float() @ w.float().t(), f"slabs M{M} N{N} K{K} cfg{cfg}")
+    # every slab is the product over its own K slice
+    kc = K // s
+    last = x[:, (s - 1) * kc:].float() @ w[:, (s - 1) * kc:].float().t()
+    _check(ws[(s - 1) * M * N: s * M * N].view(M, N), last, "last slab")
+
+
+@pytest.mark.parametrize("M", [1, 33, 64])
+def test_dec_rownorm_scale(M):
+    """Deferred RMSNorm: A holds x * w; outputs scaled by 1/rms from add_norm_partial's sums."""
+    N, K = 4096, 4096
+    res = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    nw = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w = _w(N, K)
+    xw, ss = ops.add_norm_partial(res.clone(), None, 0, nw)
+    ws = torch.empty(8 * M * N, device=DEV, dtype=torch.float32)
+    s = ops.dec_gemm(xw, ops.pack_skinny(w), 0, M, workspace=ws, rownorm=(ss, 1e-5), cfg=(8, 1, 8, 8))
+    y = ws[: s * M * N].view(s, M, N).sum(0)
+    xn = F_.rms_norm(res.float(), (K,), nw.float(), 1e-5)
+    _check(y, xn @ w.float().t(), f"rownorm M{M}", tol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 20, 64])
+@pytest.mark.parametrize("cfg", [(1, 1, 7, 16), (1, 1, 8, 16), (1, 2, 4, 8), (1, 1, 7, 8)])
+def test_dec_swiglu8_feeds_down(M, cfg):
+    K, F = 4096, 14336
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    wg, wu = _w(F, K), _w(F, K)
+    act = ops.packed_empty(M, F, torch.bfloat16, DEV)
+    ops.dec_gemm(ops.pack_activation(x), ops.pack_skinny(ops.interleave_gate_up8(torch.cat([wg, wu]))), 2, M,
+                 out=act, cfg=cfg)
+    g = (x.float() @ wg.float().t()).to(torch.bfloat16).float()
+    u = (x.float() @ wu.float().t()).to(torch.bfloat16).float()
+    _check(ops.unpack_skinny(act)[:M], F_.silu(g) * u, f"swiglu8 M{M} cfg{cfg}")
+
+
+@pytest.mark.parametrize("M", [1, 64])
+@pytest.mark.parametrize("cfg", [(1, 4, 8, 4), (1, 3, 8, 8)])
+def test_dec_bf16_lm_head(M, cfg):
+    """LM-head shape: N = 128256 does not divide the workgroup tile - the last workgroup is ragged."""
+    N, K = 128256, 4096
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = _w(N, K)
+    y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.dec_gemm(ops.pack_activation(x), ops.pack_skinny(w), 1, M, out=y, cfg=cfg)
+    ref = x.float() @ w.float().t()
+    _check(y, ref, f"lm_head M{M} cfg{cfg}")
+    assert not torch.isnan(y).any(), "every column written (the ragged last workgroup included)"
