@@ -127,6 +127,9 @@ class LLMEngine:
         self._pf_step_id = 0
         self.trace: Optional[list] = [] if os.environ.get("K8SLLM_TRACE") else None  # (t, kind, n, tokens)
         self._inflight_rows: dict = {}
+        # (rows, GPU ms) of decode steps that ran back to back, measured by events (the admission
+        # model's samples: no host time, keyed by the step that actually ran)
+        self.step_samples: deque = deque(maxlen=256)
         # TP: the step bus to the workers (shared-memory ring, parallel/step_bus.py) - collective
         self.bus = make_step_bus(self.ps, bus_slot_bytes(cfg.max_num_seqs, self.runner.max_len,
                                                          self.runner.max_blocks_per_seq)) if self.ps.tp_size > 1 else None
@@ -307,6 +310,9 @@ class LLMEngine:
     def _resolve_step(self, seqs: list, handle) -> list[Sequence]:
         toks = self.runner.decode_collect(handle)
         self._check_collectives()
+        ms = handle.gpu_ms() if hasattr(handle, "gpu_ms") else None
+        if ms is not None:  # a back-to-back decode step: its GPU time at this row count
+            self.step_samples.append((len(seqs), ms))
         now = time.perf_counter()
         done = []
         for q, tok in zip(seqs, toks):
@@ -527,6 +533,30 @@ _ROW_ORDER = os.environ.get("K8SLLM_DECODE_ROW_ORDER", "1") != "0"
 _CUS_PER_XCD = 32  # MI355X: 256 CUs in 8 XCDs
 
 
+class AnswerLengths:
+    """Observed answer lengths (generated tokens) of requests that stop on EOS / stop tokens or at
+    their max_tokens, for the deadline admission: an answer that may stop early is budgeted at the
+    ``q``-quantile of recent answers instead of its max_tokens (requests with ``ignore_eos``
+    always run to max_tokens and are budgeted so)."""
+
+    def __init__(self, keep: int = 512, min_samples: int = 16, q: float = 0.9):
+        self.lens: deque = deque(maxlen=keep)
+        self.min_samples, self.q = min_samples, q
+        self._cached: Optional[int] = None
+
+    def record(self, n: int) -> None:
+        self.lens.append(int(n))
+        self._cached = None
+
+    def quantile(self) -> Optional[int]:
+        if len(self.lens) < self.min_samples:
+            return None
+        if self._cached is None:
+            xs = sorted(self.lens)
+            self._cached = xs[min(len(xs) - 1, int(len(xs) * self.q))]
+        return self._cached
+
+
 class EngineOverloaded(RuntimeError):
     """Admission refused: the queue is full or the request cannot start within its deadline
     (the HTTP layer answers 503 - SURVEY.md §5 failure detection: reject, never crash or hang)."""
@@ -548,8 +578,11 @@ class EngineService:
       "deadline" (a truncated answer, KV freed), and a request still waiting when its deadline
       passes is dropped with EngineOverloaded;
     * deadline-feasible admission - a waiting request with a deadline starts only when the learned
-      decode step time at the batch it would join (TpotModel) x its max_tokens, plus its prefill,
-      fits its deadline AND every running request's remaining tokens still fit theirs; a request
+      decode step time at the batch it would join (TpotModel, fed by GPU-event step times) x its
+      expected answer length (max_tokens with ignore_eos, else at most the observed 90th-percentile
+      answer length: AnswerLengths), plus its prefill, fits its deadline AND every running
+      request's expected remaining tokens still fit theirs (a preempted sequence resumes without
+      the gate; a request without a deadline is not held back by the running ones); a request
       that cannot finish in time even once the first running answer completes is refused at once
       (EngineOverloaded -> 503) instead of being truncated later (reference budget:
       cmd/server/main.go:147-148 15 s write timeout, internal/config/config.go:145 llm.timeout);
@@ -582,8 +615,11 @@ class EngineService:
         self._prefill_tps: Optional[float] = None
         self._waiting_est = 0  # prompt tokens waiting in the scheduler (engine thread writes)
         self.tpot = TpotModel()
+        self.answer_lens = AnswerLengths()
+        self._step_cache: dict = {}  # per-step memo of the running set's deadline slack
         self.deadline_margin = 1.05  # safety factor on the estimated completion time
         self.infeasible = 0  # refused because the answer could not finish before its deadline
+        self._gpu_tpot = False  # step times come from GPU events (ModelRunner._chain_event)
         engine.sched.admit_gate = self._admit_ok
         self._thread.start()
 
@@ -657,23 +693,50 @@ class EngineService:
     def _prefill_s(self, seq: Sequence) -> float:
         return (seq.num_tokens / self._prefill_tps) if self._prefill_tps else 0.0
 
+    def _expected_rem(self, seq: Sequence) -> int:
+        """Tokens ``seq`` is expected to still generate: its max_tokens minus what it already has
+        (a preempted sequence keeps its answer so far), or - when it may stop on EOS - at most the
+        observed 90th-percentile answer length (AnswerLengths) minus that."""
+        gen = sum(1 for t in seq.output_ids if t >= 0)
+        rem = max(0, seq.params.max_tokens - gen)
+        if seq.params.ignore_eos:
+            return rem
+        q = self.answer_lens.quantile()
+        if q is None:
+            return rem
+        return min(rem, max(q - gen, 32))
+
+    def _running_slack(self, n_after: int, step_s: float, now: float) -> float:
+        """Smallest (deadline - expected finish) over the running requests that have a deadline,
+        at ``step_s`` per step; memoised per engine step (the gate and the infeasibility sweep of
+        every waiting request reuse it)."""
+        key = ("slack", n_after)
+        v = self._step_cache.get(key)
+        if v is None:
+            v = min((q.deadline - now - self._expected_rem(q) * step_s for q in self.engine.sched.running
+                     if q.deadline is not None), default=float("inf"))
+            self._step_cache[key] = v
+        return v
+
     def _admit_ok(self, seq: Sequence, n_after: int) -> bool:
         """Scheduler admission gate (engine thread): does ``seq`` finish before its deadline at the
-        batch it would join, without pushing a running request past its own deadline?"""
+        batch it would join, without pushing a running request past its own deadline?
+        A preempted sequence (it already has answer tokens) resumes without the gate: it was
+        admitted once, and refusing it would freeze admission behind it until its deadline.  A
+        request without a deadline is not held back by the running requests' deadlines."""
+        if seq.output_ids:
+            return True
+        if seq.deadline is None:
+            return True
         t = self.tpot.estimate(n_after)
         if t is None:
             return True
         now = time.perf_counter()
         step_s = t * 1e-3 * self.deadline_margin
         pre = self._prefill_s(seq)
-        if seq.deadline is not None and now + pre + seq.params.max_tokens * step_s > seq.deadline:
+        if now + pre + self._expected_rem(seq) * step_s > seq.deadline:
             return False
-        for q in self.engine.sched.running:
-            if q.deadline is not None:
-                rem = max(0, q.params.max_tokens - len(q.output_ids))
-                if now + pre + rem * step_s > q.deadline:
-                    return False
-        return True
+        return pre <= self._running_slack(n_after, step_s, now)
 
     def _infeasible(self, seq: Sequence, now: float) -> bool:
         """A never-started request that cannot finish before its deadline even if it starts when
@@ -685,9 +748,12 @@ class EngineService:
         step_s = t * 1e-3 * self.deadline_margin
         wait = 0.0
         if not self._admit_ok(seq, len(running) + 1):
-            rem = [max(0, q.params.max_tokens - len(q.output_ids)) for q in running]
-            wait = min(rem) * step_s if rem else 0.0
-        return now + wait + self._prefill_s(seq) + seq.params.max_tokens * step_s > seq.deadline
+            key = ("minrem",)
+            m = self._step_cache.get(key)
+            if m is None:
+                m = self._step_cache[key] = min((self._expected_rem(q) for q in running), default=0)
+            wait = m * step_s
+        return now + wait + self._prefill_s(seq) + self._expected_rem(seq) * step_s > seq.deadline
 
     def _expire_waiting(self) -> None:
         """Waiting requests whose deadline has passed: one that never started is dropped
@@ -781,6 +847,10 @@ class EngineService:
         if not self._cancels.empty():
             self._apply_cancels()
         self._drain(block=not eng.has_work())
+        self._step_cache.clear()
+        while eng.step_samples:  # GPU-event step times (back-to-back decode steps)
+            self.tpot.record(*eng.step_samples.popleft())
+            self._gpu_tpot = True
         if eng.sched.waiting:
             self._expire_waiting()
         self._waiting_est = self._waiting_tokens()
@@ -791,9 +861,10 @@ class EngineService:
         paced = eng._inflight is not None or not eng.cfg.pipeline  # this step waits for a GPU step
         ptok0 = eng.runner.n_steps.get("prefill_tokens", 0)
         finished = eng.step()
-        if paced and eng.counters["decode_steps"] > d0 and eng.counters["prefill_steps"] == p0:
-            # decode-only step: with pipelining, launching step N waits for step N-1, so the
-            # interval is one GPU step at (about) this batch size
+        if (paced and not self._gpu_tpot and eng.counters["decode_steps"] > d0
+                and eng.counters["prefill_steps"] == p0):
+            # (CPU / until event samples arrive) decode-only step: with pipelining, launching
+            # step N waits for step N-1, so the interval is one GPU step at (about) this batch size
             rows = eng._inflight[0] if eng._inflight is not None else eng.sched.running
             self.tpot.record(len(rows), (time.perf_counter() - t0) * 1e3)
         if eng.counters["prefill_steps"] > p0:
@@ -805,6 +876,8 @@ class EngineService:
         if self._streams:
             self._push_streams()
         for seq in finished:
+            if not seq.params.ignore_eos and seq.finish_reason in ("stop", "length"):
+                self.answer_lens.record(sum(1 for t in seq.output_ids if t >= 0))
             fut = seq.user
             if isinstance(fut, Future) and not fut.done():
                 self.latencies_ms.append(seq.timings()["latency_ms"])

@@ -94,6 +94,7 @@ class ModelRunner:
         self.graph_pool = None
         self.n_steps = {"prefill": 0, "decode": 0}
         self.on_launched = None  # hook after every step's launch (TP: enqueue the custom-AR error readback)
+        self._last_ev = None  # end event of the last launched step (_chain_event)
 
     # --------------------------------------------------------------------- helpers
     def bucket_for(self, n: int) -> int:
@@ -222,8 +223,7 @@ class ModelRunner:
             self._pf_out[j] = torch.empty(max(R, 2 * self.B), dtype=torch.int32, pin_memory=True)
         out = self._pf_out[j]
         out[:R].copy_(tok[:R], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        ev, _ = self._chain_event()
         return DecodeHandle(R, ev, out)
 
     # --------------------------------------------------------------------- decode
@@ -338,9 +338,21 @@ class ModelRunner:
         h = self.h_out[self._out_i]
         self._out_i ^= 1
         h[:n].copy_(self.d_out[:n], non_blocking=True)
-        ev = torch.cuda.Event()
+        ev, prev = self._chain_event()
+        return DecodeHandle(n, ev, h, prev)
+
+    def _chain_event(self) -> tuple:
+        """Record the end-of-step event (timing-enabled) and return it with the previous launched
+        step's event IF that step was still running when this one was enqueued: the GPU then went
+        from one step straight into the next, so the elapsed time between the two events is this
+        step's GPU time (no host stall inside it) - the decode step-time samples of the admission
+        model (EngineService.tpot).  Otherwise the previous event is dropped (None)."""
+        prev = self._last_ev
+        busy = prev is not None and not prev.query()
+        ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        return DecodeHandle(n, ev, h)
+        self._last_ev = ev
+        return ev, (prev if busy else None)
 
     @staticmethod
     def decode_collect(handle: "DecodeHandle") -> list[int]:
@@ -410,6 +422,13 @@ class DecodeHandle:
     n: int
     event: object  # torch.cuda.Event, None on the CPU
     out: object  # pinned host tensor (GPU) or the token list (CPU)
+    prev_event: object = None  # the back-to-back predecessor's end event (ModelRunner._chain_event)
+
+    def gpu_ms(self) -> Optional[float]:
+        """This step's GPU time (after the event completed), or None when not measurable."""
+        if self.prev_event is None or self.event is None:
+            return None
+        return float(self.prev_event.elapsed_time(self.event))
 
 
 def kv_blocks_for(cfg_layers: int, hkv: int, D: int, gb: float) -> int:

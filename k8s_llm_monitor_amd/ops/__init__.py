@@ -343,6 +343,16 @@ DEC_TABLE: dict = {
 }
 
 
+def _dec_table_env() -> None:
+    """``K8SLLM_DEC_TABLE`` = "N,K,EPI=S,NTW,WAVES,DEPTH;..." overrides table entries (A/B runs)."""
+    for item in filter(None, os.environ.get("K8SLLM_DEC_TABLE", "").split(";")):
+        shape, cfg = item.split("=")
+        DEC_TABLE[tuple(int(v) for v in shape.split(","))] = tuple(int(v) for v in cfg.split(","))
+
+
+_dec_table_env()
+
+
 def dec_config(N: int, K: int, epi: int) -> Optional[tuple]:
     """Launch configuration of gemm_dec for a weight [N, K]: (splits, ntw, waves, depth) or None
     when no configuration tiles the shape (the caller keeps gemm_skinny).  ``K8SLLM_DEC_CFG`` =

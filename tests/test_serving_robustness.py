@@ -292,3 +292,87 @@ def test_deadline_feasible_admission_refuses_instead_of_truncating():
         assert svc.stats()["infeasible_rejected"] == refused
     finally:
         svc.close()
+
+
+def _frozen_service(max_num_seqs=8):
+    eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=max_num_seqs, max_model_len=512, num_blocks=256,
+                                 use_graphs=False, seed=3, dtype="float32", admit_window_ms=0), device="cpu")
+    svc = EngineService(eng)
+    return eng, svc
+
+
+def test_admission_gate_preempted_sequence_resumes_and_does_not_freeze_admission():
+    """a preempted sequence (answer tokens already generated) re-enters the waiting
+    queue at the front; the gate must let it resume (sized by what is left, not its whole
+    max_tokens) instead of refusing it and freezing every later admission until its deadline."""
+    eng, svc = _frozen_service()
+    try:
+        svc.tpot.record(1, 20.0)
+        svc.tpot.record(8, 160.0)
+        sp = SamplingParams(max_tokens=100, temperature=0.0, ignore_eos=True)
+        s = Sequence(prompt_ids=[5] * 10, params=sp, request_id="p", deadline=time.perf_counter() + 1.0)
+        s.output_ids.extend([7] * 95)  # preempted after 95 tokens
+        assert svc._admit_ok(s, 1)  # 100 x 20 ms would not fit 1 s: the remainder is not even asked
+        assert svc._expected_rem(s) == 5
+        fresh = Sequence(prompt_ids=[5] * 10, params=sp, request_id="f", deadline=time.perf_counter() + 1.0)
+        assert not svc._admit_ok(fresh, 1)  # a fresh 100-token answer does not fit 1 s
+    finally:
+        svc.close()
+
+
+def test_admission_gate_no_deadline_not_held_back_by_running_deadlines():
+    eng, svc = _frozen_service()
+    try:
+        svc.tpot.record(1, 20.0)
+        svc.tpot.record(8, 160.0)
+        sp = SamplingParams(max_tokens=50, temperature=0.0, ignore_eos=True)
+        run = Sequence(prompt_ids=[5] * 10, params=sp, request_id="r", deadline=time.perf_counter() + 1.2)
+        eng.sched.running.append(run)  # 50 steps x ~20-40 ms: the running answer has almost no slack
+        try:
+            svc._prefill_tps = 1.0  # a prefill would take seconds: a deadline-bearing joiner is held
+            timed = Sequence(prompt_ids=[5] * 10, params=sp, request_id="t", deadline=time.perf_counter() + 60)
+            free = Sequence(prompt_ids=[5] * 10, params=sp, request_id="n")
+            assert not svc._admit_ok(timed, 2)
+            assert svc._admit_ok(free, 2)
+        finally:
+            eng.sched.running.remove(run)
+    finally:
+        svc.close()
+
+
+def test_admission_budgets_eos_answers_by_observed_lengths():
+    """answers that may stop on EOS are budgeted at the observed 90th-percentile answer
+    length, not max_tokens: at the product default (max_tokens 2000) a short-answer workload is
+    not refused as 'cannot finish'."""
+    eng, svc = _frozen_service()
+    try:
+        svc.tpot.record(1, 6.0)
+        svc.tpot.record(64, 7.0)
+        eos = SamplingParams(max_tokens=2000, temperature=0.0)
+        fixed = SamplingParams(max_tokens=2000, temperature=0.0, ignore_eos=True)
+        dl = time.perf_counter() + 5.0
+        a = Sequence(prompt_ids=[5] * 10, params=eos, request_id="a", deadline=dl)
+        b = Sequence(prompt_ids=[5] * 10, params=fixed, request_id="b", deadline=dl)
+        assert not svc._admit_ok(a, 8)  # no observations yet: budgeted at max_tokens (14 s > 5 s)
+        for n in [120, 180, 250, 300, 90, 400, 220, 150] * 2:
+            svc.answer_lens.record(n)
+        svc._step_cache.clear()
+        assert svc._expected_rem(a) == 400  # the 90th percentile of the 16 answers
+        assert svc._admit_ok(a, 8)  # ~400 x 7 ms fits 5 s
+        assert not svc._admit_ok(b, 8)  # ignore_eos: always the full 2000 tokens
+    finally:
+        svc.close()
+
+
+def test_tpot_samples_from_engine_events_feed_the_model():
+    eng, svc = _frozen_service()
+    try:
+        eng.step_samples.append((64, 5.9))
+        eng.step_samples.append((64, 6.1))
+        t0 = time.time()
+        while eng.step_samples and time.time() - t0 < 10:  # the engine thread drains them
+            time.sleep(0.01)
+        time.sleep(0.1)
+        assert svc._gpu_tpot and 5.9 <= svc.tpot.estimate(64) <= 6.1
+    finally:
+        svc.close()
