@@ -31,6 +31,7 @@ from ..models.config import ModelConfig, get_config
 from ..models.llama import CausalLM
 from ..parallel.state import ParallelState, get_state
 from ..parallel.step_bus import KIND_DECODE, KIND_PICKLE, KIND_STOP, bus_slot_bytes, decode_message, make_step_bus
+from ..parallel.health import PeerMonitor, gather_identities
 from .block_manager import BlockManager
 from .runner import ModelRunner, RunnerConfig
 from .scheduler import Scheduler, SchedulerConfig
@@ -134,6 +135,11 @@ class LLMEngine:
         self.bus = make_step_bus(self.ps, bus_slot_bytes(cfg.max_num_seqs, self.runner.max_len,
                                                          self.runner.max_blocks_per_seq)) if self.ps.tp_size > 1 else None
         self._publish = self.bus.send_raw if (self.bus is not None and self.is_leader) else None
+        # TP: every rank's (pid, start time, host) - the leader's PeerMonitor watches its workers,
+        # a worker checks it can see its leader (parallel/health.py)
+        self.peer_idents = gather_identities(self.ps) if self.ps.tp_size > 1 else []
+        if self.bus is not None and not self.is_leader:
+            self.bus.set_leader(self.peer_idents[0])
         # custom all-reduce health: its error flag is copied back after every decode launch
         car = self.ps.custom_ar
         self._car_flag = None
@@ -451,8 +457,14 @@ class LLMEngine:
     def worker_loop(self) -> None:
         """Non-leader TP ranks: mirror the leader's steps (step bus) until it sends STOP."""
         pending = None
+        fault_at = int(os.environ.get("K8SLLM_FAULT_EXIT_PREFILL", "0"))  # test hook: die at the N-th prefill
+        n_prefill = 0
         while True:
             kind, payload = decode_message(self.bus.recv())
+            if kind == KIND_PICKLE and fault_at:
+                n_prefill += 1
+                if n_prefill == fault_at:
+                    os._exit(17)
             if kind == KIND_DECODE:
                 h = self.runner.decode_launch_raw(*payload)
                 if pending is not None:  # keep at most two steps enqueued (staging is double-buffered)
@@ -591,11 +603,19 @@ class EngineService:
     * step failures - an exception inside a step fails only the requests in flight, resets the
       engine's batch and keeps serving; ``max_failures`` failures within ``failure_window_s`` (or
       any failure at TP > 1, where the workers' mirrored state is unknown) mark the service
-      unhealthy: ``healthy`` turns False and every later submit fails with EngineUnavailable.
+      unhealthy: ``healthy`` turns False and every later submit fails with EngineUnavailable;
+    * failure detection (parallel/health.py) - a watchdog thread marks the service unhealthy when a
+      step stays in flight longer than ``watchdog_s`` (a collective that never completes), and at
+      TP > 1 the leader's PeerMonitor does so as soon as a worker process is gone; both fail every
+      request in flight or queued at once (EngineUnavailable -> 503) and turn /health to 503,
+      instead of the leader blocking until the process-group timeout behind a 200 /health.
     """
 
     def __init__(self, engine: LLMEngine, max_queue: Optional[int] = None, max_failures: int = 3,
-                 failure_window_s: float = 60.0):
+                 failure_window_s: float = 60.0, watchdog_s: Optional[float] = None):
+        """``watchdog_s``: a step still in flight after this long marks the service unhealthy
+        (default ``K8SLLM_STEP_WATCHDOG_S`` or 30 s = twice the reference's 15 s write timeout;
+        a decode step takes milliseconds, a prefill step well under a second)."""
         self.engine = engine
         self.max_queue = max_queue if max_queue is not None else 4 * engine.cfg.max_num_seqs
         self.max_failures, self.failure_window_s = max_failures, failure_window_s
@@ -621,7 +641,57 @@ class EngineService:
         self.infeasible = 0  # refused because the answer could not finish before its deadline
         self._gpu_tpot = False  # step times come from GPU events (ModelRunner._chain_event)
         engine.sched.admit_gate = self._admit_ok
+        # failure detection (parallel/health.py): step watchdog + TP worker liveness
+        self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("K8SLLM_STEP_WATCHDOG_S", "30"))
+        self._step_t0: Optional[float] = None  # monotonic start of the step in flight
+        self.peer_monitor = None
+        if engine.ps.tp_size > 1 and engine.is_leader and engine.peer_idents:
+            peers = {r: ident for r, ident in enumerate(engine.peer_idents) if r != engine.ps.tp_rank}
+            self.peer_monitor = PeerMonitor(
+                peers, lambda r, ident: self._declare_dead(EngineUnavailable(
+                    f"TP worker rank {r} (pid {ident[0]}) exited: the group cannot run another step")))
+        self._wd_stop = threading.Event()
+        self._watchdog = threading.Thread(target=self._watch, name="llm-engine-watchdog", daemon=True)
         self._thread.start()
+        self._watchdog.start()
+
+    def _watch(self) -> None:
+        while not self._wd_stop.wait(0.25):
+            t0 = self._step_t0
+            if self._error is None and t0 is not None and time.monotonic() - t0 > self.watchdog_s:
+                self._declare_dead(EngineUnavailable(
+                    f"engine step in flight for more than {self.watchdog_s:.0f} s (a TP collective is not completing)"))
+            if self._error is not None:
+                return
+
+    def _declare_dead(self, e: BaseException) -> None:
+        """Mark the service unhealthy from a monitor thread (the engine thread may be blocked inside
+        a collective and never return): /health turns 503 and every request in flight or queued
+        fails now with EngineUnavailable instead of waiting for the process-group timeout."""
+        import logging
+
+        with self._lock:
+            if self._error is not None:
+                return
+            self._error = e
+        logging.getLogger("engine").error("engine unhealthy: %s", e)
+        err = e if isinstance(e, EngineUnavailable) else EngineUnavailable(str(e))
+        futs = []
+        try:
+            futs += [q.user for q in list(self.engine.sched.running) + list(self.engine.sched.waiting)]
+        except Exception:  # noqa: BLE001 - lists mutating under a live engine thread: best effort
+            pass
+        while True:
+            try:
+                futs.append(self._q.get_nowait()[3])
+            except queue.Empty:
+                break
+        for f in futs:
+            if isinstance(f, Future) and not f.done():
+                try:
+                    f.set_exception(err)
+                except Exception:  # noqa: BLE001 - resolved concurrently by the engine thread
+                    pass
 
     @property
     def healthy(self) -> bool:
@@ -860,7 +930,11 @@ class EngineService:
         d0 = eng.counters["decode_steps"]
         paced = eng._inflight is not None or not eng.cfg.pipeline  # this step waits for a GPU step
         ptok0 = eng.runner.n_steps.get("prefill_tokens", 0)
-        finished = eng.step()
+        self._step_t0 = time.monotonic()
+        try:
+            finished = eng.step()
+        finally:
+            self._step_t0 = None
         if (paced and not self._gpu_tpot and eng.counters["decode_steps"] > d0
                 and eng.counters["prefill_steps"] == p0):
             # (CPU / until event samples arrive) decode-only step: with pipelining, launching
@@ -940,5 +1014,9 @@ class EngineService:
 
     def close(self) -> None:
         self._stop.set()
+        self._wd_stop.set()
+        if self.peer_monitor is not None:
+            self.peer_monitor.stop()
         self._thread.join(timeout=10)
-        self.engine.stop_workers()
+        if self._error is None or not self.engine.ps.is_tp:
+            self.engine.stop_workers()

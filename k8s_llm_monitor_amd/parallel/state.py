@@ -106,11 +106,17 @@ def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optio
             dist.init_process_group(be, rank=rank, world_size=ws,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         be = dist.get_backend()
-        # every rank must create every group, in the same order
+        # every rank must create every group, in the same order.  The TP groups carry the serving
+        # steps' collectives: their timeout (K8SLLM_TP_TIMEOUT_S, default 60 s) bounds how long a
+        # rank can block on a dead peer before the process-group watchdog aborts it (the engine's
+        # PeerMonitor / step watchdog mark /health 503 within seconds, parallel/health.py); the
+        # default group keeps ``timeout_s`` for start-up (model init, graph capture).
+        tp_to = datetime.timedelta(seconds=float(os.environ.get("K8SLLM_TP_TIMEOUT_S", "60")))
         for g in range(ws // tp_size):
             ranks = list(range(g * tp_size, (g + 1) * tp_size))
-            grp = dist.new_group(ranks) if tp_size > 1 else None
-            cpu = dist.new_group(ranks, backend="gloo") if (tp_size > 1 and be != "gloo") else grp
+            grp = dist.new_group(ranks, timeout=tp_to) if tp_size > 1 else None
+            cpu = (dist.new_group(ranks, backend="gloo", timeout=tp_to) if (tp_size > 1 and be != "gloo")
+                   else grp)
             if rank in ranks:
                 st.tp_group, st.cpu_group = grp, cpu
         from .custom_ar import maybe_create

@@ -54,6 +54,9 @@ class GlooStepBus:
     def recv(self) -> bytes:
         return self._bcast(None)
 
+    def set_leader(self, ident: tuple) -> None:
+        self.leader_ident = ident  # gloo's own broadcast fails when the leader's socket closes
+
     def close(self) -> None:
         pass
 
@@ -62,7 +65,7 @@ class ShmStepBus:
     """Leader publishes into a native shared-memory ring; worker ``tp_rank - 1`` is reader index
     ``tp_rank - 1``.  Collective over the TP group's CPU group (name exchange + barrier)."""
 
-    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 600.0, poll_s: float = 1.0):
+    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 60.0, poll_s: float = 1.0):
         """``timeout_s`` bounds the LEADER's publish back-pressure (a worker that stopped consuming).
         A worker waits for the next step without a deadline - an idle server publishes nothing for
         as long as no request arrives - and polls the leader's liveness every ``poll_s`` instead,
@@ -74,6 +77,7 @@ class ShmStepBus:
             raise RuntimeError("native StepChannel unavailable")
         self.ps = ps
         self.timeout_s = timeout_s
+        self.idle_timeout_s = 600.0  # worker's bound on silence when it cannot observe the leader
         self.poll_s = poll_s
         src = ps.rank - ps.tp_rank
         name = [f"/k8sllm_step_{os.getpid()}_{uuid.uuid4().hex[:12]}" if ps.tp_rank == 0 else None]
@@ -113,13 +117,35 @@ class ShmStepBus:
     def send_stop(self) -> None:
         self._publish(struct.pack("<i", KIND_STOP))
 
+    def set_leader(self, ident: tuple) -> None:
+        """The leader's (pid, start time, host) from the engine's identity exchange: the liveness
+        poll below is used only if this worker can see that process (same host and pid namespace,
+        matching start time); otherwise the wait for a step is bounded by ``timeout_s`` instead."""
+        from .health import visible
+
+        self.leader_ident = ident
+        self.leader_visible = visible(ident)
+
     def recv(self) -> bytes:
+        from .health import alive
+
+        import time
+
+        t0 = time.monotonic()
         while True:
             m = self.ch.recv(self.reader, self.poll_s)
             if m is not None:
                 return m
-            if not _pid_alive(self.leader_pid):
-                raise ConnectionError(f"TP leader (pid {self.leader_pid}) exited without sending STOP")
+            ident = getattr(self, "leader_ident", None)
+            if ident is None:
+                if not _pid_alive(self.leader_pid):
+                    raise ConnectionError(f"TP leader (pid {self.leader_pid}) exited without sending STOP")
+            elif self.leader_visible:
+                if alive(ident) is False:
+                    raise ConnectionError(f"TP leader (pid {ident[0]}) exited without sending STOP")
+            elif time.monotonic() - t0 > self.idle_timeout_s:
+                raise ConnectionError(f"no step from the TP leader for {self.idle_timeout_s:.0f} s "
+                                      "(leader process not observable from this worker)")
 
     def close(self) -> None:
         self.ch.close()
