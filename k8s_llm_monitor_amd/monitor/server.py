@@ -620,6 +620,18 @@ class MonitorHTTPServer(ThreadingHTTPServer):
     allow_reuse_address = True
     request_queue_size = 1024
 
+    def handle_error(self, request, client_address) -> None:
+        """A client that hangs up mid-request (reset / broken pipe: a load generator or a probe
+        closing early) is routine for a server and is logged as one line at debug level; anything
+        else keeps socketserver's traceback."""
+        import sys
+
+        exc = sys.exc_info()[1]
+        if isinstance(exc, (ConnectionResetError, BrokenPipeError, ConnectionAbortedError)):
+            logging.getLogger("monitor.http").debug("client %s closed the connection: %r", client_address, exc)
+            return
+        super().handle_error(request, client_address)
+
 
 def make_server(app: MonitorApp, host: str = "0.0.0.0", port: int = 8080, read_timeout_s: float = 15.0):
     handler = type("BoundHandler", (_Handler,), {"app": app, "timeout": read_timeout_s})

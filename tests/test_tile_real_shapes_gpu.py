@@ -1,0 +1,134 @@
+"""Prefill tile GEMM (ops/csrc/gemm_tile.hip) against fp32 at the shapes the headline runs
+(VERDICT r3 item 3): Llama-3-8B qkv / o / down and gate_up + SwiGLU at 1024-4096 rows, the
+Mixtral-8x7B expert GEMMs grouped over 8 experts, and an engine-level check that a Llama-3-8B
+(2-layer) prefill whose chunks take the tile path inside CausalLM.forward matches an fp32 forward."""
+import pytest
+import torch
+
+from k8s_llm_monitor_amd import ops
+from k8s_llm_monitor_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+F_ = torch.nn.functional
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    ops.native()
+    torch.manual_seed(0)
+
+
+def _rel(y, r):
+    return ((y.float() - r).abs().max() / r.abs().max()).item()
+
+
+@pytest.mark.parametrize("M", [1024, 2048, 4096])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336)])
+def test_tile_dense_llama8b_shapes(M, N, K):
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    y = ops.gemm_tile(x, w, algo=ops.TILE_ALGO)
+    r = x.float() @ w.float().t()
+    assert _rel(y, r) < 1e-2, (M, N, K, _rel(y, r))
+    # the engine's routing entry point takes the same kernel at these sizes when asked to
+    yp = ops.prefill_linear(x, w) if ops.PREFILL_GEMM == "tile" else None
+    if yp is not None:
+        assert torch.equal(yp, y)
+
+
+@pytest.mark.parametrize("M", [1024, 4096])
+def test_tile_swiglu_gate_up_llama8b(M):
+    K, F = 4096, 14336
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(2 * F, K, device=DEV) * 0.02).to(torch.bfloat16)
+    y = ops.gemm_tile(x, ops.interleave_gate_up(w13).contiguous(), swiglu=True, algo=ops.TILE_ALGO)
+    gu = (x.float() @ w13.float().t()).to(torch.bfloat16).float()
+    r = F_.silu(gu[:, :F]) * gu[:, F:]
+    assert _rel(y, r) < 1.5e-2, _rel(y, r)
+
+
+@pytest.mark.parametrize("swiglu", [True, False])
+def test_tile_grouped_mixtral_8_experts(swiglu):
+    E, d, F = 8, 4096, 14336
+    counts = [1100, 0, 517, 2048, 33, 900, 1300, 250]
+    rows = sum(counts)
+    N, K = (2 * F, d) if swiglu else (d, F)
+    x = torch.randn(rows, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(E, N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    wk = torch.stack([ops.interleave_gate_up(we) for we in w]).contiguous() if swiglu else w
+    off = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device=DEV)
+    y = ops.gemm_tile(x, wk, off, swiglu=swiglu, algo=ops.TILE_ALGO)
+    o = 0
+    for e, n in enumerate(counts):
+        if n:
+            r = x[o:o + n].float() @ w[e].float().t()
+            if swiglu:
+                r = r.to(torch.bfloat16).float()
+                r = F_.silu(r[:, :F]) * r[:, F:]
+            assert _rel(y[o:o + n], r) < 1.5e-2, (e, _rel(y[o:o + n], r))
+        o += n
+
+
+def _fp32_forward(model, ids):
+    """Plain fp32 forward of the same weights (no HIP kernels): last-token logits."""
+    c = model.cfg
+    T = ids.numel()
+    x = model.embed[ids.long()].float()
+    cs = model.cos_sin.float()
+    pos = torch.arange(T, device=ids.device)
+    for L in model.layers:
+        h = F_.rms_norm(x, (c.d_model,), L["attn_norm"].float(), c.norm_eps)
+        qkv = h @ L["wqkv"].float().t()
+        Hq, Hk, D = model.hq, model.hkv, model.D
+        q, k, v = qkv.split([Hq * D, Hk * D, Hk * D], 1)
+        q, k = q.view(T, Hq, D), k.view(T, Hk, D)
+
+        def rope(t):
+            cos, sin = cs[pos, : D // 2][:, None], cs[pos, D // 2:][:, None]
+            a, b = t[..., : D // 2], t[..., D // 2:]
+            return torch.cat([a * cos - b * sin, a * sin + b * cos], -1)
+
+        q, k = rope(q), rope(k)
+        k = k.repeat_interleave(Hq // Hk, 1)
+        vv = v.view(T, Hk, D).repeat_interleave(Hq // Hk, 1)
+        att = F_.scaled_dot_product_attention(q.transpose(0, 1)[None], k.transpose(0, 1)[None],
+                                              vv.transpose(0, 1)[None], is_causal=True)[0]
+        x = x + att.transpose(0, 1).reshape(T, Hq * D) @ L["wo"].float().t()
+        h = F_.rms_norm(x, (c.d_model,), L["mlp_norm"].float(), c.norm_eps)
+        w13 = ops.deinterleave_gate_up(L["w13"]) if model._w13_il else L["w13"]
+        gu = h @ w13.float().t()
+        F = gu.shape[1] // 2
+        x = x + (F_.silu(gu[:, :F]) * gu[:, F:]) @ L["w2"].float().t()
+    h = F_.rms_norm(x[-1:], (c.d_model,), model.final_norm.float(), c.norm_eps)
+    return (h @ model.lm_head.float().t())[0][: c.vocab_size]
+
+
+@pytest.mark.parametrize("prompt_len", [1500, 3000])
+def test_engine_llama8b_two_layers_chunked_tile_prefill_matches_fp32(prompt_len, monkeypatch):
+    """A 2-layer model with Llama-3-8B dimensions, prompts chunked at 1024 tokens so every chunk's
+    projections run on gemm_tile (K8SLLM_PREFILL_GEMM=tile: M >= TILE_MIN_M) inside
+    CausalLM.forward; the first sampled token must be the fp32 argmax or a near-tie."""
+    monkeypatch.setattr(ops, "PREFILL_GEMM", "tile")
+    from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(EngineConfig(model="llama-3-8b", model_overrides={"n_layers": 2}, max_num_seqs=4,
+                                 max_model_len=4096, max_prefill_tokens=1024, chunked_prefill=True,
+                                 num_blocks=1024, use_graphs=False, seed=11), device=DEV)
+    calls = {"tile": 0}
+    orig = ops.gemm_tile
+
+    def counting(*a, **k):
+        calls["tile"] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(ops, "gemm_tile", counting)
+    g = torch.Generator().manual_seed(prompt_len)
+    ids = torch.randint(10, 120000, (prompt_len,), generator=g).tolist()
+    seq = eng.generate([ids], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))[0]
+    assert calls["tile"] >= 4 * 2, calls  # qkv / o / gate_up / down of both layers on the tile kernel
+    lg = _fp32_forward(eng.model, torch.tensor(ids, device=DEV))
+    tok = seq.output_ids[0]
+    top = lg.max()
+    assert int(lg.argmax()) == tok or float(top - lg[tok]) < 0.02 * float(lg.abs().max()), \
+        (tok, int(lg.argmax()), float(top - lg[tok]))
