@@ -422,13 +422,13 @@ class CausalLM:
         the IPC all-to-all kernel on the GPU, custom_ar.hip); the owner runs its local experts on
         what it received on the grouped skinny MFMA kernels (one launch for gate/up + SwiGLU of
         every local expert, one for their down projections into split-K slabs weighted one-hot by
-        each row's expert - the slab sum IS the per-row expert selection), in chunks of 64 rows;
+        each row's expert - the slab sum IS the per-row expert selection), in chunks of up to 128
+        rows (the row-major grouped kernel's 8-m-tile form: one weight stream per step at batch 64);
         the results return by the reverse all-to-all, are weighted and summed per token, and the
         slices are all-gathered.  Against the replicated form (every rank runs its experts on
-        every token, then one all-reduce) it computes only routed pairs but streams the local
-        expert weights once per 64-row chunk of the P x cap x K received rows, and moves two
-        all-to-alls plus an all-gather - so at decode batch sizes, where the step is bound by
-        streaming every expert's weights, the replicated form stays the default
+        every token, then one all-reduce) it computes only routed pairs, streams the local expert
+        weights once per 128-row chunk of the P x cap x K received rows (once per step at batch 64,
+        TP 2), and moves two all-to-alls plus an all-gather; the replicated form stays the default
         (K8SLLM_MOE_DECODE=a2a selects this one)."""
         c = self.cfg
         P, r, K, d = self.tp, self.rank, c.top_k_experts, c.d_model
@@ -459,8 +459,12 @@ class CausalLM:
         ws = self._skinny_ws
         if ws is not None and "w13_pg" in L:
             y = torch.empty(R, d, dtype=x.dtype, device=x.device)
-            for c0 in range(0, R, ops.SKINNY_MAX_M):
-                mc = min(ops.SKINNY_MAX_M, R - c0)
+            # up to 128 rows per grouped launch over the row-major expert weights: at decode batch
+            # 64 and TP=2 the P x cap x top-k = 128 received rows stream each local expert ONCE
+            step = (ops.SKINNY_GROUPED_MAX_M if L["w13_pg"].dim() == 3 and epr > 1 and x.is_cuda
+                    else ops.SKINNY_MAX_M)
+            for c0 in range(0, R, step):
+                mc = min(step, R - c0)
                 act = ops.skinny_grouped_swiglu(ops.pack_activation(rows[c0:c0 + mc]), L["w13_pg"], rows=mc)
                 ns = ops.skinny_grouped_slabs(act, L["w2_pg"], ws, mc, onehot[c0:c0 + mc].contiguous(), splits=1)
                 ops.reduce_slabs(ws, ns, mc, d, dtype=x.dtype, out=y[c0:c0 + mc])
@@ -616,7 +620,9 @@ class CausalLM:
 
         n = max(most(nq, d) * nq, most(d, self.hq * self.D) * d,
                 (self.e_hi - self.e_lo) * ops.skinny_nslabs(ff, 1) * d if c.is_moe else most(d, ff) * d)
-        self._skinny_ws = torch.empty(n * ops.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
+        # MoE: the EP all-to-all decode runs up to 128 received rows per grouped launch
+        rows = ops.SKINNY_GROUPED_MAX_M if c.is_moe else ops.SKINNY_MAX_M
+        self._skinny_ws = torch.empty(n * rows, dtype=torch.float32, device=self.device)
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list]) -> torch.Tensor:

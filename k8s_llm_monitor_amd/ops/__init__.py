@@ -73,6 +73,7 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
 # ---------------------------------------------------------------- decode projections (skinny GEMM)
 
 SKINNY_MAX_M = 64
+SKINNY_GROUPED_MAX_M = 128  # grouped (expert) launches over row-major weights: gemm_skinny.hip
 
 
 def pack_skinny(w: torch.Tensor) -> torch.Tensor:

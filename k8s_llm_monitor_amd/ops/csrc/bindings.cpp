@@ -554,7 +554,8 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
   TORCH_CHECK(epi == 0 || epi == 3, "gemm_skinny_grouped: epi must be 0 (slabs) or 3 (packed SwiGLU)");
   const int E = (int)wp.size(0), M = (int)rows;
   const long w_es = wp[0].numel();
-  TORCH_CHECK(M > 0 && M <= 64, "gemm_skinny_grouped: 1..64 rows");
+  TORCH_CHECK(M > 0 && (M <= 64 || (M <= 128 && w_rm && E > 1)),
+              "gemm_skinny_grouped: 1..64 rows (1..128 over row-major expert weights)");
   const int MT = (M + 15) / 16;
   long a_es = 0;
   TORCH_CHECK(a.is_contiguous() && a.size(-1) == 8 && a.size(-2) == 64 && a.size(-3) * 32 == K,

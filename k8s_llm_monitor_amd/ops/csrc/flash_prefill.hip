@@ -30,6 +30,18 @@ __device__ __forceinline__ void wait_vmcnt_fp() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// x combined with its lane ^ 32 partner by one v_permlane32_swap (VALU, no LDS round trip; a
+// __shfl_xor(x, 32) is a ds_bpermute): the swap leaves (own, partner) in lanes 0-31 and
+// (partner, own) in lanes 32-63, so an order-free op of the pair is the same on every lane.
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D, bool PAGED>
 __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restrict__ out, long out_stride,
                                                                const bf16_t* __restrict__ qkv, long qkv_stride,
@@ -373,12 +385,14 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   auto mask = [&](int t, f32x16 (&sa)[2]) {
     const int k0 = t * 64;
     if (__builtin_amdgcn_readfirstlane((k0 + 63 > wave_q0) || (k0 + 64 > LK))) {
-      const int lim = min(cst + myq, LK - 1) - k0 - 4 * hh;  // last visible key, relative
+      // last visible key, relative to this lane's first score row; one compare + select per score
+      // (a branchy form made hipcc build cumulative scalar masks: a 30-deep dependent SALU chain)
+      const float lim = (float)(min(cst + myq, LK - 1) - k0 - 4 * hh);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (32 * i + (r & 3) + 8 * (r >> 2) > lim) sa[i][r] = -1e30f;
+          sa[i][r] = (float)(32 * i + (r & 3) + 8 * (r >> 2)) > lim ? -1e30f : sa[i][r];
     }
   };
   // online softmax of one tile's scores (in place -> probabilities), then O += V^T P^T
@@ -396,24 +410,28 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
           vfr[i][s][dt] = *reinterpret_cast<const bf16x8*>(vt + (2 * i + s) * 4096 + (d * 2 + (hh ^ ((d >> 3) & 1))) * 16);
         }
     __builtin_amdgcn_sched_barrier(0);
-    float mx = sa[0][0];
+    // row max and row sum as four independent chains each (a single 32-long dependent chain is
+    // latency-bound), combined across the lane halves by v_permlane32_swap
+    float mq[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int c = 0; c < 4; ++c) mq[c] = fmaxf(sa[c >> 1][8 * (c & 1)], sa[c >> 1][8 * (c & 1) + 1]);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[i][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 2; r < 8; ++r) mq[c] = fmaxf(mq[c], sa[c >> 1][8 * (c & 1) + r]);
+    const float mx = xor32_max(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
     const float mnew = fmaxf(m, mx * scale_log2);
     const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-    float rs = 0.f;
+    float rq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i][r], scale_log2, -mnew));
         sa[i][r] = p;
-        rs += p;
+        rq[(2 * i + (r >> 3))] += p;
       }
-    rs += __shfl_xor(rs, 32, 64);
+    const float rs = xor32_sum((rq[0] + rq[1]) + (rq[2] + rq[3]));
     l = l * alpha + rs;
     const bool grew = __builtin_amdgcn_ballot_w64(mnew > m) != 0;  // lazy rescale: O only when a max moved
     m = mnew;

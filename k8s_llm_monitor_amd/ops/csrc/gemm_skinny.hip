@@ -709,7 +709,37 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
   if (M <= 0) return 0;
   if (experts < 1) return -5;
   const SkinnyGroup grp{w_es, a_es, y_es, row_w, row_w_ld};
-  if (M > 64 || K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
+  // 65..128 rows: grouped (expert) launches over row-major weights only - the EP all-to-all
+  // decode's received rows (P x cap x top-k), so every local expert's weights stream ONCE per step
+  // instead of once per 64-row chunk (2-wave workgroups: 8 m-tiles of A per stage)
+  if (M > 64) {
+    if (M > 128 || !w_rm || experts < 2 || !a_packed || K % 64 != 0 || N % 64 != 0 ||
+        (epi != EPI_SLAB && epi != EPI_SWIGLU_PACKED))
+      return -1;
+    if (S <= 0) S = 1;
+    const int kc8 = skinny_kchunk(K, S, 64);
+    const int slabs8 = (K + kc8 - 1) / kc8;
+    if (epi != EPI_SLAB && slabs8 != 1) return -3;
+    const float inv_d8 = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
+    dim3 grid8(N / 64, slabs8, experts), blk8(128);
+#define K8S_RM8(MTV, EPV)                                                                                                launch_rm<MTV, 4, EPV, 2>(grid8, blk8, s, (const bf16_t*)A, (const bf16_t*)Wp, (long)K, partial, (bf16_t*)Y, ldy,                               M, N, K, kc8, rn_ss, rn_nc, inv_d8, rn_eps, grp)
+#define K8S_RM8_M(EPV)                  \
+  switch ((M + 15) / 16) {              \
+    case 5: K8S_RM8(5, EPV); break;     \
+    case 6: K8S_RM8(6, EPV); break;     \
+    case 7: K8S_RM8(7, EPV); break;     \
+    default: K8S_RM8(8, EPV); break;    \
+  }
+    if (epi == EPI_SLAB) {
+      K8S_RM8_M(EPI_SLAB)
+    } else {
+      K8S_RM8_M(EPI_SWIGLU_PACKED)
+    }
+#undef K8S_RM8_M
+#undef K8S_RM8
+    return (int)hipGetLastError();
+  }
+  if (K % 32 != 0 || (nt_tiles != 2 && nt_tiles != 4) || N % (16 * nt_tiles) != 0) return -1;
   if (S <= 0) S = epi == EPI_SLAB ? k8sllm_gemm_skinny_auto_splits(M, N, K) : 1;
   const int kc = skinny_kchunk(K, S, w_rm ? 64 : 32);
   if (w_rm) {

@@ -164,7 +164,7 @@ def _rank_main(rank: int, world: int, port: int, q) -> None:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gpu_custom_all_reduce_ranks_one_gpu(world):
     """Every IPC collective of custom_ar.hip with ``world`` rank processes sharing the one GPU of
     the test box: one-shot / two-shot all-reduce (the W = 4 two-shot part ownership included),
@@ -183,7 +183,7 @@ def test_gpu_custom_all_reduce_ranks_one_gpu(world):
     res = {}
     try:
         for _ in procs:
-            rank, bad, err = q.get(timeout=150)
+            rank, bad, err = q.get(timeout=200)
             res[rank] = (bad, err)
     finally:
         for p in procs:

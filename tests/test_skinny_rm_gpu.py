@@ -78,8 +78,10 @@ def test_rm_deferred_rmsnorm(M):
     _close(y.cpu(), y_ref, atol=3e-2, rtol=3e-2, what="rm deferred norm")
 
 
-@pytest.mark.parametrize("M,E", [(1, 4), (64, 2)])
+@pytest.mark.parametrize("M,E", [(1, 4), (64, 2), (100, 2), (128, 4)])
 def test_rm_grouped_moe(M, E):
+    """Grouped gate/up + SwiGLU and down over every local expert; 65..128 rows take the 8-m-tile
+    2-wave form (the EP all-to-all decode's received rows in one launch)."""
     K, F, d = 512, 448, 256
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w13 = (torch.randn(E, 2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
