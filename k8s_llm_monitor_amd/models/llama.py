@@ -311,17 +311,19 @@ class CausalLM:
         return tp_all_reduce(ops.prefill_linear(h, L["w2"]), self.ps)
 
     def _moe(self, L: dict, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
-        """Top-k MoE over this rank's experts [e_lo, e_hi).  Prefill: tokens are sorted by expert
-        (moe_align) and each local expert runs one GEMM pair on its contiguous rows.  Decode: the
-        dense-masked form (every local expert on every token, scaled by its routing weight, 0 if
-        not selected) - no host sync, so the decode step stays graph-capturable; at decode batch
-        sizes the step is bound by reading every expert's weights either way."""
+        """Top-k MoE over this rank's experts [e_lo, e_hi).  Tokens are sorted by expert (moe_align)
+        and every local expert runs on its contiguous rows in ONE grouped launch per projection
+        (gemm_tile.hip / moe_gemm.hip, device-side offsets: no host sync, so a decode step beyond
+        the skinny kernels' row limit stays graph-capturable).  The CPU decode form is the
+        dense-masked reference (every local expert on every token, scaled by its routing weight)."""
         c = self.cfg
         T = x.shape[0]
         K = c.top_k_experts
         logits = F.linear(x, L["router"]).float()
         ids, w = ops.moe_route(logits, K, True)
-        if not meta.is_prefill:
+        if not meta.is_prefill and not (self._moe_grouped and x.is_cuda):
+            # CPU reference of the decode form (the GPU takes the routed grouped path below, which
+            # needs no host sync either and runs only the (token, expert) pairs that were chosen)
             wd = torch.zeros(T, c.n_experts, dtype=torch.float32, device=x.device)
             wd.scatter_(1, ids.long(), w)
             out = torch.zeros(T, c.d_model, dtype=torch.float32, device=x.device)
