@@ -247,6 +247,7 @@ class CausalLM:
         c = self.cfg
         k_cache, v_cache = kv if kv is not None else (None, None)
         partial, ns = None, 0
+        roped = False  # q / k already rotated by the qkv GEMM's epilogue
         T = rows if rows is not None else x.shape[0]
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
         if slabs is not None:
@@ -262,11 +263,14 @@ class CausalLM:
             qkv = torch.empty(T, L["wqkv"].shape[0], dtype=self.dtype, device=self.device)
         elif "bqkv" in L:
             qkv = F.linear(x, L["wqkv"], L["bqkv"])
+        elif c.arch == "llama" and self.D == 128 and self.cos_sin is not None:
+            # prefill-sized qkv on the tile kernel: RoPE of q / k fused into its epilogue
+            qkv, roped = ops.prefill_linear(x, L["wqkv"], rope=(meta.positions, cs, self.hq + self.hkv))
         else:
             qkv = ops.prefill_linear(x, L["wqkv"])
         ops.rope_and_cache(qkv, meta.positions, cs, k_cache, v_cache,
                            meta.slot_mapping if k_cache is not None else None, self.hq, self.hkv, self.D,
-                           apply_rope=c.arch == "llama", partial=partial, nslabs=ns)
+                           apply_rope=c.arch == "llama" and not roped, partial=partial, nslabs=ns)
         if meta.is_prefill:
             qb = (meta.qb_seq, meta.qb_start) if meta.qb_seq is not None else None
             paged = None

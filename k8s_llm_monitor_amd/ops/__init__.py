@@ -819,25 +819,36 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
 
 
 def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] = None, swiglu: bool = False,
-              out: Optional[torch.Tensor] = None, algo: int = 0) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, algo: int = 0, rope: Optional[tuple] = None) -> torch.Tensor:
     """Prefill-sized ``x @ w^T`` on the 256 x 256 MFMA tile kernel (csrc/gemm_tile.hip).
 
     Dense: ``w`` [N, K].  Grouped: ``w`` [E, N, K] and ``offsets`` [E + 1] int32 device offsets of
     each expert's rows in the expert-sorted ``x`` (moe_align; a slice for this rank's experts) - no
     host synchronisation.  ``swiglu``: ``w`` is gate/up-interleaved (interleave_gate_up) and the
     result is silu(gate) * up [M, N / 2].  Grouped rows outside the offsets are left as in ``out``
-    (zeros when allocated here)."""
+    (zeros when allocated here).  ``rope = (positions [M] int32, cos_sin [P, 128] fp32, heads)``
+    (dense, N % 128 == 0): the epilogue applies rotate-half RoPE (head_dim 128) to output heads
+    0 .. heads - 1 of each row at its position, on the bf16-rounded product."""
     M = x.shape[0]
     N = w.shape[-2]
     if out is None:
         alloc = torch.zeros if offsets is not None else torch.empty
         out = alloc(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if rope is not None and (offsets is not None or swiglu or N % 128):
+        raise ValueError("gemm_tile: the RoPE epilogue is dense, without SwiGLU, N % 128 == 0")
     if not _gpu(x):
         def one(xr, wr):
             y = torch.nn.functional.linear(xr.float(), wr.float()).to(x.dtype)
             return silu_mul(y, interleaved=True) if swiglu else y
         if offsets is None:
             out.copy_(one(x, w))
+            if rope is not None:
+                pos, cs, heads = rope
+                h = out[:, : heads * 128].view(M, heads, 128).float()
+                c = cs[pos.long(), :64].float()[:, None]
+                s_ = cs[pos.long(), 64:].float()[:, None]
+                a, b = h[..., :64], h[..., 64:]
+                out[:, : heads * 128] = torch.cat([a * c - b * s_, b * c + a * s_], -1).reshape(M, -1).to(out.dtype)
         else:
             off = offsets.tolist()
             for e in range(w.shape[0]):
@@ -845,7 +856,12 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
                 if b > a:
                     out[a:b] = one(x[a:b], w[e])
         return out
-    native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None, swiglu, algo)
+    if rope is not None:
+        pos, cs, heads = rope
+        native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads)
+    else:
+        native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None,
+                           swiglu, algo)
     return out
 
 
@@ -856,20 +872,30 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
 # hipBLASLt's separate silu_mul pass); qkv / o / down stay on hipBLASLt, 4-8 % faster there
 # (profiles/r03/gemm_ring_addressing.jsonl).
 PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "auto")
+QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fused RoPE on the tile kernel
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 TILE_ALGO = 1  # refill schedule: two barriers per k-tile
 
 
 def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
-                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, rope: Optional[tuple] = None) -> torch.Tensor:
     """``x @ w^T`` for a prefill-sized ``x`` [M, K] and row-major ``w`` [N, K]; ``swiglu``: ``w`` is
     gate/up-interleaved (interleave_gate_up) and the result is silu(gate) * up [M, N / 2] - fused
-    into the tile kernel's epilogue, or F.linear + silu_mul on the library path."""
+    into the tile kernel's epilogue, or F.linear + silu_mul on the library path.
+    ``rope = (positions, cos_sin, heads)`` (the qkv projection, head_dim 128): the tile kernel
+    rotates heads 0 .. heads - 1 in its epilogue; returns ``(y, rotated)`` - rotated False when the
+    library took the GEMM (the caller then applies RoPE itself)."""
     M, K = x.shape
     N = w.shape[0]
     mode = PREFILL_GEMM
     tile_ok = (_gpu(x) and M >= TILE_MIN_M and N % 16 == 0 and K % 64 == 0 and K >= 128
                and (not swiglu or N % 256 == 0) and N * K * 2 < (1 << 31))
+    if rope is not None:
+        # the qkv projection takes the tile kernel whenever its RoPE epilogue applies: it replaces
+        # rope_cache's read-rotate-write pass over q / k (more than the GEMM gives up to hipBLASLt)
+        if tile_ok and N % 128 == 0 and mode != "blas" and QKV_ROPE_TILE:
+            return gemm_tile(x, w, out=out, algo=TILE_ALGO, rope=rope), True
+        return prefill_linear(x, w, out=out), False
     use_tile = tile_ok and (mode == "tile" or (mode == "auto" and swiglu))
     if use_tile:
         return gemm_tile(x, w, swiglu=swiglu, out=out, algo=TILE_ALGO)

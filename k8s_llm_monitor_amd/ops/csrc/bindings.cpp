@@ -40,7 +40,7 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E, long w_es,
-                     int epi, int algo, hipStream_t s);
+                     int epi, int algo, const int* rope_pos, const float* rope_cs, int rope_heads, hipStream_t s);
 int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* offsets, int E, long rows, int N, int K,
                             long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
@@ -364,8 +364,11 @@ void moe_grouped_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, torch::
 // 256 x 256 MFMA GEMM (gemm_tile.hip) for prefill-sized projections: y = x . w^T, x [M, K], w [N, K]
 // (dense, offsets None) or w [E, N, K] with device offsets [E + 1] (grouped over expert-sorted rows,
 // no host sync).  swiglu: w gate/up-interleaved per 128 rows, y [M, N / 2] = silu(gate) * up.
+// rope_pos / rope_cs (dense, N % 128 == 0): the qkv projection with the rotary embedding of heads
+// 0 .. rope_heads - 1 (q and k, head_dim 128) applied in the epilogue (TILE_EPI_ROPE)
 void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, bool swiglu,
-               int64_t algo) {
+               int64_t algo, c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_cs,
+               int64_t rope_heads) {
   dev_bf16(y, "y"); dev_bf16(x, "x"); dev_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.is_contiguous() && y.is_contiguous(),
               "gemm_tile: x [M, K], w contiguous, y contiguous");
@@ -385,8 +388,21 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
     TORCH_CHECK(offsets->numel() == E + 1, "gemm_tile: offsets must hold E + 1 entries");
     op = offsets->data_ptr<int>();
   }
-  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, op, E, (long)N * K, swiglu ? 1 : 0,
-                         (int)algo, cur()),
+  const int* rp = nullptr;
+  const float* rc = nullptr;
+  if (rope_pos.has_value()) {
+    TORCH_CHECK(!grouped && !swiglu && rope_cs.has_value() && N % 128 == 0, "gemm_tile: rope epilogue is dense qkv");
+    dev_i32(*rope_pos, "rope_pos");
+    TORCH_CHECK(rope_pos->numel() >= M, "gemm_tile: rope_pos needs a position per row");
+    TORCH_CHECK(rope_heads >= 0 && rope_heads * 128 <= N, "gemm_tile: rope_heads * 128 must fit in N");
+    TORCH_CHECK(rope_cs->is_cuda() && rope_cs->scalar_type() == torch::kFloat32 && rope_cs->is_contiguous() &&
+                    rope_cs->dim() == 2 && rope_cs->size(1) == 128,
+                "gemm_tile: rope_cs must be [max_pos, 128] fp32 (head_dim 128)");
+    rp = rope_pos->data_ptr<int>();
+    rc = rope_cs->data_ptr<float>();
+  }
+  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, op, E, (long)N * K,
+                         rp ? 2 : (swiglu ? 1 : 0), (int)algo, rp, rc, (int)rope_heads, cur()),
         "gemm_tile");
 }
 
@@ -739,7 +755,8 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("silu_mul", &silu_mul);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_tile", &gemm_tile, py::arg("y"), py::arg("x"), py::arg("w"), py::arg("offsets"), py::arg("swiglu"),
-        py::arg("algo") = 0);
+        py::arg("algo") = 1, py::arg("rope_pos") = py::none(), py::arg("rope_cs") = py::none(),
+        py::arg("rope_heads") = 0);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("embedding", &embedding);
   m.def("resolve_ids", &resolve_ids);

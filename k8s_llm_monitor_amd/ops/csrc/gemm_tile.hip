@@ -60,12 +60,23 @@ __device__ __forceinline__ void vm_wait_n() {
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 }  // namespace
 
-enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1 };
+enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2 };
+
+// TILE_EPI_ROPE (the prefill qkv projection): the output columns are heads of 128; a wave's
+// 128-column quarter is exactly one head, and for q / k heads (head < rope_heads) the rotary
+// embedding (neox pairs i, i + 64) is applied to the staged bf16 rows before they are stored -
+// rope_cache's separate read-rotate-write pass over q / k disappears.
+struct TileRope {
+  const int* positions;  // [M] absolute position of each row
+  const float* cos_sin;  // [max_pos][128]: cos (64) | sin (64)
+  int rope_heads;        // Hq + Hkv: heads 0 .. rope_heads - 1 are rotated
+};
 
 template <int EPI, bool GROUPED, int SCH>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
-                                                         int E, int M, int N, int K, long w_es, int n_mt, int n_nt) {
+                                                         int E, int M, int N, int K, long w_es, int n_mt, int n_nt,
+                                                         TileRope rope) {
   constexpr int HS = 32768;  // one half-slot: 256 rows x 128 B
   __shared__ __attribute__((aligned(16))) char smem[5 * HS];
   const int lane = threadIdx.x & 63;
@@ -323,6 +334,39 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     }
   }
   lgkm_wait0();
+  if constexpr (EPI == TILE_EPI_ROPE) {
+    const int head = (n0 + wn * 128) >> 7;
+    if (head < rope.rope_heads && nrows - wn * 128 >= 128) {
+      // one lane per (row, chunk pair c, c + 8): 8 rows per pass, 16 passes over the quarter's rows
+      const int c = lane & 7, rsub = lane >> 3;
+      bf16_t* ybase = Y + (long)row0 * N + n0 + wn * 128;
+#pragma unroll 4
+      for (int pass = 0; pass < 16; ++pass) {
+        const int r = pass * 8 + rsub, grow = wm * 128 + r;
+        if (grow >= mrows) continue;
+        const uint4 a = *reinterpret_cast<const uint4*>(stage + r * RS + c * 16);
+        const uint4 b = *reinterpret_cast<const uint4*>(stage + r * RS + (c + 8) * 16);
+        const float* cs = rope.cos_sin + (long)rope.positions[row0 + grow] * 128;
+        const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8), c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(cs + 64 + c * 8),
+                     s1 = *reinterpret_cast<const float4*>(cs + 64 + c * 8 + 4);
+        const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float x1[8], x2[8], o1[8], o2[8];
+        unpack8(a, x1);
+        unpack8(b, x2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o1[j] = x1[j] * cc[j] - x2[j] * ss[j];
+          o2[j] = x2[j] * cc[j] + x1[j] * ss[j];
+        }
+        bf16_t* yr = ybase + (long)grow * N;
+        *reinterpret_cast<uint4*>(yr + c * 8) = pack8(o1);
+        *reinterpret_cast<uint4*>(yr + 64 + c * 8) = pack8(o2);
+      }
+      return;
+    }
+  }
   constexpr int CPR = OUTW / 8;  // 16-B chunks per row
   constexpr int RPI = 64 / CPR;  // rows per wave instruction
   const int ldy = EPI == TILE_EPI_SWIGLU ? (N >> 1) : N;
@@ -354,12 +398,15 @@ using namespace k8sllm;
 // bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
 // Shapes: N % 16 == 0 (SwiGLU: N % 256 == 0), K % 64 == 0.  algo: the refill schedule (0 or 1).
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
-                                long w_es, int epi, int algo, hipStream_t s) {
+                                long w_es, int epi, int algo, const int* rope_pos, const float* rope_cs,
+                                int rope_heads, hipStream_t s) {
   if (M <= 0) return 0;
   const bool grouped = offsets != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
   if (algo < 0 || algo > 1) return -1;
   if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
+  if (epi == TILE_EPI_ROPE && (grouped || N % 128 != 0 || rope_pos == nullptr || rope_cs == nullptr)) return -1;
+  const TileRope rope{rope_pos, rope_cs, rope_heads};
   // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert / n-tile)
   if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
   const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = (N + 255) / 256;
@@ -368,13 +415,14 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
   const dim3 grid((unsigned)nwg);
 #define K8_TILE_LAUNCH(EPI_, G_, SCH_)                                                                               \
   hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, SCH_>), grid, dim3(256), 0, s, (const bf16_t*)X, (const bf16_t*)W,   \
-                     (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt)
+                     (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt, rope)
 #define K8_TILE_SCH(SCH_)                                                                                            \
   if (grouped) {                                                                                                     \
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true, SCH_);                                         \
     else K8_TILE_LAUNCH(TILE_EPI_BF16, true, SCH_);                                                                  \
   } else {                                                                                                           \
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, SCH_);                                        \
+    else if (epi == TILE_EPI_ROPE) K8_TILE_LAUNCH(TILE_EPI_ROPE, false, SCH_);                                       \
     else K8_TILE_LAUNCH(TILE_EPI_BF16, false, SCH_);                                                                 \
   }
   if (algo == 1) {

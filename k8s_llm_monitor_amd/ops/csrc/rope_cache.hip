@@ -214,11 +214,15 @@ extern "C" int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* position
   const int* rope_slots = runs ? nullptr : slot_mapping;
   const int items = (Hq + (runs ? 1 : 2) * Hkv) * (D / 8);
   dim3 grid((unsigned)T, (items + 127) / 128);
+  // nothing to rotate (q / k rotated by the qkv GEMM epilogue, or a model without RoPE) and the
+  // cache written run-wise below: the in-place pass would only copy q / k onto themselves
+  const bool skip_rope = runs && !apply_rope;
 #define K8S_ROPE(DV, SL)                                                                                       \
   hipLaunchKernelGGL((rope_cache_kernel<DV, SL>), grid, dim3(128), 0, s, (bf16_t*)qkv, qkv_stride, positions,  \
                      cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, rope_slots, Hq, Hkv, block_size, apply_rope,   \
                      partial, S, (int)T)
-  if (D == 128) {
+  if (skip_rope) {
+  } else if (D == 128) {
     if (partial) K8S_ROPE(128, true); else K8S_ROPE(128, false);
   } else if (D == 64) {
     if (partial) K8S_ROPE(64, true); else K8S_ROPE(64, false);

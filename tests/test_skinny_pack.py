@@ -137,3 +137,28 @@ def test_gemm_tile_cpu_path():
     wi = ops.interleave_gate_up(we[1])
     torch.testing.assert_close(ops.gemm_tile(x, wi, swiglu=True),
                                ops.silu_mul(F_.linear(x, we[1]), interleaved=False))
+
+
+def test_gemm_tile_rope_cpu_path():
+    """ops.gemm_tile(rope=...) off the GPU rotates heads 0 .. heads - 1 of the bf16 product exactly as
+    ops.reference.apply_rope and leaves the rest; rejected with grouped / SwiGLU weights."""
+    from k8s_llm_monitor_amd.ops import reference as ref
+
+    torch.manual_seed(3)
+    M, K, H, Hr = 40, 256, 6, 4
+    x = torch.randn(M, K, dtype=torch.bfloat16)
+    w = (torch.randn(H * 128, K) * 0.05).to(torch.bfloat16)
+    cs = ref.rope_cos_sin(512, 128, 10000.0)
+    pos = torch.randint(0, 512, (M,), dtype=torch.int32)
+    y = ops.gemm_tile(x, w, rope=(pos, cs, Hr))
+    plain = torch.nn.functional.linear(x.float(), w.float()).to(torch.bfloat16)
+    want = ref.apply_rope(plain[:, : Hr * 128].view(M, Hr, 128), pos, cs).reshape(M, -1)
+    torch.testing.assert_close(y[:, : Hr * 128].float(), want, atol=2e-2, rtol=1e-2)
+    assert torch.equal(y[:, Hr * 128:], plain[:, Hr * 128:])
+    # the routing entry point reports that the library took it (RoPE left to rope_and_cache)
+    y2, rotated = ops.prefill_linear(x, w, rope=(pos, cs, Hr))
+    assert not rotated
+    torch.testing.assert_close(y2.float(), plain.float(), atol=2e-2, rtol=1e-2)
+    import pytest
+    with pytest.raises(ValueError):
+        ops.gemm_tile(x, w, swiglu=True, rope=(pos, cs, Hr))

@@ -70,6 +70,26 @@ def test_tile_grouped_mixtral_8_experts(swiglu):
         o += n
 
 
+@pytest.mark.parametrize("M", [1024, 1609, 4096])
+def test_tile_qkv_rope_epilogue_llama8b(M):
+    """qkv projection with RoPE of the 32 q + 8 k heads fused into the tile epilogue (TILE_EPI_ROPE)
+    vs fp32 GEMM -> bf16 -> rotate; v heads untouched; ragged last m-tile at M = 1609; positions
+    not monotone (a mixed batch of several sequences)."""
+    N, K, Hq, Hk = 6144, 4096, 32, 8
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    cs = ref.rope_cos_sin(8192, 128, 500000.0).to(DEV).float().contiguous()
+    pos = torch.cat([torch.arange(M // 2), torch.arange(M - M // 2) + 3000]).to(DEV, torch.int32)
+    y = ops.gemm_tile(x, w, algo=ops.TILE_ALGO, rope=(pos, cs, Hq + Hk))
+    r = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    qk = ref.apply_rope(r[:, : (Hq + Hk) * 128].view(M, Hq + Hk, 128), pos, cs).reshape(M, -1)
+    assert _rel(y[:, : (Hq + Hk) * 128], qk) < 1e-2
+    assert _rel(y[:, (Hq + Hk) * 128:], r[:, (Hq + Hk) * 128:]) < 1e-2
+    # the engine's entry point fuses it whenever the tile kernel takes the projection
+    yp, rot = ops.prefill_linear(x, w, rope=(pos, cs, Hq + Hk))
+    assert rot and torch.equal(yp, y)
+
+
 def _fp32_forward(model, ids):
     """Plain fp32 forward of the same weights (no HIP kernels): last-token logits."""
     c = model.cfg
@@ -126,7 +146,7 @@ def test_engine_llama8b_two_layers_chunked_tile_prefill_matches_fp32(prompt_len,
     g = torch.Generator().manual_seed(prompt_len)
     ids = torch.randint(10, 120000, (prompt_len,), generator=g).tolist()
     seq = eng.generate([ids], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))[0]
-    assert calls["tile"] >= 4 * 2, calls  # qkv / o / gate_up / down of both layers on the tile kernel
+    assert calls["tile"] >= 4 * 2, calls  # qkv (+ RoPE) / o / gate_up / down of both layers on the tile kernel
     lg = _fp32_forward(eng.model, torch.tensor(ids, device=DEV))
     tok = seq.output_ids[0]
     top = lg.max()

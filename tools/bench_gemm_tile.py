@@ -46,6 +46,26 @@ def main() -> None:
             "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
             "hipblaslt": (lambda i, xin=xin, w=w, y=y: torch.matmul(xin, w.t(), out=y)),
         }))
+    # qkv + RoPE + paged-cache write, as the prefill layer runs it: tile GEMM with the RoPE epilogue
+    # + cache-only pass, vs hipBLASLt + the rotate-and-cache pass
+    from k8s_llm_monitor_amd.ops import reference as ref
+    wq = torch.randn(6144, d, device=dev, dtype=torch.bfloat16) * 0.02
+    yq = torch.empty(T, 6144, device=dev, dtype=torch.bfloat16)
+    cs = ref.rope_cos_sin(max(T, 8192), 128, 500000.0).to(dev).float().contiguous()
+    pos = (torch.arange(T, device=dev) % 8192).to(torch.int32)
+    nb = (T + 15) // 16
+    kc = torch.empty(nb, 8, 16, 16, 8, device=dev, dtype=torch.bfloat16)
+    vc = torch.empty(nb, 8, 128, 16, device=dev, dtype=torch.bfloat16)
+    slots = torch.arange(T, device=dev, dtype=torch.int32)
+    cases.append(("qkv+rope+cache", 2 * T * 6144 * d, {
+        "w4s": (lambda i: ops.rope_and_cache(ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40)), pos, cs,
+                                             kc, vc, slots, 32, 8, 128, apply_rope=False)),
+        "hipblaslt": (lambda i: ops.rope_and_cache(torch.matmul(x, wq.t(), out=yq), pos, cs, kc, vc, slots,
+                                                   32, 8, 128, apply_rope=True)),
+        "w4s_gemm_only": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40))),
+        "rope_cache_only": (lambda i: ops.rope_and_cache(yq, pos, cs, kc, vc, slots, 32, 8, 128, apply_rope=True)),
+        "cache_only": (lambda i: ops.rope_and_cache(yq, pos, cs, kc, vc, slots, 32, 8, 128, apply_rope=False)),
+    }))
     w13 = ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02).contiguous()
     gu = torch.empty(T, 2 * F, device=dev, dtype=torch.bfloat16)
     act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
