@@ -317,8 +317,8 @@ class LLMEngine:
         toks = self.runner.decode_collect(handle)
         self._check_collectives()
         ms = handle.gpu_ms() if hasattr(handle, "gpu_ms") else None
-        if ms is not None:  # a back-to-back decode step: its GPU time at this row count
-            self.step_samples.append((len(seqs), ms))
+        if ms is not None:  # a back-to-back decode step: its GPU time at this row count and context
+            self.step_samples.append((len(seqs), ms, sum(q.num_tokens for q in seqs)))
         now = time.perf_counter()
         done = []
         for q, tok in zip(seqs, toks):
@@ -502,28 +502,77 @@ class _Skip(Exception):
 
 
 class TpotModel:
-    """Decode step time (ms) as a function of the batch size, learned online: an EWMA per batch
-    size seen, and a least-squares line t(b) = a + c*b over those sizes (a decode step streams the
-    weights once - the constant - plus per-row KV and activations - the slope).  ``estimate`` is
-    None until a step has been seen; with one size seen, that time is used for every size up to
-    it and grows in proportion beyond it."""
+    """Decode step time (ms) learned online from measured steps.
 
-    def __init__(self, alpha: float = 0.25):
+    Two models, the richer one used once it is trustworthy:
+
+    * by batch size - an EWMA per batch size seen and a least-squares line t(b) = a + c*b over
+      those sizes; with one size seen, that time is used for every size up to it and grows in
+      proportion beyond it;
+    * by batch size AND context - t(b, kv) = a + r*b + k*kv with kv the batch's total context
+      tokens (every decode step streams the weights once - a - and each cached token's K/V once -
+      k; r is the per-row activation / sampling cost), a non-negative least-squares fit over the
+      last ``window`` (b, kv, ms) samples, refit every ``refit`` new samples and used only when it
+      explains the samples to within ``max_rel_err`` (RMS).  Attention time grows with every
+      generated token, so a batch-size-only EWMA, which follows the latest (longest-context) steps,
+      overstates the step time of an answer that starts now - the admission gate would refuse
+      answers that fit (profiles/r04/production_2000tok_b64.json: predicted 6.66 ms at 40 rows,
+      5.91 ms measured over the answers).
+    """
+
+    def __init__(self, alpha: float = 0.25, window: int = 1024, refit: int = 64, min_samples: int = 48,
+                 max_rel_err: float = 0.08):
         self.alpha = alpha
         self.ew: dict[int, float] = {}
         self._fit: Optional[tuple] = None
+        self.samples: deque = deque(maxlen=window)  # (b, kv tokens, ms)
+        self.refit, self.min_samples, self.max_rel_err = refit, min_samples, max_rel_err
+        self._since = 0
+        self.kv_fit: Optional[tuple] = None  # (a, r, k per 1000 tokens, rms rel err)
 
-    def record(self, b: int, ms: float) -> None:
+    def record(self, b: int, ms: float, kv: Optional[int] = None) -> None:
         if b <= 0 or ms <= 0:
             return
         old = self.ew.get(b)
         self.ew[b] = ms if old is None else (1 - self.alpha) * old + self.alpha * ms
         self._fit = None
+        if kv is not None and kv > 0:
+            self.samples.append((b, kv, ms))
+            self._since += 1
+            if len(self.samples) >= self.min_samples and (self.kv_fit is None or self._since >= self.refit):
+                self._fit_kv()
 
-    def estimate(self, b: int) -> Optional[float]:
+    def _fit_kv(self) -> None:
+        import numpy as np
+
+        self._since = 0
+        a = np.asarray(self.samples, dtype=np.float64)
+        X = np.stack([np.ones(len(a)), a[:, 0], a[:, 1] / 1000.0], 1)
+        y = a[:, 2]
+        if np.ptp(X[:, 2]) <= 0.05 * max(1.0, X[:, 2].mean()):
+            return  # no context spread: the slope is not identifiable
+        # one batch size only: the per-row term is not separable from the constant - leave it out
+        active = [0, 1, 2] if np.ptp(X[:, 1]) > 0 else [0, 2]
+        coef = np.zeros(3)
+        for _ in range(3):  # non-negative least squares by dropping negative terms (3 unknowns)
+            sol, *_ = np.linalg.lstsq(X[:, active], y, rcond=None)
+            if (sol >= 0).all():
+                coef[:] = 0.0
+                coef[active] = sol
+                break
+            active = [c for c, v in zip(active, sol) if v > 0] or [0]
+        else:
+            return
+        err = float(np.sqrt(np.mean(((X @ coef) - y) ** 2 / y ** 2)))
+        self.kv_fit = (float(coef[0]), float(coef[1]), float(coef[2]), err) if err <= self.max_rel_err else None
+
+    def estimate(self, b: int, kv: Optional[float] = None) -> Optional[float]:
         if not self.ew:
             return None
         b = max(1, b)
+        if kv is not None and self.kv_fit is not None:
+            a, r, k, _ = self.kv_fit
+            return max(0.5 * min(self.ew.values()), a + r * b + k * kv / 1000.0)
         if len(self.ew) == 1:
             (b0, t0), = self.ew.items()
             return t0 if b <= b0 else t0 * b / b0
@@ -538,7 +587,12 @@ class TpotModel:
         return max(lo, a + c * b)
 
     def snapshot(self) -> dict:
-        return {str(b): round(t, 3) for b, t in sorted(self.ew.items())}
+        d = {str(b): round(t, 3) for b, t in sorted(self.ew.items())}
+        if self.kv_fit is not None:
+            a, r, k, e = self.kv_fit
+            d["kv_fit"] = {"ms_const": round(a, 4), "ms_per_row": round(r, 5), "ms_per_1k_ctx_tokens": round(k, 5),
+                           "rms_rel_err": round(e, 4), "samples": len(self.samples)}
+        return d
 
 
 _ROW_ORDER = os.environ.get("K8SLLM_DECODE_ROW_ORDER", "1") != "0"
@@ -776,15 +830,37 @@ class EngineService:
             return rem
         return min(rem, max(q - gen, 32))
 
-    def _running_slack(self, n_after: int, step_s: float, now: float) -> float:
-        """Smallest (deadline - expected finish) over the running requests that have a deadline,
-        at ``step_s`` per step; memoised per engine step (the gate and the infeasibility sweep of
-        every waiting request reuse it)."""
-        key = ("slack", n_after)
+    def _kv_now(self) -> int:
+        """Total context tokens of the running batch (memoised per engine step)."""
+        v = self._step_cache.get("kv")
+        if v is None:
+            v = self._step_cache["kv"] = sum(q.num_tokens for q in self.engine.sched.running)
+        return v
+
+    def _answer_s(self, n: int, rem: int, extra_kv: int = 0) -> Optional[float]:
+        """Seconds for ``rem`` more decode steps at batch ``n``, with the safety margin.  With the
+        context-aware model the step time is taken at the batch's mean context over those steps:
+        today's running contexts + ``extra_kv`` (a joiner's prompt) + n tokens per step, rem / 2
+        steps on average (running answers are assumed not to finish earlier - conservative)."""
+        kv = None
+        if self.tpot.kv_fit is not None:
+            kv = self._kv_now() + extra_kv + n * rem / 2.0
+        t = self.tpot.estimate(n, kv)
+        return None if t is None else rem * t * 1e-3 * self.deadline_margin
+
+    def _running_slack(self, n_after: int, now: float, extra_kv: int = 0) -> float:
+        """Smallest (deadline - expected finish) over the running requests that have a deadline, at
+        batch ``n_after``; memoised per engine step (the gate and the infeasibility sweep of every
+        waiting request reuse it; joiners' prompts are bucketed by 256 tokens)."""
+        bucket = (extra_kv + 255) // 256
+        key = ("slack", n_after, bucket)
         v = self._step_cache.get(key)
         if v is None:
-            v = min((q.deadline - now - self._expected_rem(q) * step_s for q in self.engine.sched.running
-                     if q.deadline is not None), default=float("inf"))
+            v = float("inf")
+            for q in self.engine.sched.running:
+                if q.deadline is not None:
+                    t = self._answer_s(n_after, self._expected_rem(q), bucket * 256)
+                    v = min(v, q.deadline - now - (t or 0.0))
             self._step_cache[key] = v
         return v
 
@@ -798,32 +874,31 @@ class EngineService:
             return True
         if seq.deadline is None:
             return True
-        t = self.tpot.estimate(n_after)
-        if t is None:
+        ans = self._answer_s(n_after, self._expected_rem(seq), seq.num_tokens)
+        if ans is None:
             return True
         now = time.perf_counter()
-        step_s = t * 1e-3 * self.deadline_margin
         pre = self._prefill_s(seq)
-        if now + pre + self._expected_rem(seq) * step_s > seq.deadline:
+        if now + pre + ans > seq.deadline:
             return False
-        return pre <= self._running_slack(n_after, step_s, now)
+        return pre <= self._running_slack(n_after, now, seq.num_tokens)
 
     def _infeasible(self, seq: Sequence, now: float) -> bool:
         """A never-started request that cannot finish before its deadline even if it starts when
         the first running answer completes (or now, if the gate admits it now)."""
         running = self.engine.sched.running
-        t = self.tpot.estimate(max(1, len(running)))
-        if t is None or seq.deadline is None:
+        n = max(1, len(running))
+        ans = self._answer_s(n, self._expected_rem(seq), seq.num_tokens)
+        if ans is None or seq.deadline is None:
             return False
-        step_s = t * 1e-3 * self.deadline_margin
         wait = 0.0
         if not self._admit_ok(seq, len(running) + 1):
             key = ("minrem",)
             m = self._step_cache.get(key)
             if m is None:
                 m = self._step_cache[key] = min((self._expected_rem(q) for q in running), default=0)
-            wait = m * step_s
-        return now + wait + self._prefill_s(seq) + self._expected_rem(seq) * step_s > seq.deadline
+            wait = self._answer_s(n, m) or 0.0
+        return now + wait + self._prefill_s(seq) + ans > seq.deadline
 
     def _expire_waiting(self) -> None:
         """Waiting requests whose deadline has passed: one that never started is dropped
@@ -940,7 +1015,7 @@ class EngineService:
             # (CPU / until event samples arrive) decode-only step: with pipelining, launching
             # step N waits for step N-1, so the interval is one GPU step at (about) this batch size
             rows = eng._inflight[0] if eng._inflight is not None else eng.sched.running
-            self.tpot.record(len(rows), (time.perf_counter() - t0) * 1e3)
+            self.tpot.record(len(rows), (time.perf_counter() - t0) * 1e3, sum(q.num_tokens for q in rows))
         if eng.counters["prefill_steps"] > p0:
             dt = time.perf_counter() - t0
             n = eng.runner.n_steps.get("prefill_tokens", 0) - ptok0

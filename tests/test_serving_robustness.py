@@ -376,3 +376,45 @@ def test_tpot_samples_from_engine_events_feed_the_model():
         assert svc._gpu_tpot and 5.9 <= svc.tpot.estimate(64) <= 6.1
     finally:
         svc.close()
+
+
+def test_tpot_context_model_fit():
+    """t(b, kv) = a + r*b + k*kv is recovered from (batch, context tokens, ms) samples; without a
+    context spread (or with a poor fit) the batch-size-only model stays in charge."""
+    from k8s_llm_monitor_amd.engine.engine import TpotModel
+
+    m = TpotModel(alpha=1.0)
+    for i in range(60):  # one batch size, context growing as the answers grow: no spread yet
+        m.record(64, 3.0 + 0.02 * 64 + 0.021 * (100000 + 64 * 0) / 1000, kv=100000)
+    assert m.kv_fit is None
+    m = TpotModel(alpha=1.0)
+    for b in (40, 64):
+        for step in range(0, 2000, 20):
+            kv = b * (1600 + step)
+            m.record(b, 3.0 + 0.02 * b + 0.021 * kv / 1000, kv=kv)
+    a, r, k, err = m.kv_fit
+    assert abs(a - 3.0) < 0.05 and abs(r - 0.02) < 0.002 and abs(k - 0.021) < 0.001 and err < 1e-6
+    # an answer that starts now at 64 rows x 1.6k context is priced at its own context, not at the
+    # latest (longest-context) steps the per-batch EWMA follows
+    assert abs(m.estimate(64, 64 * 1600) - (3.0 + 1.28 + 0.021 * 102.4)) < 0.01
+    assert m.estimate(64) > m.estimate(64, 64 * 1600) + 2.0
+    assert m.snapshot()["kv_fit"]["samples"] == 200
+
+
+def test_admission_prices_answers_at_their_context():
+    """The batch-size EWMA follows the latest, longest-context steps; the context-aware model
+    prices a fresh answer at the mean context over its own life, so an answer that fits its
+    deadline is admitted (production runs: 36 % refused with the EWMA alone)."""
+    eng, svc = _frozen_service()
+    try:
+        for kv in range(1000, 9001, 100):  # 8 rows, step time 10 ms + 2 ms per 1k context tokens
+            svc.tpot.record(8, 10.0 + 2.0 * kv / 1000, kv=kv)
+        assert svc.tpot.kv_fit is not None and svc.tpot.estimate(8) > 27.0
+        sp = SamplingParams(max_tokens=100, temperature=0.0, ignore_eos=True)
+        s = Sequence(prompt_ids=[5] * 10, params=sp, request_id="c", deadline=time.perf_counter() + 2.0)
+        # EWMA: 100 x 28 ms x 1.05 = 2.9 s > 2 s; at its context (10 + 8 x 50 tokens): ~1.2 s
+        assert svc._admit_ok(s, 8)
+        tight = Sequence(prompt_ids=[5] * 10, params=sp, request_id="t", deadline=time.perf_counter() + 1.0)
+        assert not svc._admit_ok(tight, 8)
+    finally:
+        svc.close()
