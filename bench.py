@@ -299,13 +299,15 @@ def run_rank(a) -> None:
     # `value` counts complete answers: a production-mode answer cut at its deadline is reported
     # separately (requests.deadline_truncated_rank0), not as a served query
     n_full = sum(1 for r in ok if r.get("finish_reason") != "deadline")
-    _finish(a, ps, comm, elapsed, n_full, ptoks, gtoks, res, stats, devices, eng, on_gpu)
+    _finish(a, ps, comm, elapsed, n_full, ptoks, gtoks, res, stats, devices, eng, on_gpu, n_answered=len(ok))
 
 
-def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, on_gpu) -> None:
+def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, on_gpu, n_answered=None) -> None:
     world = ps.world_size
     t_max = comm.all_reduce_max_scalar(elapsed)
     total_q = comm.all_reduce_sum_scalar(float(n_ok))
+    # prompt tokens are summed over every answered request (deadline-truncated ones included)
+    total_ans = comm.all_reduce_sum_scalar(float(n_ok if n_answered is None else n_answered))
     total_gen = comm.all_reduce_sum_scalar(float(gtoks))
     total_p = comm.all_reduce_sum_scalar(float(ptoks))
     ok = [r for r in res if r.get("http_status", 200) == 200]
@@ -340,7 +342,7 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
         "dtype": "bf16",
         "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
         "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": 8192, "parallelism": par,
-                   "prompt_tokens_mean": round(total_p / max(1.0, total_q), 1),
+                   "prompt_tokens_mean": round(total_p / max(1.0, total_ans), 1),
                    "max_new_tokens": a.max_new_tokens, "path": a.path, "mode": a.mode,
                    "client": a.client if a.path != "engine" else None,
                    "server_timeouts": "production 15s/30s" if a.production else "bench 600s"},

@@ -831,10 +831,24 @@ class EngineService:
         return min(rem, max(q - gen, 32))
 
     def _kv_now(self) -> int:
-        """Total context tokens of the running batch (memoised per engine step)."""
-        v = self._step_cache.get("kv")
+        """Total context tokens of the running batch (memoised per engine step and batch size)."""
+        key = ("kv", len(self.engine.sched.running))
+        v = self._step_cache.get(key)
         if v is None:
-            v = self._step_cache["kv"] = sum(q.num_tokens for q in self.engine.sched.running)
+            v = self._step_cache[key] = sum(q.num_tokens for q in self.engine.sched.running)
+        return v
+
+    def _backlog_s(self) -> float:
+        """Seconds of prefill still owed to admitted sequences (prompt tokens not yet computed):
+        in a burst every answer's first decode step waits for the whole burst's prefill, not only
+        its own (production runs at 64 concurrent: ~0.9 s)."""
+        if not self._prefill_tps:
+            return 0.0
+        key = ("backlog", len(self.engine.sched.running))
+        v = self._step_cache.get(key)
+        if v is None:
+            v = self._step_cache[key] = sum(max(0, q.num_tokens - q.num_computed)
+                                            for q in self.engine.sched.running) / self._prefill_tps
         return v
 
     def _answer_s(self, n: int, rem: int, extra_kv: int = 0) -> Optional[float]:
@@ -853,7 +867,7 @@ class EngineService:
         batch ``n_after``; memoised per engine step (the gate and the infeasibility sweep of every
         waiting request reuse it; joiners' prompts are bucketed by 256 tokens)."""
         bucket = (extra_kv + 255) // 256
-        key = ("slack", n_after, bucket)
+        key = ("slack", n_after, bucket, len(self.engine.sched.running))
         v = self._step_cache.get(key)
         if v is None:
             v = float("inf")
@@ -878,10 +892,10 @@ class EngineService:
         if ans is None:
             return True
         now = time.perf_counter()
-        pre = self._prefill_s(seq)
-        if now + pre + ans > seq.deadline:
+        pre, backlog = self._prefill_s(seq), self._backlog_s()
+        if now + backlog + pre + ans > seq.deadline:
             return False
-        return pre <= self._running_slack(n_after, now, seq.num_tokens)
+        return pre <= self._running_slack(n_after, now, seq.num_tokens) - backlog
 
     def _infeasible(self, seq: Sequence, now: float) -> bool:
         """A never-started request that cannot finish before its deadline even if it starts when
@@ -898,7 +912,7 @@ class EngineService:
             if m is None:
                 m = self._step_cache[key] = min((self._expected_rem(q) for q in running), default=0)
             wait = self._answer_s(n, m) or 0.0
-        return now + wait + self._prefill_s(seq) + ans > seq.deadline
+        return now + max(wait, self._backlog_s()) + self._prefill_s(seq) + ans > seq.deadline
 
     def _expire_waiting(self) -> None:
         """Waiting requests whose deadline has passed: one that never started is dropped

@@ -866,12 +866,13 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
 
 
 # Prefill projections (qkv / o / gate_up + SwiGLU / down) on the hand-written 4-wave MFMA GEMM
-# (csrc/gemm_tile.hip, two-barrier schedule) or hipBLASLt (torch F.linear).  K8SLLM_PREFILL_GEMM=
-# tile|blas forces one; the default ("auto") takes the tile kernel where it measured at least at
-# parity with hipBLASLt on the same box: the fused gate_up + SwiGLU (1.50 vs 1.42 PF/s including
-# hipBLASLt's separate silu_mul pass); qkv / o / down stay on hipBLASLt, 4-8 % faster there
-# (profiles/r03/gemm_ring_addressing.jsonl).
-PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "auto")
+# (csrc/gemm_tile.hip, two-barrier schedule) or hipBLASLt (torch F.linear).  The default ("tile")
+# takes the tile kernel for every projection of at least TILE_MIN_M rows: in isolation hipBLASLt is
+# 4-8 % faster on o / down (profiles/r03/gemm_ring_addressing.jsonl), but in the served headline
+# the all-tile routing measured +1.4 % (three interleaved pairs, profiles/r04/bench_pg2_*.json:
+# 25.06 vs 24.71 q/s), with qkv's RoPE fused into the tile epilogue.  "auto" = tile for the fused
+# epilogues only (gate_up + SwiGLU, qkv + RoPE), hipBLASLt for o / down; "blas" = hipBLASLt for all.
+PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "tile")
 QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fused RoPE on the tile kernel
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 TILE_ALGO = 1  # refill schedule: two barriers per k-tile

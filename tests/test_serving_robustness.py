@@ -418,3 +418,29 @@ def test_admission_prices_answers_at_their_context():
         assert not svc._admit_ok(tight, 8)
     finally:
         svc.close()
+
+
+def test_admission_counts_the_burst_prefill_backlog():
+    """Every answer of a burst waits for the whole burst's prefill before its first decode step:
+    prompt tokens admitted but not yet computed delay a joiner's answer (and the running ones')."""
+    eng, svc = _frozen_service()
+    try:
+        svc.tpot.record(1, 10.0)
+        svc.tpot.record(8, 10.0)
+        svc._prefill_tps = 1000.0  # 1k prompt tokens per second
+        sp = SamplingParams(max_tokens=50, temperature=0.0, ignore_eos=True)
+        joiner = Sequence(prompt_ids=[5] * 10, params=sp, request_id="j", deadline=time.perf_counter() + 1.0)
+        assert svc._admit_ok(joiner, 2)  # 10 ms prefill + 50 x 10.5 ms fits 1 s
+        queued = Sequence(prompt_ids=[5] * 800, params=sp, request_id="q")  # admitted, not yet prefilled
+        eng.sched.running.append(queued)
+        try:
+            svc._step_cache.clear()
+            assert svc._backlog_s() > 0.79
+            assert not svc._admit_ok(joiner, 2)  # 0.8 s of backlog + 0.53 s no longer fits
+            queued.num_computed = 800
+            svc._step_cache.clear()
+            assert svc._admit_ok(joiner, 2)
+        finally:
+            eng.sched.running.remove(queued)
+    finally:
+        svc.close()
