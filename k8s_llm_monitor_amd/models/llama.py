@@ -239,7 +239,8 @@ class CausalLM:
         return tp_all_reduce(y, self.ps)
 
     def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None,
-                   rows: Optional[int] = None, rownorm: Optional[tuple] = None) -> torch.Tensor:
+                   rows: Optional[int] = None, rownorm: Optional[tuple] = None,
+                   rowscale: Optional[tuple] = None) -> torch.Tensor:
         """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
         ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM over ``x`` (row-major
         or fragment-packed with ``rows`` valid rows), reduced inside rope_and_cache; the attention
@@ -265,7 +266,8 @@ class CausalLM:
             qkv = F.linear(x, L["wqkv"], L["bqkv"])
         elif c.arch == "llama" and self.D == 128 and self.cos_sin is not None:
             # prefill-sized qkv on the tile kernel: RoPE of q / k fused into its epilogue
-            qkv, roped = ops.prefill_linear(x, L["wqkv"], rope=(meta.positions, cs, self.hq + self.hkv))
+            qkv, roped = ops.prefill_linear(x, L["wqkv"], rope=(meta.positions, cs, self.hq + self.hkv),
+                                            rowscale=rowscale)
         else:
             qkv = ops.prefill_linear(x, L["wqkv"])
         ops.rope_and_cache(qkv, meta.positions, cs, k_cache, v_cache,
@@ -510,6 +512,8 @@ class CausalLM:
             residual = h
             if self._use_skinny(meta, h):
                 return self._decode_layers_skinny(None, residual, meta, kv_caches)
+            if self._fused_norm_ok(h):
+                return self._logits(self._prefill_fused_norm(residual, meta, kv_caches))
             x = ops.rms_norm(h, self.layers[0]["attn_norm"], c.norm_eps)
             n = len(self.layers)
             for i, L in enumerate(self.layers):
@@ -525,6 +529,44 @@ class CausalLM:
                         residual = residual[meta.logits_idx].contiguous()
                     x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
         return self._logits(x)
+
+    def _fused_norm_ok(self, h: torch.Tensor) -> bool:
+        """Dense Llama-family prefill at TP=1 on the tile GEMMs: the RMSNorms between projections
+        can live in the GEMM epilogues (``_prefill_fused_norm``)."""
+        c = self.cfg
+        if not h.is_cuda or c.arch != "llama" or c.is_moe or self.tp != 1 or not self._w13_il:
+            return False
+        if self.D != 128 or self.cos_sin is None or any(k in self.layers[0] for k in ("bqkv", "bo")):
+            return False
+        L = self.layers[0]
+        return ops.fused_norm_ok(h.shape[0], c.d_model, L["wqkv"].shape[0], L["wo"].shape[1], L["w13"].shape[0],
+                                 L["w2"].shape[1])
+
+    def _prefill_fused_norm(self, residual: torch.Tensor, meta: AttnMeta, kv_caches: Optional[list]) -> torch.Tensor:
+        """The prefill layers with every RMSNorm but the first and the final one folded into the
+        tile GEMMs: the o / down epilogues add their product to the residual stream in place and
+        emit (residual * next norm weight, per-128-column sums of squares); qkv (+ RoPE) and
+        gate_up (+ SwiGLU) scale their rows by the resulting 1/rms - no separate fused-add RMSNorm
+        pass over the [tokens, d_model] activations between projections."""
+        c = self.cfg
+        eps = c.norm_eps
+        n = len(self.layers)
+        x = ops.rms_norm(residual, self.layers[0]["attn_norm"], eps)
+        ss = None
+        for i, L in enumerate(self.layers):
+            kv = kv_caches[i] if kv_caches is not None else None
+            o = self._attn_core(L, x, meta, kv, rowscale=(ss, eps) if ss is not None else None)
+            x, ss = ops.gemm_tile_resid(o, L["wo"], residual, L["mlp_norm"])
+            act = ops.prefill_linear(x, L["w13"], swiglu=True, rowscale=(ss, eps))
+            if i + 1 < n:
+                x, ss = ops.gemm_tile_resid(act, L["w2"], residual, self.layers[i + 1]["attn_norm"])
+            else:
+                y = ops.prefill_linear(act, L["w2"])
+                if meta.logits_idx is not None:
+                    y = y[meta.logits_idx]
+                    residual = residual[meta.logits_idx].contiguous()
+                x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, eps)
+        return x
 
     def _logits(self, x: torch.Tensor, rows: Optional[int] = None) -> torch.Tensor:
         """LM head (+ the TP all-gather of the vocab shards).  ``x``: the final-normed rows,

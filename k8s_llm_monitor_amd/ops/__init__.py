@@ -819,7 +819,8 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
 
 
 def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] = None, swiglu: bool = False,
-              out: Optional[torch.Tensor] = None, algo: int = 0, rope: Optional[tuple] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, algo: int = 0, rope: Optional[tuple] = None,
+              rowscale: Optional[tuple] = None) -> torch.Tensor:
     """Prefill-sized ``x @ w^T`` on the 256 x 256 MFMA tile kernel (csrc/gemm_tile.hip).
 
     Dense: ``w`` [N, K].  Grouped: ``w`` [E, N, K] and ``offsets`` [E + 1] int32 device offsets of
@@ -828,7 +829,11 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
     result is silu(gate) * up [M, N / 2].  Grouped rows outside the offsets are left as in ``out``
     (zeros when allocated here).  ``rope = (positions [M] int32, cos_sin [P, 128] fp32, heads)``
     (dense, N % 128 == 0): the epilogue applies rotate-half RoPE (head_dim 128) to output heads
-    0 .. heads - 1 of each row at its position, on the bf16-rounded product."""
+    0 .. heads - 1 of each row at its position, on the bf16-rounded product.
+    ``rowscale = (ss_part [M, K / 128] fp32, eps)`` (dense, with ``swiglu`` or ``rope``, schedule 1):
+    the deferred half of an RMSNorm - every row of the product is multiplied by
+    rsqrt(sum(ss_part[row]) / K + eps) before the epilogue (``x`` holds the norm's weighted input,
+    gemm_tile_resid's ``hw``)."""
     M = x.shape[0]
     N = w.shape[-2]
     if out is None:
@@ -836,9 +841,19 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
         out = alloc(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
     if rope is not None and (offsets is not None or swiglu or N % 128):
         raise ValueError("gemm_tile: the RoPE epilogue is dense, without SwiGLU, N % 128 == 0")
+    if rowscale is not None and (offsets is not None or not (swiglu or rope is not None)):
+        raise ValueError("gemm_tile: the row scale is for the dense fused consumers (SwiGLU or RoPE)")
     if not _gpu(x):
+        inv = None
+        if rowscale is not None:
+            ssp, eps = rowscale
+            inv = torch.rsqrt(ssp[:M].float().sum(1, keepdim=True) / x.shape[1] + eps)
+
         def one(xr, wr):
-            y = torch.nn.functional.linear(xr.float(), wr.float()).to(x.dtype)
+            y = torch.nn.functional.linear(xr.float(), wr.float())
+            if inv is not None:
+                y = y * inv
+            y = y.to(x.dtype)
             return silu_mul(y, interleaved=True) if swiglu else y
         if offsets is None:
             out.copy_(one(x, w))
@@ -856,13 +871,42 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
                 if b > a:
                     out[a:b] = one(x[a:b], w[e])
         return out
+    rs_part, rs_eps = rowscale if rowscale is not None else (None, 1e-5)
+    if rowscale is not None and algo != 1:
+        raise ValueError("gemm_tile: the row scale needs schedule 1")
     if rope is not None:
         pos, cs, heads = rope
-        native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads)
+        native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads, rs_part, rs_eps)
+    elif rowscale is not None:
+        native().gemm_tile(out, x.contiguous(), w, None, swiglu, algo, None, None, 0, rs_part, rs_eps)
     else:
         native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None,
                            swiglu, algo)
     return out
+
+
+def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_w: torch.Tensor,
+                    hw: Optional[torch.Tensor] = None, ss: Optional[torch.Tensor] = None) -> tuple:
+    """A residual-producing prefill projection with the next RMSNorm's pass fused into its epilogue
+    (csrc/gemm_tile.hip TILE_EPI_RESID; dense, N % 128 == 0): ``resid`` [M, N] <- bf16(resid +
+    bf16(x @ w^T)) in place; returns ``(hw, ss)`` - hw = bf16(resid * norm_w) [M, N] and ss [M, N / 128]
+    fp32 partial sums of resid^2 over each 128 columns, the operands of the consumer's row scale
+    (``gemm_tile(hw, ..., rowscale=(ss, eps))`` = the projection of rms_norm(resid) * norm_w)."""
+    M, N = x.shape[0], w.shape[0]
+    if N % 128 or resid.shape != (M, N):
+        raise ValueError("gemm_tile_resid: N % 128 == 0 and resid [M, N]")
+    hw = hw if hw is not None else torch.empty_like(resid)
+    ss = ss if ss is not None else torch.empty(M, N // 128, dtype=torch.float32, device=resid.device)
+    if not _gpu(x):
+        y = torch.nn.functional.linear(x.float(), w.float()).to(x.dtype)
+        h = (y.float() + resid.float()).to(resid.dtype)
+        resid.copy_(h)
+        hw.copy_((h.float() * norm_w.float()).to(hw.dtype))
+        ss.copy_((h.float() ** 2).view(M, N // 128, 128).sum(2))
+        return hw, ss
+    native().gemm_tile(resid, x.contiguous(), w, None, False, 1, None, None, 0, None, 1e-5, resid, hw,
+                       norm_w.contiguous(), ss)
+    return hw, ss
 
 
 # Prefill projections (qkv / o / gate_up + SwiGLU / down) on the hand-written 4-wave MFMA GEMM
@@ -874,12 +918,30 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
 # epilogues only (gate_up + SwiGLU, qkv + RoPE), hipBLASLt for o / down; "blas" = hipBLASLt for all.
 PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "tile")
 QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fused RoPE on the tile kernel
+# residual-add RMSNorm folded into the o / down epilogues and the qkv / gate_up row scale
+FUSED_NORM = os.environ.get("K8SLLM_FUSED_NORM", "0") != "0"
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 TILE_ALGO = 1  # refill schedule: two barriers per k-tile
 
 
+def tile_shape_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
+    """gemm_tile takes this prefill GEMM (rows, output columns, depth)."""
+    return (M >= TILE_MIN_M and N % 16 == 0 and K % 64 == 0 and K >= 128 and (not swiglu or N % 256 == 0)
+            and N * K * 2 < (1 << 31))
+
+
+def fused_norm_ok(M: int, d: int, n_qkv: int, n_o_in: int, n_13: int, f: int) -> bool:
+    """The prefill layer may run with its RMSNorms folded into the tile GEMMs (gemm_tile_resid +
+    row scale): every projection on the tile kernel (default routing), qkv with the RoPE epilogue,
+    d a multiple of 128 with at most 32 partial sums per row."""
+    return (FUSED_NORM and PREFILL_GEMM == "tile" and QKV_ROPE_TILE and d % 128 == 0 and d // 128 <= 32
+            and n_qkv % 128 == 0 and tile_shape_ok(M, n_qkv, d) and tile_shape_ok(M, d, n_o_in)
+            and tile_shape_ok(M, n_13, d, swiglu=True) and tile_shape_ok(M, d, f) and 256 * d * 2 < (1 << 31))
+
+
 def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
-                   out: Optional[torch.Tensor] = None, rope: Optional[tuple] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
+                   rowscale: Optional[tuple] = None) -> torch.Tensor:
     """``x @ w^T`` for a prefill-sized ``x`` [M, K] and row-major ``w`` [N, K]; ``swiglu``: ``w`` is
     gate/up-interleaved (interleave_gate_up) and the result is silu(gate) * up [M, N / 2] - fused
     into the tile kernel's epilogue, or F.linear + silu_mul on the library path.
@@ -889,14 +951,15 @@ def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
     M, K = x.shape
     N = w.shape[0]
     mode = PREFILL_GEMM
-    tile_ok = (_gpu(x) and M >= TILE_MIN_M and N % 16 == 0 and K % 64 == 0 and K >= 128
-               and (not swiglu or N % 256 == 0) and N * K * 2 < (1 << 31))
+    tile_ok = _gpu(x) and tile_shape_ok(M, N, K, swiglu)
     if rope is not None:
         # the qkv projection takes the tile kernel whenever its RoPE epilogue applies: it replaces
         # rope_cache's read-rotate-write pass over q / k (more than the GEMM gives up to hipBLASLt)
-        if tile_ok and N % 128 == 0 and mode != "blas" and QKV_ROPE_TILE:
-            return gemm_tile(x, w, out=out, algo=TILE_ALGO, rope=rope), True
+        if (tile_ok and N % 128 == 0 and mode != "blas" and QKV_ROPE_TILE) or rowscale is not None:
+            return gemm_tile(x, w, out=out, algo=TILE_ALGO, rope=rope, rowscale=rowscale), True
         return prefill_linear(x, w, out=out), False
+    if rowscale is not None:  # the fused-norm consumer (the caller checked fused_norm_ok)
+        return gemm_tile(x, w, swiglu=swiglu, out=out, algo=TILE_ALGO, rowscale=rowscale)
     use_tile = tile_ok and (mode == "tile" or (mode == "auto" and swiglu))
     if use_tile:
         return gemm_tile(x, w, swiglu=swiglu, out=out, algo=TILE_ALGO)

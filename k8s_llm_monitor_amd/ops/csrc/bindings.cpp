@@ -40,7 +40,9 @@ int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, co
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
 int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E, long w_es,
-                     int epi, int algo, const int* rope_pos, const float* rope_cs, int rope_heads, hipStream_t s);
+                     int epi, int algo, const int* rope_pos, const float* rope_cs, int rope_heads,
+                     const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw, const void* norm_w,
+                     float* ss_out, hipStream_t s);
 int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* offsets, int E, long rows, int N, int K,
                             long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
@@ -368,7 +370,9 @@ void moe_grouped_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, torch::
 // 0 .. rope_heads - 1 (q and k, head_dim 128) applied in the epilogue (TILE_EPI_ROPE)
 void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, bool swiglu,
                int64_t algo, c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_cs,
-               int64_t rope_heads) {
+               int64_t rope_heads, c10::optional<torch::Tensor> rs_part, double rs_eps,
+               c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> hw,
+               c10::optional<torch::Tensor> norm_w, c10::optional<torch::Tensor> ss_out) {
   dev_bf16(y, "y"); dev_bf16(x, "x"); dev_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.is_contiguous() && y.is_contiguous(),
               "gemm_tile: x [M, K], w contiguous, y contiguous");
@@ -401,8 +405,35 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
     rp = rope_pos->data_ptr<int>();
     rc = rope_cs->data_ptr<float>();
   }
-  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, op, E, (long)N * K,
-                         rp ? 2 : (swiglu ? 1 : 0), (int)algo, rp, rc, (int)rope_heads, cur()),
+  // row scale (deferred RMSNorm of the A rows): rs_part [M][K / 128] fp32 partial sums of squares
+  const float* rsp = nullptr;
+  int rs_np = 0;
+  if (rs_part.has_value()) {
+    TORCH_CHECK(!grouped && K % 128 == 0, "gemm_tile: row scale needs dense, K % 128 == 0");
+    TORCH_CHECK(rs_part->is_cuda() && rs_part->scalar_type() == torch::kFloat32 && rs_part->is_contiguous() &&
+                    rs_part->dim() == 2 && rs_part->size(0) >= M && rs_part->size(1) == K / 128,
+                "gemm_tile: rs_part must be [M, K / 128] fp32");
+    rsp = rs_part->data_ptr<float>();
+    rs_np = K / 128;
+  }
+  // residual epilogue: resid [M][N] += y (in place), hw = resid * norm_w, ss_out [M][N / 128]
+  const bool rsd = resid.has_value();
+  if (rsd) {
+    TORCH_CHECK(!grouped && !swiglu && !rp && !rsp && N % 128 == 0 && hw.has_value() && norm_w.has_value() &&
+                    ss_out.has_value(), "gemm_tile: residual epilogue is dense, N % 128 == 0, with hw / norm_w / ss_out");
+    dev_bf16(*resid, "resid"); dev_bf16(*hw, "hw"); dev_bf16(*norm_w, "norm_w");
+    TORCH_CHECK(resid->is_contiguous() && resid->dim() == 2 && resid->size(0) == M && resid->size(1) == N,
+                "gemm_tile: resid [M, N]");
+    TORCH_CHECK(hw->is_contiguous() && hw->dim() == 2 && hw->size(0) == M && hw->size(1) == N, "gemm_tile: hw [M, N]");
+    TORCH_CHECK(norm_w->is_contiguous() && norm_w->numel() == N, "gemm_tile: norm_w [N]");
+    TORCH_CHECK(ss_out->is_cuda() && ss_out->scalar_type() == torch::kFloat32 && ss_out->is_contiguous() &&
+                    ss_out->numel() >= (long)M * (N / 128), "gemm_tile: ss_out [M, N / 128] fp32");
+  }
+  const int epi = rsd ? 3 : rp ? 2 : (swiglu ? 1 : 0);
+  check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), rsd ? resid->data_ptr() : y.data_ptr(), M, N, K, op, E,
+                         (long)N * K, epi, (int)algo, rp, rc, (int)rope_heads, rsp, rs_np, (float)rs_eps,
+                         rsd ? resid->data_ptr() : nullptr, rsd ? hw->data_ptr() : nullptr,
+                         rsd ? norm_w->data_ptr() : nullptr, rsd ? ss_out->data_ptr<float>() : nullptr, cur()),
         "gemm_tile");
 }
 
@@ -756,7 +787,9 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_tile", &gemm_tile, py::arg("y"), py::arg("x"), py::arg("w"), py::arg("offsets"), py::arg("swiglu"),
         py::arg("algo") = 1, py::arg("rope_pos") = py::none(), py::arg("rope_cs") = py::none(),
-        py::arg("rope_heads") = 0);
+        py::arg("rope_heads") = 0, py::arg("rs_part") = py::none(), py::arg("rs_eps") = 1e-5,
+        py::arg("resid") = py::none(), py::arg("hw") = py::none(), py::arg("norm_w") = py::none(),
+        py::arg("ss_out") = py::none());
   m.def("gelu_tanh", &gelu_tanh);
   m.def("embedding", &embedding);
   m.def("resolve_ids", &resolve_ids);

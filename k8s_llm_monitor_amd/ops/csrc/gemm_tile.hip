@@ -60,23 +60,50 @@ __device__ __forceinline__ void vm_wait_n() {
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 }  // namespace
 
-enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2 };
+enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2, TILE_EPI_RESID = 3 };
 
-// TILE_EPI_ROPE (the prefill qkv projection): the output columns are heads of 128; a wave's
-// 128-column quarter is exactly one head, and for q / k heads (head < rope_heads) the rotary
-// embedding (neox pairs i, i + 64) is applied to the staged bf16 rows before they are stored -
-// rope_cache's separate read-rotate-write pass over q / k disappears.
-struct TileRope {
-  const int* positions;  // [M] absolute position of each row
-  const float* cos_sin;  // [max_pos][128]: cos (64) | sin (64)
-  int rope_heads;        // Hq + Hkv: heads 0 .. rope_heads - 1 are rotated
+// Fused epilogues of the dense prefill projections.
+//
+// TILE_EPI_ROPE (the qkv projection): the output columns are heads of 128; a wave's 128-column
+// quarter is exactly one head, and for q / k heads (head < rope_heads) the rotary embedding (neox
+// pairs i, i + 64) is applied to the staged bf16 rows before they are stored - rope_cache's
+// separate read-rotate-write pass over q / k disappears.
+//
+// TILE_EPI_RESID (o / down, the residual producers): resid <- bf16(resid + bf16(y)) in place,
+// hw <- bf16(resid * norm_w) (the next RMSNorm's weighted input, NOT yet divided by the row's rms)
+// and ss_out[row][c] <- sum of resid^2 over the 128 columns c*128 .. c*128+127 - the fused
+// residual-add RMSNorm pass between two projections becomes part of the producer's epilogue.
+//
+// RS (row scale, the consumers qkv / gate_up that read hw): every output row is multiplied by
+// rsqrt(sum_c rs_part[row][c] / K + rs_eps) before its epilogue - the deferred half of the RMSNorm
+// (a row scale commutes with the projection; SwiGLU and RoPE see the normalised values).
+struct TileEpi {
+  const int* positions;  // ROPE: [M] absolute position of each row
+  const float* cos_sin;  // ROPE: [max_pos][128]: cos (64) | sin (64)
+  int rope_heads;        // ROPE: Hq + Hkv: heads 0 .. rope_heads - 1 are rotated
+  const float* rs_part;  // RS: [M][rs_np] partial sums of squares of the A rows
+  int rs_np;             // RS: partials per row (K / 128, <= 32)
+  float rs_eps;
+  bf16_t* resid;         // RESID: [M][N] residual stream, updated in place
+  bf16_t* hw;            // RESID: [M][N] resid * norm_w
+  const bf16_t* norm_w;  // RESID: [N] the next RMSNorm's weight
+  float* ss_out;         // RESID: [M][N / 128]
 };
 
-template <int EPI, bool GROUPED, int SCH>
+// sum over the 16 lanes of a DPP row (lanes 16r .. 16r + 15), the total in every lane
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));  // row_ror:2
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));  // row_ror:1
+  return v;
+}
+
+template <int EPI, bool GROUPED, int SCH, bool RS = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt,
-                                                         TileRope rope) {
+                                                         TileEpi ep) {
   constexpr int HS = 32768;  // one half-slot: 256 rows x 128 B
   __shared__ __attribute__((aligned(16))) char smem[5 * HS];
   const int lane = threadIdx.x & 63;
@@ -163,6 +190,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     return *reinterpret_cast<const bf16x8*>(smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + rd[ks]);
   };
 
+  float rs_inv = 1.f;  // RS: 1 / rms of this thread's row (threadIdx.x of the tile)
   f32x4 acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -216,6 +244,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
         }
       }
     };
+    // RS: this thread's row partials (row row0 + tid, clamped), loaded ahead of the prologue DMAs
+    // so their wait is the prologue's own (a fixed 8 loads: up to 32 partials, extra ones masked)
+    f32x4 rsq[RS ? 8 : 1];
+    if constexpr (RS) {
+      const float* rp = ep.rs_part + (long)(row0 + min((int)threadIdx.x, mrows - 1)) * ep.rs_np;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rsq[j] = *reinterpret_cast<const f32x4*>(rp + min(4 * j, ep.rs_np - 4));
+    }
     issue_half(0, 0);
     issue_half(1, 0);
     issue_half(0, 1);
@@ -223,6 +259,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     issue_half(0, 2);
     vm_wait_n<24>();
     __builtin_amdgcn_s_barrier();
+    if constexpr (RS) {
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (4 * j < ep.rs_np) sum += (rsq[j][0] + rsq[j][1]) + (rsq[j][2] + rsq[j][3]);
+      rs_inv = rsqrtf(sum / (float)K + ep.rs_eps);
+    }
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       fa0[g] = frag(0, 0, 0, g);
@@ -307,20 +350,44 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   lgkm_wait0();
   __builtin_amdgcn_s_barrier();  // every wave is done with the ring (its last DMAs retired above)
   constexpr int OUTW = EPI == TILE_EPI_SWIGLU ? 64 : 128;  // output columns of this wave's quarter
-  constexpr int RS = OUTW * 2 + 16;                        // LDS row stride (16-B pad: 2-way writes)
-  char* stage = smem + wave * (128 * RS);
+  constexpr int RS_ = OUTW * 2 + 16;                       // LDS row stride (16-B pad: 2-way writes)
+  char* stage = smem + wave * (128 * RS_);
   const int ml = lane & 15, nq = 4 * (lane >> 4);
+  // RESID: this lane's residual chunks (rows rr + 4b of the wave's 128, 16 B at column chunk cc),
+  // issued now so their latency hides behind the staging writes
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int rr = lane >> 4, cc = lane & 15;
+  u32x4 res[EPI == TILE_EPI_RESID ? 16 : 1];  // a rolling window of 16 chunks in flight
+  uint4 nwv{};
+  if constexpr (EPI == TILE_EPI_RESID) {
+    const __amdgpu_buffer_rsrc_t rres = rsrc(ep.resid + (long)row0 * N, (long)mrows * N * 2);
+    const uint32_t ro = (uint32_t)(((wm * 128 + rr) * N + n0 + wn * 128 + cc * 8) * 2);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) res[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * b * N * 2), 0, 0);
+    nwv = *reinterpret_cast<const uint4*>(ep.norm_w + n0 + wn * 128 + cc * 8);
+  }
+  // RS: each thread's row scale through LDS (after the staging area) to the lanes holding the row
+  float sc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sc[i] = 1.f;
+  if constexpr (RS) {
+    float* inv_s = reinterpret_cast<float*>(smem + 4 * 128 * (128 * 2 + 16));
+    inv_s[threadIdx.x] = rs_inv;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc[i] = inv_s[wm * 128 + i * 16 + ml];
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     __builtin_amdgcn_sched_barrier(0);  // one row block's accumulators at a time (no hoisted AGPR reads)
-    char* srow = stage + (i * 16 + ml) * RS + nq * 2;
+    char* srow = stage + (i * 16 + ml) * RS_ + nq * 2;
     if constexpr (EPI == TILE_EPI_SWIGLU) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float o[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float gt = bf2f(f2bf(acc[i][j][r])), up = bf2f(f2bf(acc[i][j + 4][r]));
+          const float gt = bf2f(f2bf(acc[i][j][r] * sc[i])), up = bf2f(f2bf(acc[i][j + 4][r] * sc[i]));
           o[r] = gt * up / (1.f + __expf(-gt));
         }
         *reinterpret_cast<uint2*>(srow + j * 32) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
@@ -328,15 +395,49 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const f32x4 v = acc[i][j];
+        const f32x4 v = acc[i][j] * sc[i];
         *reinterpret_cast<uint2*>(srow + j * 32) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
       }
     }
   }
   lgkm_wait0();
+  if constexpr (EPI == TILE_EPI_RESID) {
+    // lane (rr, cc): row rr + 4b, columns cc*8 .. +7 of the wave's quarter; N % 128 == 0 (host)
+    const __amdgpu_buffer_rsrc_t rres = rsrc(ep.resid + (long)row0 * N, (long)mrows * N * 2);
+    const __amdgpu_buffer_rsrc_t rhw = rsrc(ep.hw + (long)row0 * N, (long)mrows * N * 2);
+    const uint32_t ro = (uint32_t)(((wm * 128 + rr) * N + n0 + wn * 128 + cc * 8) * 2);
+    float wf[8];
+    unpack8(nwv, wf);
+    const int ss_np = N >> 7, ssc = (n0 + wn * 128) >> 7;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      const int r = rr + 4 * b;
+      const uint4 yv = *reinterpret_cast<const uint4*>(stage + r * RS_ + cc * 16);
+      float y[8], rv[8], h[8], hw[8];
+      unpack8(yv, y);
+      const u32x4 rb = res[b & 15];
+      if (b < 16) res[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * (b + 16) * N * 2), 0, 0);
+      unpack8(uint4{rb[0], rb[1], rb[2], rb[3]}, rv);
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        h[e] = bf2f(f2bf(y[e] + rv[e]));
+        ss += h[e] * h[e];
+        hw[e] = h[e] * wf[e];
+      }
+      const uint4 hq = pack8(h), wq = pack8(hw);
+      const uint32_t off = ro + (uint32_t)(4 * b * N * 2);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 0);
+      ss = row16_sum(ss);
+      const int grow = wm * 128 + r;
+      if (cc == 0 && grow < mrows) ep.ss_out[(long)(row0 + grow) * ss_np + ssc] = ss;
+    }
+    return;
+  }
   if constexpr (EPI == TILE_EPI_ROPE) {
     const int head = (n0 + wn * 128) >> 7;
-    if (head < rope.rope_heads && nrows - wn * 128 >= 128) {
+    if (head < ep.rope_heads && nrows - wn * 128 >= 128) {
       // one lane per (row, chunk pair c, c + 8): 8 rows per pass, 16 passes over the quarter's rows
       const int c = lane & 7, rsub = lane >> 3;
       bf16_t* ybase = Y + (long)row0 * N + n0 + wn * 128;
@@ -344,9 +445,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       for (int pass = 0; pass < 16; ++pass) {
         const int r = pass * 8 + rsub, grow = wm * 128 + r;
         if (grow >= mrows) continue;
-        const uint4 a = *reinterpret_cast<const uint4*>(stage + r * RS + c * 16);
-        const uint4 b = *reinterpret_cast<const uint4*>(stage + r * RS + (c + 8) * 16);
-        const float* cs = rope.cos_sin + (long)rope.positions[row0 + grow] * 128;
+        const uint4 a = *reinterpret_cast<const uint4*>(stage + r * RS_ + c * 16);
+        const uint4 b = *reinterpret_cast<const uint4*>(stage + r * RS_ + (c + 8) * 16);
+        const float* cs = ep.cos_sin + (long)ep.positions[row0 + grow] * 128;
         const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8), c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
         const float4 s0 = *reinterpret_cast<const float4*>(cs + 64 + c * 8),
                      s1 = *reinterpret_cast<const float4*>(cs + 64 + c * 8 + 4);
@@ -372,17 +473,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   const int ldy = EPI == TILE_EPI_SWIGLU ? (N >> 1) : N;
   const int col0 = EPI == TILE_EPI_SWIGLU ? ((n0 + wn * 128) >> 1) : n0 + wn * 128;
   const int ncols = EPI == TILE_EPI_SWIGLU ? (nrows >> 1) - wn * 64 : nrows - wn * 128;
-  const int rr = lane / CPR, cc = lane % CPR;
+  const int rr2 = lane / CPR, cc2 = lane % CPR;
   // branch-free masked stores: a buffer descriptor over this m-tile's rows drops every store past
   // row mrows (out of range), and a lane whose columns are past N gets an out-of-range offset
   const __amdgpu_buffer_rsrc_t yr = rsrc(Y + (long)row0 * ldy, (long)mrows * ldy * 2);
-  const uint32_t yo = cc * 8 < ncols ? (uint32_t)(((wm * 128 + rr) * ldy + col0 + cc * 8) * 2) : 0x80000000u;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t yo = cc2 * 8 < ncols ? (uint32_t)(((wm * 128 + rr2) * ldy + col0 + cc2 * 8) * 2) : 0x80000000u;
 #pragma unroll
   for (int b = 0; b < 128 / RPI; b += 8) {  // 8 row groups per batch: reads issued back to back
     u32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const u32x4*>(stage + ((b + u) * RPI + rr) * RS + cc * 16);
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const u32x4*>(stage + ((b + u) * RPI + rr2) * RS_ + cc2 * 16);
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       __builtin_amdgcn_raw_buffer_store_b128(v[u], yr, yo + (uint32_t)((b + u) * RPI * ldy * 2), 0, 0);
@@ -399,33 +499,49 @@ using namespace k8sllm;
 // Shapes: N % 16 == 0 (SwiGLU: N % 256 == 0), K % 64 == 0.  algo: the refill schedule (0 or 1).
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
                                 long w_es, int epi, int algo, const int* rope_pos, const float* rope_cs,
-                                int rope_heads, hipStream_t s) {
+                                int rope_heads, const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw,
+                                const void* norm_w, float* ss_out, hipStream_t s) {
   if (M <= 0) return 0;
   const bool grouped = offsets != nullptr;
+  const bool rs = rs_part != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
   if (algo < 0 || algo > 1) return -1;
   if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
   if (epi == TILE_EPI_ROPE && (grouped || N % 128 != 0 || rope_pos == nullptr || rope_cs == nullptr)) return -1;
-  const TileRope rope{rope_pos, rope_cs, rope_heads};
+  if (epi == TILE_EPI_RESID && (grouped || rs || N % 128 != 0 || resid == nullptr || hw == nullptr ||
+                                norm_w == nullptr || ss_out == nullptr || algo != 1))
+    return -1;
+  // row scale: the fused consumers only (qkv + RoPE, gate_up + SwiGLU), schedule 1
+  if (rs && (grouped || algo != 1 || rs_np < 4 || rs_np > 32 || rs_np % 4 != 0 ||
+             (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
+    return -1;
+  const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,
+                   (const bf16_t*)norm_w, ss_out};
   // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert / n-tile)
   if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
+  if (epi == TILE_EPI_RESID && 256L * N * 2 >= (1L << 31)) return -3;
   const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = (N + 255) / 256;
   const long nwg = (long)n_mt * n_nt;
   if (nwg > (1L << 30)) return -2;
   const dim3 grid((unsigned)nwg);
-#define K8_TILE_LAUNCH(EPI_, G_, SCH_)                                                                               \
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, SCH_>), grid, dim3(256), 0, s, (const bf16_t*)X, (const bf16_t*)W,   \
-                     (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt, rope)
+#define K8_TILE_LAUNCH(EPI_, G_, SCH_, RS_)                                                                          \
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, SCH_, RS_>), grid, dim3(256), 0, s, (const bf16_t*)X,                \
+                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt, ep)
 #define K8_TILE_SCH(SCH_)                                                                                            \
   if (grouped) {                                                                                                     \
-    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true, SCH_);                                         \
-    else K8_TILE_LAUNCH(TILE_EPI_BF16, true, SCH_);                                                                  \
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true, SCH_, false);                                  \
+    else K8_TILE_LAUNCH(TILE_EPI_BF16, true, SCH_, false);                                                           \
   } else {                                                                                                           \
-    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, SCH_);                                        \
-    else if (epi == TILE_EPI_ROPE) K8_TILE_LAUNCH(TILE_EPI_ROPE, false, SCH_);                                       \
-    else K8_TILE_LAUNCH(TILE_EPI_BF16, false, SCH_);                                                                 \
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, SCH_, false);                                 \
+    else if (epi == TILE_EPI_ROPE) K8_TILE_LAUNCH(TILE_EPI_ROPE, false, SCH_, false);                                \
+    else K8_TILE_LAUNCH(TILE_EPI_BF16, false, SCH_, false);                                                          \
   }
-  if (algo == 1) {
+  if (epi == TILE_EPI_RESID) {
+    K8_TILE_LAUNCH(TILE_EPI_RESID, false, 1, false);
+  } else if (rs) {
+    if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, 1, true);
+    else K8_TILE_LAUNCH(TILE_EPI_ROPE, false, 1, true);
+  } else if (algo == 1) {
     K8_TILE_SCH(1)
   } else {
     K8_TILE_SCH(0)

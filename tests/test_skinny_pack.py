@@ -162,3 +162,30 @@ def test_gemm_tile_rope_cpu_path():
     import pytest
     with pytest.raises(ValueError):
         ops.gemm_tile(x, w, swiglu=True, rope=(pos, cs, Hr))
+
+
+def test_fused_norm_epilogues_cpu_path():
+    """gemm_tile_resid (residual add + next RMSNorm's weighted input + per-128-column sums of
+    squares) followed by gemm_tile(rowscale=...) equals rms_norm(resid + x W^T) * w projected -
+    the CPU reference of the fused prefill norm (HIP numerics: test_tile_real_shapes_gpu.py)."""
+    from k8s_llm_monitor_amd.ops import reference as ref
+
+    torch.manual_seed(5)
+    M, d, F = 64, 256, 512
+    x = torch.randn(M, d, dtype=torch.bfloat16)
+    wo = (torch.randn(d, d) * 0.05).to(torch.bfloat16)
+    res = torch.randn(M, d, dtype=torch.bfloat16)
+    nw = (torch.rand(d) + 0.5).to(torch.bfloat16)
+    w13 = (torch.randn(2 * F, d) * 0.05).to(torch.bfloat16)
+    r0 = res.clone()
+    hw, ss = ops.gemm_tile_resid(x, wo, res, nw)
+    h = (torch.nn.functional.linear(x.float(), wo.float()).to(torch.bfloat16).float() + r0.float()).to(torch.bfloat16)
+    assert torch.equal(res, h)
+    torch.testing.assert_close(ss.sum(1), (h.float() ** 2).sum(1), rtol=1e-5, atol=1e-3)
+    y = ops.gemm_tile(hw, ops.interleave_gate_up(w13), swiglu=True, rowscale=(ss, 1e-5))
+    xn = ref.rms_norm(h, nw, 1e-5)
+    want = ops.silu_mul(torch.nn.functional.linear(xn.float(), w13.float()).to(torch.bfloat16))
+    torch.testing.assert_close(y.float(), want.float(), atol=3e-2, rtol=3e-2)
+    import pytest
+    with pytest.raises(ValueError):
+        ops.gemm_tile(hw, wo, rowscale=(ss, 1e-5))  # only the fused consumers take a row scale

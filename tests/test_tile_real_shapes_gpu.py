@@ -90,6 +90,49 @@ def test_tile_qkv_rope_epilogue_llama8b(M):
     assert rot and torch.equal(yp, y)
 
 
+@pytest.mark.parametrize("M", [1024, 1609])
+@pytest.mark.parametrize("K", [4096, 14336])
+def test_tile_resid_epilogue_llama8b(M, K):
+    """o / down with the residual add + next-RMSNorm operands in the epilogue (TILE_EPI_RESID) vs
+    fp32: resid updated in place, hw = resid * w, per-128-column sums of squares; ragged M."""
+    d = 4096
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(d, K, device=DEV) * 0.02).to(torch.bfloat16)
+    res = torch.randn(M, d, device=DEV, dtype=torch.bfloat16)
+    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+    r0 = res.clone()
+    hw, ss = ops.gemm_tile_resid(x, w, res, nw)
+    y = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    h = (y + r0.float()).to(torch.bfloat16).float()
+    assert _rel(res, h) < 1e-2
+    assert _rel(hw, (h * nw.float()).to(torch.bfloat16).float()) < 1e-2
+    torch.testing.assert_close(ss, (res.float() ** 2).view(M, d // 128, 128).sum(2), rtol=2e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1024, 1609])
+def test_tile_rowscale_consumers_llama8b(M):
+    """qkv + RoPE and gate_up + SwiGLU scaling their rows by the deferred RMSNorm (rs_part from the
+    producer epilogue) vs fp32 rms_norm -> projection."""
+    d, F, Hq, Hk = 4096, 14336, 32, 8
+    h = torch.randn(M, d, device=DEV, dtype=torch.bfloat16) * 3
+    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+    hw = (h.float() * nw.float()).to(torch.bfloat16)
+    ss = (h.float() ** 2).view(M, d // 128, 128).sum(2).contiguous()
+    xn = F_.rms_norm(h.float(), (d,), nw.float(), 1e-5)
+    wq = (torch.randn(6144, d, device=DEV) * 0.02).to(torch.bfloat16)
+    cs = ref.rope_cos_sin(4096, 128, 500000.0).to(DEV).float().contiguous()
+    pos = (torch.arange(M, device=DEV) % 4096).to(torch.int32)
+    y = ops.gemm_tile(hw, wq, algo=1, rope=(pos, cs, Hq + Hk), rowscale=(ss, 1e-5))
+    r = (xn @ wq.float().t()).to(torch.bfloat16).float()
+    qk = ref.apply_rope(r[:, : (Hq + Hk) * 128].view(M, Hq + Hk, 128), pos, cs).reshape(M, -1)
+    assert _rel(y[:, : (Hq + Hk) * 128], qk) < 1.5e-2
+    assert _rel(y[:, (Hq + Hk) * 128:], r[:, (Hq + Hk) * 128:]) < 1.5e-2
+    w13 = (torch.randn(2 * F, d, device=DEV) * 0.02).to(torch.bfloat16)
+    a = ops.gemm_tile(hw, ops.interleave_gate_up(w13).contiguous(), swiglu=True, algo=1, rowscale=(ss, 1e-5))
+    gu = (xn @ w13.float().t()).to(torch.bfloat16).float()
+    assert _rel(a, F_.silu(gu[:, :F]) * gu[:, F:]) < 2e-2
+
+
 def _fp32_forward(model, ids):
     """Plain fp32 forward of the same weights (no HIP kernels): last-token logits."""
     c = model.cfg
@@ -130,23 +173,31 @@ def test_engine_llama8b_two_layers_chunked_tile_prefill_matches_fp32(prompt_len,
     projections run on gemm_tile (K8SLLM_PREFILL_GEMM=tile: M >= TILE_MIN_M) inside
     CausalLM.forward; the first sampled token must be the fp32 argmax or a near-tie."""
     monkeypatch.setattr(ops, "PREFILL_GEMM", "tile")
+    monkeypatch.setattr(ops, "FUSED_NORM", True)
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
 
     eng = LLMEngine(EngineConfig(model="llama-3-8b", model_overrides={"n_layers": 2}, max_num_seqs=4,
                                  max_model_len=4096, max_prefill_tokens=1024, chunked_prefill=True,
                                  num_blocks=1024, use_graphs=False, seed=11), device=DEV)
-    calls = {"tile": 0}
-    orig = ops.gemm_tile
+    calls = {"tile": 0, "resid": 0}
+    orig, orig_r = ops.gemm_tile, ops.gemm_tile_resid
 
     def counting(*a, **k):
         calls["tile"] += 1
         return orig(*a, **k)
 
+    def counting_r(*a, **k):
+        calls["resid"] += 1
+        return orig_r(*a, **k)
+
     monkeypatch.setattr(ops, "gemm_tile", counting)
+    monkeypatch.setattr(ops, "gemm_tile_resid", counting_r)
     g = torch.Generator().manual_seed(prompt_len)
     ids = torch.randint(10, 120000, (prompt_len,), generator=g).tolist()
     seq = eng.generate([ids], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))[0]
-    assert calls["tile"] >= 4 * 2, calls  # qkv (+ RoPE) / o / gate_up / down of both layers on the tile kernel
+    # qkv (+ RoPE) / o / gate_up / down of both layers on the tile kernel, the RMSNorms between
+    # them folded into the o / down epilogues (gemm_tile_resid) and the qkv / gate_up row scale
+    assert calls["tile"] + calls["resid"] >= 4 * 2 and calls["resid"] >= 3, calls
     lg = _fp32_forward(eng.model, torch.tensor(ids, device=DEV))
     tok = seq.output_ids[0]
     top = lg.max()
