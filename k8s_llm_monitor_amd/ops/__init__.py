@@ -919,7 +919,7 @@ def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_
 PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "tile")
 QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fused RoPE on the tile kernel
 # residual-add RMSNorm folded into the o / down epilogues and the qkv / gate_up row scale
-FUSED_NORM = os.environ.get("K8SLLM_FUSED_NORM", "0") != "0"
+FUSED_NORM = os.environ.get("K8SLLM_FUSED_NORM", "1") != "0"
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 TILE_ALGO = 1  # refill schedule: two barriers per k-tile
 
