@@ -40,7 +40,7 @@ def main() -> None:
     ap.add_argument("--ms", default="1,32,64")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ops", default="qkv,o,gate_up,down,lm_head")
-    ap.add_argument("--cfgs", default=None, help="op:S,NTW,W,D;... overrides the sweep list")
+    ap.add_argument("--cfgs", default=None, help="op:S,NTW,W,D|S,NTW,W,D;... overrides the sweep list")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -48,7 +48,7 @@ def main() -> None:
     if a.cfgs:
         for item in a.cfgs.split(";"):
             op, c = item.split(":")
-            cfgs[op] = [tuple(int(v) for v in c.split(","))]
+            cfgs[op] = [tuple(int(v) for v in cc.split(",")) for cc in c.split("|")]
     for name in a.ops.split(","):
         N, K, epi = SHAPES[name]
         ncopy = max(2, (512 << 20) // (N * K * 2) + 1)
