@@ -104,9 +104,8 @@ class ModelRunner:
         raise ValueError(f"batch {n} exceeds max_num_seqs {self.B}")
 
     def _sample(self, logits: torch.Tensor, temp, topk, topp, out=None) -> torch.Tensor:
-        tok = ops.sample(logits, temp, topk, topp, self.rng, out=out)
-        self.rng[1:] += 1  # fresh numbers next step (also inside a captured graph)
-        return tok
+        # fresh numbers next step: the counter advances inside the sampling kernel (also in a graph)
+        return ops.sample(logits, temp, topk, topp, self.rng, out=out, advance=True)
 
     # --------------------------------------------------------------------- prefill
     def prefill(self, seqs: list[Sequence], decode: Optional[list] = None) -> list[int]:

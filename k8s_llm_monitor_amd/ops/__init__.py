@@ -721,14 +721,18 @@ def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int
 
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None, top_k: Optional[torch.Tensor] = None,
            top_p: Optional[torch.Tensor] = None, rng: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Next tokens [B] int32.  temperature <= 0 (or None) is greedy."""
+           out: Optional[torch.Tensor] = None, advance: bool = False) -> torch.Tensor:
+    """Next tokens [B] int32.  temperature <= 0 (or None) is greedy.  ``advance``: bump the RNG
+    counter ``rng[1]`` after drawing (on the GPU inside the final sampling kernel - no extra
+    launch inside a captured decode step)."""
     if not _gpu(logits):
         r = _sample_cpu(logits, temperature, top_k, top_p, rng)
+        if advance and rng is not None:
+            rng[1] += 1
         return out.copy_(r) if out is not None else r
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
-    native().sample(out, logits, temperature, top_k, top_p, rng)
+    native().sample(out, logits, temperature, top_k, top_p, rng, advance and rng is not None)
     return out
 
 

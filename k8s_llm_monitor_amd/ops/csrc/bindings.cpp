@@ -30,7 +30,7 @@ int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_s
                          const int* ctx_start, const void* k_cache, const void* v_cache, const int* block_tables,
                          int bt_stride, hipStream_t s);
 int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V, const float* temps,
-                  const int* top_k, const float* top_p, const int64_t* rng, float* pv, int* pi, hipStream_t s);
+                  const int* top_k, const float* top_p, const int64_t* rng, float* pv, int* pi, int advance, hipStream_t s);
 int k8sllm_sample_parts(long B, int V);
 int k8sllm_moe_route(const void* logits, long T, int E, int K, int renorm, int* topk_ids, float* topk_w,
                      hipStream_t s);
@@ -294,7 +294,8 @@ void flash_prefill(torch::Tensor out, torch::Tensor qkv, torch::Tensor cu_seqlen
 }
 
 void sample(torch::Tensor out, torch::Tensor logits, c10::optional<torch::Tensor> temps,
-            c10::optional<torch::Tensor> top_k, c10::optional<torch::Tensor> top_p, c10::optional<torch::Tensor> rng) {
+            c10::optional<torch::Tensor> top_k, c10::optional<torch::Tensor> top_p, c10::optional<torch::Tensor> rng,
+            bool advance) {
   dev_i32(out, "out");
   TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
   const bool f32 = logits.scalar_type() == torch::kFloat32;
@@ -310,7 +311,7 @@ void sample(torch::Tensor out, torch::Tensor logits, c10::optional<torch::Tensor
   auto pv = torch::empty({np}, logits.options().dtype(torch::kFloat32));
   auto pi = torch::empty({np}, logits.options().dtype(torch::kInt32));
   check(k8sllm_sample(out.data_ptr<int>(), logits.data_ptr(), f32 ? 1 : 0, B, logits.stride(0), V, t, k, p, r,
-                      pv.data_ptr<float>(), pi.data_ptr<int>(), cur()),
+                      pv.data_ptr<float>(), pi.data_ptr<int>(), advance ? 1 : 0, cur()),
         "sample");
 }
 
@@ -797,7 +798,8 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);
   m.def("flash_prefill", &flash_prefill);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),
+        py::arg("rng"), py::arg("advance") = false);
   m.def("moe_route", &moe_route);
   m.def("moe_align", &moe_align);
   m.def("moe_combine", &moe_combine);

@@ -181,8 +181,12 @@ __global__ __launch_bounds__(64) void sample_final_kernel(int* __restrict__ out,
                                                           const int* __restrict__ pi, int B, int V, int P,
                                                           const float* __restrict__ temps,
                                                           const int* __restrict__ top_k,
-                                                          const float* __restrict__ top_p) {
+                                                          const float* __restrict__ top_p,
+                                                          int64_t* __restrict__ rng_advance) {
   const int row = blockIdx.x * 64 + threadIdx.x;
+  // the partial kernel has drawn this step's numbers: advance the counter for the next step here
+  // (one lane, a vector store) instead of a separate `rng[1] += 1` launch after every sample
+  if (rng_advance != nullptr && row == 0) rng_advance[1] = rng_advance[1] + 1;
   if (row >= B) return;
   const float temp = temps ? temps[row] : 0.f;
   const int k = top_k ? top_k[row] : 0;
@@ -211,7 +215,7 @@ extern "C" int k8sllm_sample_parts(long B, int V) {
 // pv/pi: workspace of at least B * k8sllm_sample_parts(B, V) entries
 extern "C" int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride, int V,
                              const float* temps, const int* top_k, const float* top_p, const int64_t* rng,
-                             float* pv, int* pi, hipStream_t s) {
+                             float* pv, int* pi, int advance, hipStream_t s) {
   if (B <= 0) return 0;
   const int P = k8sllm_sample_parts(B, V);
   dim3 grid((unsigned)B, P);
@@ -222,6 +226,6 @@ extern "C" int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, 
     hipLaunchKernelGGL((sample_partial_kernel<bf16_t>), grid, dim3(kST), 0, s, pv, pi, (const bf16_t*)logits,
                        stride, V, P, temps, top_k, top_p, rng);
   hipLaunchKernelGGL(sample_final_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, out, pv, pi, (int)B, V, P,
-                     temps, top_k, top_p);
+                     temps, top_k, top_p, advance && rng ? const_cast<int64_t*>(rng) : nullptr);
   return (int)hipGetLastError();
 }

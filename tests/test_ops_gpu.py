@@ -223,6 +223,35 @@ def test_sample_distribution():
     assert torch.allclose(freq, torch.softmax(base, 0), atol=0.03)
 
 
+def test_sample_advances_rng_in_kernel_and_graph():
+    """advance=True bumps rng[1] inside the final sampling kernel: eager and hipGraph replays draw
+    a fresh counter each time (the engine no longer launches a separate increment)."""
+    B, V = 8, 32000
+    logits = torch.randn(B, V, device=DEV)
+    temps = torch.full((B,), 1.0, device=DEV)
+    rng = torch.tensor([11, 5], device=DEV, dtype=torch.int64)
+    a = ops.sample(logits, temps, None, None, rng, advance=True).clone()
+    assert int(rng[1]) == 6 and int(rng[0]) == 11
+    out = torch.empty(B, dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.sample(logits, temps, None, None, rng, out=out, advance=True)  # warm-up allocation
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.sample(logits, temps, None, None, rng, out=out, advance=True)
+    rng[1] = 5
+    draws = []
+    for _ in range(3):
+        g.replay()
+        draws.append(out.clone())
+    torch.cuda.synchronize()
+    assert int(rng[1]) == 8
+    assert torch.equal(draws[0], a)  # replay 1 drew with counter 5, like the eager call
+    assert not (torch.equal(draws[0], draws[1]) and torch.equal(draws[1], draws[2]))
+
+
 def test_moe_route_align_combine():
     T, E, K, d = 300, 8, 2, 256
     logits = torch.randn(T, E, device=DEV)
