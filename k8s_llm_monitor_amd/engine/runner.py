@@ -69,7 +69,6 @@ class ModelRunner:
         self.d_src.fill_(-1)
         self.d_slots.fill_(-1)
         self.d_topp.fill_(1.0)
-        self.d_rids = torch.zeros(B, dtype=torch.int32, device=dev)  # resolved input ids (graph-internal)
         self.rng = torch.tensor([cfg.seed, 0], dtype=torch.int64, device=dev)
         self.d_out = torch.zeros(B, dtype=torch.int32, device=dev)
         self.decode_ws = ops.decode_workspace(B, model.hq, D, self.max_blocks_per_seq * BLOCK_SIZE, dev, model.hkv) \
@@ -227,13 +226,13 @@ class ModelRunner:
 
     # --------------------------------------------------------------------- decode
     def _decode_body(self, b: int) -> None:
-        meta = AttnMeta(is_prefill=False, positions=self.d_pos[:b], slot_mapping=self.d_slots[:b],
-                        block_tables=self.d_bt[:b], seq_lens=self.d_lens[:b], decode_ws=self.decode_ws)
         # pipelined decode: a row whose input is the token sampled by the previous step (still in
         # flight when this step was enqueued) takes it from d_out on the device (d_src = its row
-        # there); other rows take the host-provided id
-        ids = ops.resolve_ids(self.d_ids[:b], self.d_src[:b], self.d_out, out=self.d_rids[:b])
-        logits = self.model.forward(ids, meta, self.kv)
+        # there); other rows take the host-provided id - resolved by the model's first kernel
+        meta = AttnMeta(is_prefill=False, positions=self.d_pos[:b], slot_mapping=self.d_slots[:b],
+                        block_tables=self.d_bt[:b], seq_lens=self.d_lens[:b], decode_ws=self.decode_ws,
+                        dec_src=self.d_src[:b], dec_prev=self.d_out)
+        logits = self.model.forward(self.d_ids[:b], meta, self.kv)
         self._sample(logits, self.d_temp[:b], self.d_topk[:b], self.d_topp[:b], out=self.d_out[:b])
 
     def capture_graphs(self, buckets: Optional[list[int]] = None) -> None:

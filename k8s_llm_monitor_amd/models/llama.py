@@ -65,6 +65,10 @@ class AttnMeta:
     num_decode: int = 0
     dec_block_tables: Optional[torch.Tensor] = None  # [num_decode, W] int32
     dec_seq_lens: Optional[torch.Tensor] = None  # [num_decode] int32 (including the decoded token)
+    # pipelined decode inputs: row i feeds dec_prev[dec_src[i]] when dec_src[i] >= 0 (the token the
+    # previous step sampled, still on the device), else ids[i]; resolved inside the first kernel
+    dec_src: Optional[torch.Tensor] = None  # [B] int32
+    dec_prev: Optional[torch.Tensor] = None  # [>= B] int32
 
 
 def _seed_for(name: str, seed: int) -> int:
@@ -496,6 +500,14 @@ class CausalLM:
         """Returns logits [rows, vocab_size] for the rows selected by ``meta.logits_idx`` (all rows
         when None)."""
         c = self.cfg
+        if meta.dec_src is not None:
+            if (self.tp == 1 and ids.is_cuda and c.arch != "gpt2" and self._use_skinny(meta, ids)
+                    and c.d_model % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0"):
+                # decode front end in one launch: ids -> embedding -> layer 0's deferred-norm operands
+                residual, xw, ss = ops.embed_norm_partial(ids, self.embed, self.layers[0]["attn_norm"],
+                                                          meta.dec_src, meta.dec_prev)
+                return self._decode_layers_skinny(None, residual, meta, kv_caches, first=(xw, (ss, c.norm_eps)))
+            ids = ops.resolve_ids(ids, meta.dec_src, meta.dec_prev)
         h = self.embed_tokens(ids)
         if c.arch == "gpt2":
             h = h + self.pos_embed[meta.positions.long()]
@@ -673,7 +685,7 @@ class CausalLM:
         self._skinny_ws = torch.empty(n * rows, dtype=torch.float32, device=self.device)
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
-                              kv_caches: Optional[list]) -> torch.Tensor:
+                              kv_caches: Optional[list], first: Optional[tuple] = None) -> torch.Tensor:
         """Activations between the skinny GEMMs travel fragment-packed (whole-line A loads): the
         attention output (paged_decode) and the MLP activation (SwiGLU epilogue) are written in the
         A-operand layout, and every RMSNorm is deferred: add_norm_partial writes residual * w plus
@@ -681,7 +693,8 @@ class CausalLM:
         c, ws, n = self.cfg, self._skinny_ws, len(self.layers)
         eps = c.norm_eps
         M = residual.shape[0]
-        xw, rn = self._norm_tail(residual, None, 0, self.layers[0]["attn_norm"])
+        # first = layer 0's (A operand, rownorm), already produced with the embedding (embed_norm_partial)
+        xw, rn = first if first is not None else self._norm_tail(residual, None, 0, self.layers[0]["attn_norm"])
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)

@@ -562,6 +562,27 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, vocab_start: int = 0,
     return out
 
 
+def embed_norm_partial(ids: torch.Tensor, weight: torch.Tensor, norm_w: torch.Tensor,
+                       src: Optional[torch.Tensor] = None, prev: Optional[torch.Tensor] = None,
+                       packed: bool = True) -> tuple:
+    """The decode step's front end: the (pipelined, see :func:`resolve_ids`) input ids' embedding
+    rows and the first layer's deferred-norm operands - ``(residual [M, d], residual * norm_w
+    (fragment-packed), ss_part [M, d/512])``, what embedding + add_norm_partial(nslabs=0) return,
+    in one launch."""
+    M, d = ids.numel(), weight.shape[1]
+    if not _gpu(weight):
+        if src is not None:
+            ids = resolve_ids(ids, src, prev)
+        res = ref.embedding(ids, weight, 0).contiguous()
+        xw, ss = add_norm_partial(res, None, 0, norm_w, packed=packed)
+        return res, xw, ss
+    res = torch.empty(M, d, dtype=weight.dtype, device=weight.device)
+    ss = torch.empty(M, d // 512, dtype=torch.float32, device=weight.device)
+    out = packed_empty(M, d, weight.dtype, weight.device) if packed else torch.empty_like(res)
+    native().embed_norm_partial(out, res, ids, src, prev, weight, norm_w, ss)
+    return res, out, ss
+
+
 def resolve_ids(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Decode input ids under pipelining: ``prev[src[i]]`` where ``src[i] >= 0`` (the token the

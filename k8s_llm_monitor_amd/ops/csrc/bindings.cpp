@@ -55,6 +55,9 @@ int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long
                     hipStream_t s);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
+int k8sllm_embed_norm_partial(void* out, long out_stride, void* residual, const int* ids, const int* src,
+                              const int* prev, const void* emb, int vocab, const void* w, int M, int d,
+                              float* ss_part, hipStream_t s);
 int k8sllm_gemm_skinny_slabs(int K, int S);
 int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
@@ -650,6 +653,38 @@ int64_t gemm_skinny_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<tor
 
 // residual += sum of S slabs; out = residual * w (row-major or fragment-packed); ss_part[m][c] =
 // sum of residual^2 over columns [512 c, 512 c + 512) - the deferred-RMSNorm producer.
+// decode front end: resolved ids -> embedding rows (residual) + the first layer's deferred-norm operands
+void embed_norm_partial(torch::Tensor out, torch::Tensor residual, torch::Tensor ids, c10::optional<torch::Tensor> src,
+                        c10::optional<torch::Tensor> prev, torch::Tensor emb, torch::Tensor w, torch::Tensor ss_part) {
+  dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(emb, "emb"); dev_bf16(w, "w"); dev_i32(ids, "ids");
+  TORCH_CHECK(residual.is_contiguous() && residual.dim() == 2 && emb.is_contiguous() && emb.dim() == 2 &&
+                  w.is_contiguous(), "embed_norm_partial layout");
+  const int M = (int)residual.size(0), d = (int)residual.size(1);
+  TORCH_CHECK(d % 512 == 0 && emb.size(1) == d && w.numel() == d && ids.numel() >= M, "embed_norm_partial shapes");
+  TORCH_CHECK(src.has_value() == prev.has_value(), "embed_norm_partial: src and prev go together");
+  const int* sp = nullptr;
+  const int* pp = nullptr;
+  if (src.has_value()) {
+    dev_i32(*src, "src"); dev_i32(*prev, "prev");
+    TORCH_CHECK(src->numel() >= M, "embed_norm_partial: src [M]");
+    sp = src->data_ptr<int>();
+    pp = prev->data_ptr<int>();
+  }
+  TORCH_CHECK(ss_part.is_cuda() && ss_part.scalar_type() == torch::kFloat32 && ss_part.is_contiguous() &&
+                  ss_part.numel() >= (int64_t)M * (d / 512), "ss_part");
+  long ostride = d;
+  if (out.dim() == 4) {
+    TORCH_CHECK(out.size(0) == (M + 15) / 16 && out.size(1) * 32 == d && out.size(2) == 64 && out.size(3) == 8,
+                "packed out must be [ceil(M/16), d/32, 64, 8]");
+    ostride = -(long)(d / 32);
+  } else {
+    TORCH_CHECK(out.numel() == (int64_t)M * d, "out shape");
+  }
+  check(k8sllm_embed_norm_partial(out.data_ptr(), ostride, residual.data_ptr(), ids.data_ptr<int>(), sp, pp,
+                                  emb.data_ptr(), (int)emb.size(0), w.data_ptr(), M, d, ss_part.data_ptr<float>(), cur()),
+        "embed_norm_partial");
+}
+
 void add_norm_partial(torch::Tensor out, torch::Tensor residual, c10::optional<torch::Tensor> partial, int64_t S,
                       torch::Tensor w, torch::Tensor ss_part) {
   dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
@@ -798,6 +833,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);
   m.def("flash_prefill", &flash_prefill);
+  m.def("embed_norm_partial", &embed_norm_partial);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),
         py::arg("rng"), py::arg("advance") = false);
   m.def("moe_route", &moe_route);

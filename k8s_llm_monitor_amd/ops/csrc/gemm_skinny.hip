@@ -605,6 +605,44 @@ __global__ __launch_bounds__(64) void add_norm_partial_kernel(bf16_t* __restrict
   if (threadIdx.x == 0) ss_part[row * (d / 512) + chunk] = ss;
 }
 
+// The decode step's front end in one launch (grid (M, d/512), one wave per 512 columns): the row's
+// input id - prev[src[row]] when src[row] >= 0 (the token the previous, possibly still running,
+// step sampled: pipelined decode), else ids[row] - its embedding row -> residual, and the first
+// layer's deferred RMSNorm operands as add_norm_partial writes them (residual * w, packed via
+// act_index; per-512-column sums of squares).  Replaces resolve_ids + embedding + add_norm_partial.
+__global__ __launch_bounds__(64) void embed_norm_partial_kernel(bf16_t* __restrict__ out, long out_stride,
+                                                                bf16_t* __restrict__ residual,
+                                                                const int* __restrict__ ids,
+                                                                const int* __restrict__ src,
+                                                                const int* __restrict__ prev,
+                                                                const bf16_t* __restrict__ emb, int vocab,
+                                                                const bf16_t* __restrict__ w, int d,
+                                                                float* __restrict__ ss_part) {
+  const int row = blockIdx.x, chunk = blockIdx.y;
+  const int col = chunk * 512 + threadIdx.x * 8;
+  int id = ids[row];
+  if (src != nullptr) {
+    const int r = src[row];
+    if (r >= 0) id = prev[r];
+  }
+  const bool in = id >= 0 && id < vocab;
+  const uint4 ev = in ? *reinterpret_cast<const uint4*>(emb + (long)id * d + col) : make_uint4(0, 0, 0, 0);
+  const uint4 wv = *reinterpret_cast<const uint4*>(w + col);
+  *reinterpret_cast<uint4*>(residual + (long)row * d + col) = ev;
+  float v[8], wf[8], o[8];
+  unpack8(ev, v);
+  unpack8(wv, wf);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss += v[j] * v[j];
+    o[j] = v[j] * wf[j];
+  }
+  *reinterpret_cast<uint4*>(out + act_index(row, col, out_stride)) = pack8(o);
+  ss = wave_sum(ss);
+  if (threadIdx.x == 0) ss_part[row * (d / 512) + chunk] = ss;
+}
+
 // out[i] = bf16(sum_s partial[s][i]) over n elements (n % 8 == 0): the TP>1 decode tails sum
 // the split-K slabs before the RCCL all-reduce.
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(bf16_t* __restrict__ out,
@@ -642,6 +680,16 @@ extern "C" int k8sllm_add_norm_partial(void* out, long out_stride, void* residua
     default: K8S_ANP(0); break;
   }
 #undef K8S_ANP
+  return (int)hipGetLastError();
+}
+
+extern "C" int k8sllm_embed_norm_partial(void* out, long out_stride, void* residual, const int* ids, const int* src,
+                                         const int* prev, const void* emb, int vocab, const void* w, int M, int d,
+                                         float* ss_part, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (d % 512 != 0) return -1;
+  hipLaunchKernelGGL(embed_norm_partial_kernel, dim3(M, d / 512), dim3(64), 0, s, (bf16_t*)out, out_stride,
+                     (bf16_t*)residual, ids, src, prev, (const bf16_t*)emb, vocab, (const bf16_t*)w, d, ss_part);
   return (int)hipGetLastError();
 }
 

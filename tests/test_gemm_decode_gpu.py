@@ -97,3 +97,23 @@ def test_dec_bf16_lm_head(M, cfg):
     ref = x.float() @ w.float().t()
     _check(y, ref, f"lm_head M{M} cfg{cfg}")
     assert not torch.isnan(y).any(), "every column written (the ragged last workgroup included)"
+
+
+@pytest.mark.parametrize("M", [1, 37, 64])
+def test_embed_norm_partial_matches_resolve_embed_norm(M):
+    """The decode front end in one launch (embed_norm_partial) equals resolve_ids -> embedding ->
+    add_norm_partial(nslabs=0): residual rows, packed residual * w, per-512-column sums of squares."""
+    V, d = 1000, 4096
+    emb = torch.randn(V, d, device=DEV, dtype=torch.bfloat16)
+    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+    ids = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
+    prev = torch.randint(0, V, (64,), device=DEV, dtype=torch.int32)
+    src = torch.where(torch.rand(M, device=DEV) < 0.5, torch.randint(0, 64, (M,), device=DEV),
+                      torch.full((M,), -1, device=DEV)).to(torch.int32)
+    res, xw, ss = ops.embed_norm_partial(ids, emb, nw, src, prev)
+    rid = ops.resolve_ids(ids, src, prev)
+    r0 = ops.embedding(rid, emb)
+    xw0, ss0 = ops.add_norm_partial(r0.clone(), None, 0, nw)
+    assert torch.equal(res, r0)
+    assert torch.equal(ops.unpack_skinny(xw)[:M], ops.unpack_skinny(xw0)[:M])
+    torch.testing.assert_close(ss, ss0, rtol=1e-5, atol=1e-4)
