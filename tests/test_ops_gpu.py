@@ -223,6 +223,20 @@ def test_sample_distribution():
     assert torch.allclose(freq, torch.softmax(base, 0), atol=0.03)
 
 
+@pytest.mark.parametrize("T", [0.1, 0.7, 1.0, 3.0])
+def test_sample_gumbel_skip_is_exact(T):
+    """The partial kernel evaluates the Gumbel noise only where x / T is within the noise's range of
+    the part's maximum; the whole-row (filtered) path evaluates it everywhere with the same hash.
+    With top_k = V - 1 (drops only the smallest logit) both must pick the same token."""
+    B, V = 64, 128256
+    logits = (torch.randn(B, V, device=DEV) * 1.3).to(torch.bfloat16)
+    temps = torch.full((B,), T, device=DEV)
+    rng = torch.tensor([99, 7], device=DEV, dtype=torch.int64)
+    fast = ops.sample(logits, temps, None, None, rng)
+    full = ops.sample(logits, temps, torch.full((B,), V - 1, device=DEV, dtype=torch.int32), None, rng)
+    assert torch.equal(fast, full)
+
+
 def test_sample_advances_rng_in_kernel_and_graph():
     """advance=True bumps rng[1] inside the final sampling kernel: eager and hipGraph replays draw
     a fresh counter each time (the engine no longer launches a separate increment)."""
