@@ -251,9 +251,6 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     else if (ntw == 4 && waves == 4 && depth == 8) { K8S_DEC_M(4, 4, DEC_SLAB, 8) }
     else if (ntw == 3 && waves == 8 && depth == 8) { K8S_DEC_M(3, 8, DEC_SLAB, 8) }
     else if (ntw == 1 && waves == 4 && depth == 8) { K8S_DEC_M(1, 4, DEC_SLAB, 8) }
-    // a wave's whole K slice in one ring turn (o / qkv at 8 splits: 16 k-steps; down at 14: 32)
-    else if (ntw == 1 && waves == 8 && depth == 16) { K8S_DEC_M(1, 8, DEC_SLAB, 16) }
-    else if (ntw == 1 && waves == 8 && depth == 32) { K8S_DEC_M(1, 8, DEC_SLAB, 32) }
   } else if (epi == DEC_SWIGLU8) {
     if (ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 16) }
     else if (ntw == 1 && waves == 8 && depth == 16) { K8S_DEC_M(1, 8, DEC_SWIGLU8, 16) }

@@ -48,10 +48,15 @@ __device__ __forceinline__ uint64_t row_key(const int64_t* rng, int row) {
   return mix64(seed ^ mix64(off * 0x100000001b3ull + (uint64_t)row * 0x9e3779b97ull));
 }
 
+// Standard Gumbel noise -log(-log(u)).  u is drawn as 1 - w with w = (23-bit hash + 0.5) / 2^23,
+// so w lies in [2^-24, 1 - 2^-24] and -log(u) = -log1p(-w) stays accurate (and > 0) as u -> 1.
+// (The earlier 24-bit u = (h + 0.5) / 2^24 rounded to exactly 1.0f for the top hash value, and the
+// fast log of 1 is 0: a +inf noise that made an arbitrary token win - about once per two 64-row
+// steps of a 128K vocabulary.)  Range: [-log(16.64), 16.64] = [-2.81, 16.64].
 __device__ __forceinline__ float gumbel(uint64_t key, int i) {
   const uint32_t h = fmix32(fmix32((uint32_t)i * 0x9e3779b9u ^ (uint32_t)key) + (uint32_t)(key >> 32));
-  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
-  return -__logf(-__logf(u));
+  const float w = ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
+  return -logf(-log1pf(-w));
 }
 
 struct ArgMax {
@@ -166,10 +171,10 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
     for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i), i});
   } else {
     // Gumbel-max with the hash and the two logs only where they can matter: gumbel() lies in
-    // [-log(log(2^25)), log(2^25) - ...] = [-2.86, 17.33] for every u the 24-bit hash yields, so an
-    // element whose x / T is more than kGumbelSpan below the part's largest x / T can never beat
-    // the element holding it (at T = 0.1 that skips ~99 % of a 128K vocabulary).  Exact.
-    constexpr float kGumbelSpan = 20.5f;  // 17.33 + 2.86, plus slack for __logf's error
+    // [-2.81, 16.64] for every hash value, so an element whose x / T is more than kGumbelSpan below
+    // the part's largest x / T can never beat the element holding it (at T = 0.1 that skips ~99 %
+    // of a 128K vocabulary).  Exact.
+    constexpr float kGumbelSpan = 20.5f;  // 16.64 + 2.81, plus slack
     const float itemp = 1.f / temp;
     const uint64_t key = row_key(rng, row);
     float mx = -INFINITY;
