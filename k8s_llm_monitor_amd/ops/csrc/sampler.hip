@@ -14,6 +14,7 @@
 // path and its answer is taken as is.  The per-element hash is 32-bit (two murmur3 finalisers of
 // a per-row 64-bit key) - 64-bit multiplies are multi-instruction sequences on CDNA.
 #include "common.h"
+#include <stdlib.h>
 
 namespace k8sllm {
 
@@ -49,14 +50,17 @@ __device__ __forceinline__ uint64_t row_key(const int64_t* rng, int row) {
 }
 
 // Standard Gumbel noise -log(-log(u)).  u is drawn as 1 - w with w = (23-bit hash + 0.5) / 2^23,
-// so w lies in [2^-24, 1 - 2^-24] and -log(u) = -log1p(-w) stays accurate (and > 0) as u -> 1.
+// so w lies in [2^-24, 1 - 2^-24] and -log(u) = -log(1 - w) is taken by its series for small w:
+// accurate and > 0 as u -> 1.
 // (The earlier 24-bit u = (h + 0.5) / 2^24 rounded to exactly 1.0f for the top hash value, and the
 // fast log of 1 is 0: a +inf noise that made an arbitrary token win - about once per two 64-row
 // steps of a 128K vocabulary.)  Range: [-log(16.64), 16.64] = [-2.81, 16.64].
 __device__ __forceinline__ float gumbel(uint64_t key, int i) {
   const uint32_t h = fmix32(fmix32((uint32_t)i * 0x9e3779b9u ^ (uint32_t)key) + (uint32_t)(key >> 32));
   const float w = ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
-  return -logf(-log1pf(-w));
+  // -log(1 - w): the series w + w^2 / 2 below 2^-10 (relative error < 4e-7), the fast log above
+  const float e = w < 0x1p-10f ? __builtin_fmaf(0.5f * w, w, w) : -__logf(1.f - w);
+  return -__logf(e);
 }
 
 struct ArgMax {
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
                                                              const float* __restrict__ temps,
                                                              const int* __restrict__ top_k,
                                                              const float* __restrict__ top_p,
-                                                             const int64_t* __restrict__ rng) {
+                                                             const int64_t* __restrict__ rng, int skip) {
   __shared__ float sv[kST / 64];
   __shared__ int si[kST / 64];
   const int row = blockIdx.x, part = blockIdx.y, tid = threadIdx.x;
@@ -178,8 +182,9 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
     const float itemp = 1.f / temp;
     const uint64_t key = row_key(rng, row);
     float mx = -INFINITY;
-    for (int i = lo + tid; i < hi; i += kST) mx = fmaxf(mx, ld<T>(x, i));
-    const float thr = block_max<kST>(mx, sv) * itemp - kGumbelSpan;
+    if (skip)
+      for (int i = lo + tid; i < hi; i += kST) mx = fmaxf(mx, ld<T>(x, i));
+    const float thr = skip ? block_max<kST>(mx, sv) * itemp - kGumbelSpan : -INFINITY;
     for (int i = lo + tid; i < hi; i += kST) {
       const float v = ld<T>(x, i) * itemp;
       if (v >= thr) a = better(a, ArgMax{v + gumbel(key, i), i});
@@ -235,12 +240,16 @@ extern "C" int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, 
   if (B <= 0) return 0;
   const int P = k8sllm_sample_parts(B, V);
   dim3 grid((unsigned)B, P);
+  static const int skip = [] {
+    const char* e = getenv("K8SLLM_SAMPLE_SKIP");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   if (is_fp32)
     hipLaunchKernelGGL((sample_partial_kernel<float>), grid, dim3(kST), 0, s, pv, pi, (const float*)logits, stride,
-                       V, P, temps, top_k, top_p, rng);
+                       V, P, temps, top_k, top_p, rng, skip);
   else
     hipLaunchKernelGGL((sample_partial_kernel<bf16_t>), grid, dim3(kST), 0, s, pv, pi, (const bf16_t*)logits,
-                       stride, V, P, temps, top_k, top_p, rng);
+                       stride, V, P, temps, top_k, top_p, rng, skip);
   hipLaunchKernelGGL(sample_final_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, out, pv, pi, (int)B, V, P,
                      temps, top_k, top_p, advance && rng ? const_cast<int64_t*>(rng) : nullptr);
   return (int)hipGetLastError();
