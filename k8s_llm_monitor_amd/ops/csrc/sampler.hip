@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
                                                              const float* __restrict__ temps,
                                                              const int* __restrict__ top_k,
                                                              const float* __restrict__ top_p,
-                                                             const int64_t* __restrict__ rng, int skip) {
+                                                             const int64_t* __restrict__ rng) {
   __shared__ float sv[kST / 64];
   __shared__ int si[kST / 64];
   const int row = blockIdx.x, part = blockIdx.y, tid = threadIdx.x;
@@ -174,21 +174,9 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
   if (!(temp > 0.f)) {
     for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i), i});
   } else {
-    // Gumbel-max with the hash and the two logs only where they can matter: gumbel() lies in
-    // [-2.81, 16.64] for every hash value, so an element whose x / T is more than kGumbelSpan below
-    // the part's largest x / T can never beat the element holding it (at T = 0.1 that skips ~99 %
-    // of a 128K vocabulary).  Exact.
-    constexpr float kGumbelSpan = 20.5f;  // 16.64 + 2.81, plus slack
     const float itemp = 1.f / temp;
     const uint64_t key = row_key(rng, row);
-    float mx = -INFINITY;
-    if (skip)
-      for (int i = lo + tid; i < hi; i += kST) mx = fmaxf(mx, ld<T>(x, i));
-    const float thr = skip ? block_max<kST>(mx, sv) * itemp - kGumbelSpan : -INFINITY;
-    for (int i = lo + tid; i < hi; i += kST) {
-      const float v = ld<T>(x, i) * itemp;
-      if (v >= thr) a = better(a, ArgMax{v + gumbel(key, i), i});
-    }
+    for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i) * itemp + gumbel(key, i), i});
   }
   a = block_argmax(a, sv, si);
   if (tid == 0) {
@@ -240,16 +228,12 @@ extern "C" int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, 
   if (B <= 0) return 0;
   const int P = k8sllm_sample_parts(B, V);
   dim3 grid((unsigned)B, P);
-  static const int skip = [] {
-    const char* e = getenv("K8SLLM_SAMPLE_SKIP");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
   if (is_fp32)
     hipLaunchKernelGGL((sample_partial_kernel<float>), grid, dim3(kST), 0, s, pv, pi, (const float*)logits, stride,
-                       V, P, temps, top_k, top_p, rng, skip);
+                       V, P, temps, top_k, top_p, rng);
   else
     hipLaunchKernelGGL((sample_partial_kernel<bf16_t>), grid, dim3(kST), 0, s, pv, pi, (const bf16_t*)logits,
-                       stride, V, P, temps, top_k, top_p, rng, skip);
+                       stride, V, P, temps, top_k, top_p, rng);
   hipLaunchKernelGGL(sample_final_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, out, pv, pi, (int)B, V, P,
                      temps, top_k, top_p, advance && rng ? const_cast<int64_t*>(rng) : nullptr);
   return (int)hipGetLastError();
