@@ -198,6 +198,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // RESID: this lane's first 16 residual chunks (rows rr + 4b of the wave's 128, 16 B at column
+  // chunk cc), issued during the last k-tile's second half so they land behind its MFMAs
+  u32x4 resq[EPI == TILE_EPI_RESID ? 16 : 1];
 
   if constexpr (SCH == 1) {
     // Ring addressing: the half-slot byte offsets of the current tile live in SGPRs and rotate
@@ -212,9 +216,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       char* dst = smem + slot_bytes + (p * 4 + wave) * 1024;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], min(kt, nk - 1) * 128, 0, 0);
     };
-    auto sub = [&](auto ph, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8], uint32_t sa,
-                   uint32_t sb, uint32_t da, uint32_t db, int t) {
-      constexpr int PH = decltype(ph)::value;
+    // PM (the ring tail, peeled): 0 = B_{t+2} and A_{t+3} refills; 1 = B_{t+2} only (A_{t+3} is
+    // past the end); 2 = no refill; 3 = no refill and, in (t, 1), no reads of tile t+1 (there is
+    // none).  The tail issues no dummy pieces (a re-read of the last k-tile kept the counts fixed:
+    // 40 of every tile's 1064 pieces per wave, ~4 % of the DMA issue at K = 4096).
+    auto sub = [&](auto ph, auto pm, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8],
+                   uint32_t sa, uint32_t sb, uint32_t da, uint32_t db, int t) {
+      constexpr int PH = decltype(ph)::value, PM = decltype(pm)::value;
+      constexpr bool READS = !(PH == 1 && PM == 3);
       // sa / sb: half-slot bytes of the fragments read here; da / db: B_{t+2}'s / A_{t+3}'s targets
       const uint32_t ba = sa + (PH == 0 ? fbA1 : fbA0), bb = sb + (PH == 0 ? fbB1 : fbB0);
       __builtin_amdgcn_sched_barrier(0);
@@ -225,25 +234,29 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
           const int n = g * 8 + j;
           acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[g], acc[g][j], 0, 0, 0);
           if (n < 8) {
-            nb[n] = rd16(bb, n);
+            if constexpr (READS) nb[n] = rd16(bb, n);
           } else if (n < 16) {
-            na[n - 8] = rd16(ba, n - 8);
-          } else if (PH == 0 && n == 19) {
+            if constexpr (READS) na[n - 8] = rd16(ba, n - 8);
+          } else if (PH == 0 && PM <= 1 && n == 19) {  // frees tile t's half-slots for the refills
             lgkm_wait0();
             __builtin_amdgcn_s_barrier();
-          } else if (PH == 0 && n >= 22 && (n - 22) % 6 == 0 && (n - 22) / 6 < 7) {
+          } else if (PH == 0 && PM <= 1 && n >= 22 && (n - 22) % 6 == 0 && (n - 22) / 6 < 7) {
             pc(1, (n - 22) / 6, t + 2, da);
-          } else if (PH == 1 && n >= 19 && (n - 19) % 5 == 0 && (n - 19) / 5 < 9) {
+          } else if (PH == 1 && PM <= 1 && n >= 19 && (n - 19) % 5 == 0 && (n - 19) / 5 < 9) {
             const int i = 7 + (n - 19) / 5;
             if (i < 8)
               pc(1, i, t + 2, da);
-            else
+            else if (PM == 0)
               pc(0, i - 8, t + 3, db);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
     };
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
     // RS: this thread's row partials (row row0 + tid, clamped), loaded ahead of the prologue DMAs
     // so their wait is the prologue's own (a fixed 8 loads: up to 32 partials, extra ones masked)
     f32x4 rsq[RS ? 8 : 1];
@@ -274,19 +287,54 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     // half-slot bytes of tile t: S0 = (2t % 5) HS (A_t), S1 = ((2t + 1) % 5) HS (B_t), S2 / S3 =
     // tile t+1's.  Tile t+1: S0' = S2, S1' = S3, S2' = ((2t + 4) % 5) HS, S3' = S0.
     uint32_t S0 = 0, S1 = HS, S2 = 2 * HS, S3 = 3 * HS;
-    for (int t = 0; t < nk; ++t) {
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous sub-step's reads, explicitly
-      sub(std::integral_constant<int, 0>{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
-      vm_wait_n<15>();
-      __builtin_amdgcn_s_barrier();
-      sub(std::integral_constant<int, 1>{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+    auto rotate = [&]() {
       const uint32_t s4 = S0 == 0 ? 4 * HS : S0 - HS, s0 = S0;
       S0 = S2;
       S1 = S3;
       S2 = s4;
       S3 = s0;
+    };
+    // vmcnt at the mid-tile wait: B_{t+1} must have landed; younger are A_{t+2} (8) + B_{t+2}'s
+    // first 7 pieces (15) in the steady state and at t = nk - 3, nothing from t = nk - 2 on
+    for (int t = 0; t < nk - 3; ++t) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous sub-step's reads, explicitly
+      sub(P0{}, P0{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
+      vm_wait_n<15>();
+      __builtin_amdgcn_s_barrier();
+      sub(P1{}, P0{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+      rotate();
     }
-    vm_wait_n<0>();
+    {  // t = nk - 3 (host: nk >= 3): B_{nk-1} is the last refill
+      const int t = nk - 3;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      sub(P0{}, P1{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
+      vm_wait_n<15>();
+      __builtin_amdgcn_s_barrier();
+      sub(P1{}, P1{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+      rotate();
+    }
+    {  // t = nk - 2: every piece issued so far must land (B_{nk-1} is read in (t, 1))
+      const int t = nk - 2;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      sub(P0{}, P2{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
+      vm_wait_n<0>();
+      __builtin_amdgcn_s_barrier();
+      sub(P1{}, P2{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+      rotate();
+    }
+    {  // t = nk - 1: the last k-tile; (t, 1) reads nothing - RESID issues its residual loads here
+      const int t = nk - 1;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      sub(P0{}, P3{}, fa0, fb0, fa1, fb1, S0, S1, S0, S1, t);
+      if constexpr (EPI == TILE_EPI_RESID) {
+        const __amdgpu_buffer_rsrc_t rres = rsrc(ep.resid + (long)row0 * N, (long)mrows * N * 2);
+        const uint32_t ro = (uint32_t)(((wm * 128 + (lane >> 4)) * N + n0 + wn * 128 + (lane & 15) * 8) * 2);
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+          resq[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * b * N * 2), 0, 0);
+      }
+      sub(P1{}, P3{}, fa1, fb1, fa0, fb0, S2, S3, S0, S1, t);
+    }
   } else {
     // One 32-deep sub-step: 64 MFMAs from (ca, cb), each carrying at most one other instruction in
     // its shadow.  The 8 DMA pieces of the sub-step ride MFMAs 4, 12, ..., 60 - evenly spread: an
@@ -353,19 +401,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   constexpr int RS_ = OUTW * 2 + 16;                       // LDS row stride (16-B pad: 2-way writes)
   char* stage = smem + wave * (128 * RS_);
   const int ml = lane & 15, nq = 4 * (lane >> 4);
-  // RESID: this lane's residual chunks (rows rr + 4b of the wave's 128, 16 B at column chunk cc),
-  // issued now so their latency hides behind the staging writes
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int rr = lane >> 4, cc = lane & 15;
-  u32x4 res[EPI == TILE_EPI_RESID ? 16 : 1];  // a rolling window of 16 chunks in flight
   uint4 nwv{};
-  if constexpr (EPI == TILE_EPI_RESID) {
-    const __amdgpu_buffer_rsrc_t rres = rsrc(ep.resid + (long)row0 * N, (long)mrows * N * 2);
-    const uint32_t ro = (uint32_t)(((wm * 128 + rr) * N + n0 + wn * 128 + cc * 8) * 2);
-#pragma unroll
-    for (int b = 0; b < 16; ++b) res[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * b * N * 2), 0, 0);
-    nwv = *reinterpret_cast<const uint4*>(ep.norm_w + n0 + wn * 128 + cc * 8);
-  }
+  if constexpr (EPI == TILE_EPI_RESID) nwv = *reinterpret_cast<const uint4*>(ep.norm_w + n0 + wn * 128 + cc * 8);
   // RS: each thread's row scale through LDS (after the staging area) to the lanes holding the row
   float sc[8];
 #pragma unroll
@@ -415,8 +453,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       const uint4 yv = *reinterpret_cast<const uint4*>(stage + r * RS_ + cc * 16);
       float y[8], rv[8], h[8], hw[8];
       unpack8(yv, y);
-      const u32x4 rb = res[b & 15];
-      if (b < 16) res[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * (b + 16) * N * 2), 0, 0);
+      const u32x4 rb = resq[b & 15];
+      if (b < 16) resq[b] = __builtin_amdgcn_raw_buffer_load_b128(rres, ro + (uint32_t)(4 * (b + 16) * N * 2), 0, 0);
       unpack8(uint4{rb[0], rb[1], rb[2], rb[3]}, rv);
       float ss = 0.f;
 #pragma unroll
@@ -506,6 +544,10 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
   const bool rs = rs_part != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
   if (algo < 0 || algo > 1) return -1;
+  if (algo == 1 && K < 192) {  // schedule 1's peeled ring tail needs three k-tiles
+    if (epi == TILE_EPI_RESID || rs_part != nullptr) return -1;
+    algo = 0;
+  }
   if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
   if (epi == TILE_EPI_ROPE && (grouped || N % 128 != 0 || rope_pos == nullptr || rope_cs == nullptr)) return -1;
   if (epi == TILE_EPI_RESID && (grouped || rs || N % 128 != 0 || resid == nullptr || hw == nullptr ||
