@@ -10,6 +10,8 @@
 // EPI_SWIGLU: W is gate/up-interleaved per 128 rows ([64 gate | 64 up], ops.interleave_gate_up),
 //          Y = silu(gate) * up [rows][N / 2] - the separate silu_mul pass over the [rows][N]
 //          intermediate disappears.
+// EPI_ROPE / EPI_RESID / RS: the qkv projection's rotary embedding, the o / down residual add +
+//          next-RMSNorm operands, and the consumers' deferred 1/rms row scale (see TileEpi below).
 //
 // Structure: 4 waves (one per SIMD), each owning a 128 x 128 quarter of the tile as 64 accumulators
 // of v_mfma_f32_16x16x32_bf16 (256 f32 per lane in AGPRs).  Per 32-deep k sub-step a wave reads 16

@@ -66,9 +66,30 @@ def main() -> None:
         "rope_cache_only": (lambda i: ops.rope_and_cache(yq, pos, cs, kc, vc, slots, 32, 8, 128, apply_rope=True)),
         "cache_only": (lambda i: ops.rope_and_cache(yq, pos, cs, kc, vc, slots, 32, 8, 128, apply_rope=False)),
     }))
+    # the fused-norm epilogues vs their plain forms, same operands: gate_up + SwiGLU with / without
+    # the row scale, qkv + RoPE with / without it, o with the residual epilogue vs plain
+    ssq = (torch.rand(T, d // 128, device=dev) * 128 + 64).contiguous()
+    resid = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    hwb = torch.empty(T, d, device=dev, dtype=torch.bfloat16)
+    ssb = torch.empty(T, d // 128, device=dev, dtype=torch.float32)
+    nwv = torch.ones(d, device=dev, dtype=torch.bfloat16)
+    wo_ = torch.randn(d, d, device=dev, dtype=torch.bfloat16) * 0.02
+    yo = torch.empty(T, d, device=dev, dtype=torch.bfloat16)
+    cases.append(("qkv+rope_rs", 2 * T * 6144 * d, {
+        "plain": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40))),
+        "rowscale": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40), rowscale=(ssq, 1e-5))),
+    }))
+    cases.append(("o_resid", 2 * T * d * d, {
+        "plain": (lambda i: ops.gemm_tile(x, wo_, out=yo, algo=1)),
+        "resid": (lambda i: ops.gemm_tile_resid(x, wo_, resid, nwv, hw=hwb, ss=ssb)),
+    }))
     w13 = ops.interleave_gate_up(torch.randn(2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02).contiguous()
     gu = torch.empty(T, 2 * F, device=dev, dtype=torch.bfloat16)
     act = torch.empty(T, F, device=dev, dtype=torch.bfloat16)
+    cases.append(("gate_up+swiglu_rs", 2 * T * 2 * F * d, {
+        "plain": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
+        "rowscale": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1, rowscale=(ssq, 1e-5))),
+    }))
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
         "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
