@@ -189,3 +189,19 @@ def test_fused_norm_epilogues_cpu_path():
     import pytest
     with pytest.raises(ValueError):
         ops.gemm_tile(hw, wo, rowscale=(ss, 1e-5))  # only the fused consumers take a row scale
+
+
+def test_embed_norm_partial_cpu_path():
+    """ops.embed_norm_partial off the GPU = resolve_ids -> embedding -> add_norm_partial(nslabs=0)."""
+    torch.manual_seed(7)
+    V, d, M = 50, 512, 5
+    emb = torch.randn(V, d, dtype=torch.bfloat16)
+    nw = (torch.rand(d) + 0.5).to(torch.bfloat16)
+    ids = torch.tensor([3, 7, 11, 13, 17], dtype=torch.int32)
+    prev = torch.tensor([40, 41, 42], dtype=torch.int32)
+    src = torch.tensor([-1, 2, -1, 0, -1], dtype=torch.int32)
+    res, xw, ss = ops.embed_norm_partial(ids, emb, nw, src, prev)
+    want_ids = torch.tensor([3, 42, 11, 40, 17])
+    assert torch.equal(res, emb[want_ids])
+    xw0, ss0 = ops.add_norm_partial(emb[want_ids].clone(), None, 0, nw)
+    assert torch.equal(xw, xw0) and torch.allclose(ss, ss0)
