@@ -329,8 +329,7 @@ class CausalLM:
         c = self.cfg
         T = x.shape[0]
         K = c.top_k_experts
-        logits = F.linear(x, L["router"]).float()
-        ids, w = ops.moe_route(logits, K, True)
+        ids, w, _ = ops.moe_router(x, L["router"], K, True)
         if not meta.is_prefill and not (self._moe_grouped and x.is_cuda):
             # CPU reference of the decode form (the GPU takes the routed grouped path below, which
             # needs no host sync either and runs only the (token, expert) pairs that were chosen)
@@ -379,8 +378,7 @@ class CausalLM:
         t0, t1 = min(T, r * chunk), min(T, (r + 1) * chunk)
         n = t1 - t0
         xs = x[t0:t1]
-        logits = F.linear(xs, L["router"]).float()
-        ids, w = ops.moe_route(logits, K, True)
+        ids, w, _ = ops.moe_router(xs, L["router"], K, True)
         offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
         send = ops.gather_rows(xs, sorted_idx, K) if n else xs.new_zeros(0, c.d_model)
         send_exp = ids.reshape(-1)[sorted_idx.long()].to(torch.int64)
@@ -450,7 +448,7 @@ class CausalLM:
         if M < P * cap:
             x = torch.cat([x, x.new_zeros(P * cap - M, d)])
         xs = x[r * cap:(r + 1) * cap]
-        ids, w = ops.moe_route(F.linear(xs, L["router"]).float(), K, True)  # [cap, K]
+        ids, w, _ = ops.moe_router(xs, L["router"], K, True)  # [cap, K]
         ids = ids.long()
         npair = cap * K
         pair_x = xs.repeat_interleave(K, dim=0)  # [cap*K, d], pair j = (token j // K, slot j % K)
@@ -757,8 +755,7 @@ class CausalLM:
                 xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps)
             else:
                 xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
-        ids, w = ops.moe_route(F.linear(xn, L["router"]).float(), c.top_k_experts, True)
-        wd = torch.zeros(M, c.n_experts, dtype=torch.float32, device=xn.device).scatter_(1, ids.long(), w)
+        _, _, wd = ops.moe_router(xn, L["router"], c.top_k_experts, True)
         act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 

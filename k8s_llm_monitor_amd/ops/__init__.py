@@ -795,6 +795,22 @@ def moe_route(router_logits: torch.Tensor, k: int, renorm: bool = True):
     return ids, w
 
 
+def moe_router(x: torch.Tensor, router_w: torch.Tensor, k: int, renorm: bool = True) -> tuple:
+    """MoE decode routing in one launch: ``(ids [T, k] int32, w [T, k] fp32, wd [T, E] fp32)`` -
+    the top-k experts of bf16(x . router_w^T), their (renormalised) softmax weights, and the dense
+    per-expert weight rows (0 where an expert was not chosen) for the grouped expert kernels."""
+    T, E = x.shape[0], router_w.shape[0]
+    if not _gpu(x) or E > 16:
+        ids, w = moe_route(torch.nn.functional.linear(x, router_w).float(), k, renorm)
+        wd = torch.zeros(T, E, dtype=torch.float32, device=x.device).scatter_(1, ids.long(), w)
+        return ids, w, wd
+    ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
+    w = torch.empty(T, k, dtype=torch.float32, device=x.device)
+    wd = torch.empty(T, E, dtype=torch.float32, device=x.device)
+    native().moe_router(x.contiguous(), router_w, ids, w, wd, renorm)
+    return ids, w, wd
+
+
 def moe_align(ids: torch.Tensor, E: int):
     if not _gpu(ids) or E > 16:
         return ref.moe_align(ids, E)

@@ -34,6 +34,8 @@ int k8sllm_sample(int* out, const void* logits, int is_fp32, long B, long stride
 int k8sllm_sample_parts(long B, int V);
 int k8sllm_moe_route(const void* logits, long T, int E, int K, int renorm, int* topk_ids, float* topk_w,
                      hipStream_t s);
+int k8sllm_moe_router(const void* x, const void* wr, long T, int d, int E, int K, int renorm, int* ids, float* w,
+                      float* wd, hipStream_t s);
 int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, int* sorted_idx, int* inv_idx,
                      hipStream_t s);
 int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
@@ -316,6 +318,20 @@ void sample(torch::Tensor out, torch::Tensor logits, c10::optional<torch::Tensor
   check(k8sllm_sample(out.data_ptr<int>(), logits.data_ptr(), f32 ? 1 : 0, B, logits.stride(0), V, t, k, p, r,
                       pv.data_ptr<float>(), pi.data_ptr<int>(), advance ? 1 : 0, cur()),
         "sample");
+}
+
+void moe_router(torch::Tensor x, torch::Tensor wr, torch::Tensor ids, torch::Tensor w, torch::Tensor wd, bool renorm) {
+  dev_bf16(x, "x"); dev_bf16(wr, "router"); dev_i32(ids, "ids");
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 2 && wr.is_contiguous() && wr.dim() == 2 && wr.size(1) == x.size(1),
+              "moe_router: x [T, d], router [E, d]");
+  const long T = x.size(0);
+  const int E = (int)wr.size(0), K = (int)ids.size(1);
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && w.is_cuda() && w.scalar_type() == torch::kFloat32 &&
+                  w.sizes() == ids.sizes() && wd.is_cuda() && wd.scalar_type() == torch::kFloat32 &&
+                  wd.is_contiguous() && wd.numel() == T * E, "moe_router: ids / w [T, K], wd [T, E] fp32");
+  check(k8sllm_moe_router(x.data_ptr(), wr.data_ptr(), T, (int)x.size(1), E, K, renorm ? 1 : 0, ids.data_ptr<int>(),
+                          w.data_ptr<float>(), wd.data_ptr<float>(), cur()),
+        "moe_router");
 }
 
 void moe_route(torch::Tensor logits, torch::Tensor topk_ids, torch::Tensor topk_w, bool renorm) {
@@ -837,6 +853,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),
         py::arg("rng"), py::arg("advance") = false);
   m.def("moe_route", &moe_route);
+  m.def("moe_router", &moe_router);
   m.def("moe_align", &moe_align);
   m.def("moe_combine", &moe_combine);
   m.def("gather_rows", &gather_rows);

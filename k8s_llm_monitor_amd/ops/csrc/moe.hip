@@ -37,6 +37,73 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
     for (int k = 0; k < K; ++k) w[t * K + k] /= sel;
 }
 
+// MoE decode router in one launch (one workgroup per row): logits = bf16(x . W_router^T) (as the
+// library GEMM's bf16 output would be), softmax top-k (+ renormalisation) as moe_route_kernel, and
+// the dense per-expert weight row wd[t][e] (0 for an expert the row did not choose) that the grouped
+// expert kernels scale their slabs by.  Replaces GEMM + fp32 cast + route + zeros + scatter.
+template <int EMAX>
+__global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wr,
+                                                         int d, int E, int K, int renorm, int* __restrict__ ids,
+                                                         float* __restrict__ w, float* __restrict__ wd) {
+  __shared__ float red[4][EMAX];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  float acc[EMAX];
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) acc[e] = 0.f;
+  const bf16_t* xr = x + (long)t * d;
+  for (int c = tid * 8; c < d; c += 256 * 8) {
+    float xv[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), xv);
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      if (e < E) {
+        float wv[8];
+        unpack8(*reinterpret_cast<const uint4*>(wr + (long)e * d + c), wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[e] = __builtin_fmaf(xv[j], wv[j], acc[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {
+    const float v = wave_sum(acc[e]);
+    if ((tid & 63) == 0) red[tid >> 6][e] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  float lg[EMAX];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    lg[e] = bf2f(f2bf((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])));
+    mx = fmaxf(mx, lg[e]);
+  }
+  float z = 0.f;
+  for (int e = 0; e < E; ++e) z += __expf(lg[e] - mx);
+  uint32_t taken = 0u;
+  float sel = 0.f, pk[EMAX];
+  int bk[EMAX];
+  for (int k = 0; k < K; ++k) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((taken >> e) & 1u) && lg[e] > bv) {
+        bv = lg[e];
+        best = e;
+      }
+    taken |= 1u << best;
+    pk[k] = __expf(bv - mx) / z;
+    bk[k] = best;
+    sel += pk[k];
+  }
+  for (int e = 0; e < E; ++e) wd[(long)t * E + e] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float p = renorm ? pk[k] / sel : pk[k];
+    ids[(long)t * K + k] = bk[k];
+    w[(long)t * K + k] = p;
+    wd[(long)t * E + bk[k]] = p;
+  }
+}
+
 constexpr int kAT = 1024;
 constexpr int kMaxE = 16;
 
@@ -129,6 +196,19 @@ int k8sllm_moe_route(const void* logits, long T, int E, int K, int renorm, int* 
   if (E > 64 || K > E) return -1;
   hipLaunchKernelGGL(moe_route_kernel, dim3((T + 255) / 256), dim3(256), 0, s, (const float*)logits, T, E, K, renorm,
                      topk_ids, topk_w);
+  return (int)hipGetLastError();
+}
+
+int k8sllm_moe_router(const void* x, const void* wr, long T, int d, int E, int K, int renorm, int* ids, float* w,
+                      float* wd, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (E > 16 || K > E || d % 8 != 0) return -1;
+  if (E <= 8)
+    hipLaunchKernelGGL(moe_router_kernel<8>, dim3(T), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wr, d, E, K,
+                       renorm, ids, w, wd);
+  else
+    hipLaunchKernelGGL(moe_router_kernel<16>, dim3(T), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wr, d, E, K,
+                       renorm, ids, w, wd);
   return (int)hipGetLastError();
 }
 

@@ -121,3 +121,20 @@ def test_moe_decode_beyond_skinny_rows_grouped_in_graph(T):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(yg.float(), y)
+
+
+@pytest.mark.parametrize("T", [1, 64, 300])
+@pytest.mark.parametrize("E,K", [(8, 2), (16, 4)])
+def test_moe_router_matches_linear_route_scatter(T, E, K):
+    """The one-launch MoE router (moe_router_kernel) = bf16 F.linear -> fp32 -> moe_route -> dense
+    per-expert weight rows: same experts, same weights (fp32 tolerance)."""
+    d = 4096
+    x = torch.randn(T, d, device="cuda", dtype=torch.bfloat16)
+    wr = (torch.randn(E, d, device="cuda") * 0.02).to(torch.bfloat16)
+    ids, w, wd = ops.moe_router(x, wr, K, True)
+    lg = torch.nn.functional.linear(x.float(), wr.float()).to(torch.bfloat16).float()
+    rids, rw = ops.moe_route(lg, K, True)
+    assert torch.equal(ids, rids)
+    torch.testing.assert_close(w, rw, rtol=1e-5, atol=1e-6)
+    ref_wd = torch.zeros(T, E, device="cuda").scatter_(1, rids.long(), rw)
+    torch.testing.assert_close(wd, ref_wd, rtol=1e-5, atol=1e-6)
