@@ -336,7 +336,9 @@ def deinterleave_gate_up8(w: torch.Tensor) -> torch.Tensor:
 # profiles/r04/decode_gemm_sweep.jsonl).  Shapes not listed get an automatic pick.
 DEC_TABLE: dict = {
     # Llama-3-8B at TP=1 (profiles/r04/decode_gemm_sweep_v1.jsonl, M = 64 / M = 1 us):
-    (6144, 4096, 0): (4, 1, 8, 8),      # qkv      13.2 / 10.3   (row-major skinny 13.4 / 10.4)
+    # qkv: 6 waves -> 64 column groups x 4 splits = 256 workgroups (8 waves left 64 CUs idle):
+    # 12.1 vs 13.8 us at M = 64, 9.8 vs 11.0 at M = 1 (decode_gemm_qkv_6waves.jsonl)
+    (6144, 4096, 0): (4, 1, 6, 8),      # qkv      12.1 / 9.8    (row-major skinny 13.5 / 10.6)
     (4096, 4096, 0): (8, 1, 8, 8),      # o         9.6 / 7.5    (10.2 / 7.5)
     (28672, 4096, 2): (1, 1, 7, 8),     # gate_up  39.9 / 38.1   (47.9 / 40.0)
     (4096, 14336, 0): (8, 1, 8, 8),     # down     22.3 / 19.0   (24.3 / 19.9)

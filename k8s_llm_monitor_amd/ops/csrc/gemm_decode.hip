@@ -251,6 +251,9 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     else if (ntw == 4 && waves == 4 && depth == 8) { K8S_DEC_M(4, 4, DEC_SLAB, 8) }
     else if (ntw == 3 && waves == 8 && depth == 8) { K8S_DEC_M(3, 8, DEC_SLAB, 8) }
     else if (ntw == 1 && waves == 4 && depth == 8) { K8S_DEC_M(1, 4, DEC_SLAB, 8) }
+    // qkv at 4 splits: 384 n-tiles / 6 per workgroup = 64 column groups x 4 = 256 workgroups
+    else if (ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_M(1, 6, DEC_SLAB, 8) }
+    else if (ntw == 2 && waves == 3 && depth == 8) { K8S_DEC_M(2, 3, DEC_SLAB, 8) }
   } else if (epi == DEC_SWIGLU8) {
     if (ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 16) }
     else if (ntw == 1 && waves == 8 && depth == 16) { K8S_DEC_M(1, 8, DEC_SWIGLU8, 16) }
