@@ -31,6 +31,8 @@ def _w(N, K, s=0.02):
 
 CASES = [  # (N, K, cfg)  - the engine's picks plus ragged / edge configurations
     (6144, 4096, (8, 3, 4, 8)),
+    (6144, 4096, (4, 1, 6, 8)),  # the engine's qkv pick: 6-wave workgroups
+    (4096, 4096, (4, 2, 3, 8)),
     (4096, 4096, (8, 1, 8, 8)),
     (4096, 4096, (4, 1, 4, 16)),
     (4096, 14336, (8, 2, 4, 8)),
