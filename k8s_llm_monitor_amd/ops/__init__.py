@@ -976,8 +976,8 @@ def tile_shape_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
 def fused_norm_ok(M: int, d: int, n_qkv: int, n_o_in: int, n_13: int, f: int) -> bool:
     """The prefill layer may run with its RMSNorms folded into the tile GEMMs (gemm_tile_resid +
     row scale): every projection on the tile kernel (default routing), qkv with the RoPE epilogue,
-    d a multiple of 128 with at most 32 partial sums per row."""
-    return (FUSED_NORM and PREFILL_GEMM == "tile" and QKV_ROPE_TILE and d % 128 == 0 and d // 128 <= 32
+    d a multiple of 128 with at most 64 partial sums per row (d <= 8192)."""
+    return (FUSED_NORM and PREFILL_GEMM == "tile" and QKV_ROPE_TILE and d % 128 == 0 and d // 128 <= 64
             and n_qkv % 128 == 0 and tile_shape_ok(M, n_qkv, d) and tile_shape_ok(M, d, n_o_in)
             and tile_shape_ok(M, n_13, d, swiglu=True) and tile_shape_ok(M, d, f) and 256 * d * 2 < (1 << 31))
 

@@ -84,7 +84,7 @@ struct TileEpi {
   const float* cos_sin;  // ROPE: [max_pos][128]: cos (64) | sin (64)
   int rope_heads;        // ROPE: Hq + Hkv: heads 0 .. rope_heads - 1 are rotated
   const float* rs_part;  // RS: [M][rs_np] partial sums of squares of the A rows
-  int rs_np;             // RS: partials per row (K / 128, <= 32)
+  int rs_np;             // RS: partials per row (K / 128, <= 64)
   float rs_eps;
   bf16_t* resid;         // RESID: [M][N] residual stream, updated in place
   bf16_t* hw;            // RESID: [M][N] resid * norm_w
@@ -260,12 +260,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     using P2 = std::integral_constant<int, 2>;
     using P3 = std::integral_constant<int, 3>;
     // RS: this thread's row partials (row row0 + tid, clamped), loaded ahead of the prologue DMAs
-    // so their wait is the prologue's own (a fixed 8 loads: up to 32 partials, extra ones masked)
-    f32x4 rsq[RS ? 8 : 1];
+    // so their wait is the prologue's own (a fixed 16 loads: up to 64 partials, extra ones masked)
+    f32x4 rsq[RS ? 16 : 1];
     if constexpr (RS) {
       const float* rp = ep.rs_part + (long)(row0 + min((int)threadIdx.x, mrows - 1)) * ep.rs_np;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rsq[j] = *reinterpret_cast<const f32x4*>(rp + min(4 * j, ep.rs_np - 4));
+      for (int j = 0; j < 16; ++j) rsq[j] = *reinterpret_cast<const f32x4*>(rp + min(4 * j, ep.rs_np - 4));
     }
     issue_half(0, 0);
     issue_half(1, 0);
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     if constexpr (RS) {
       float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 16; ++j)
         if (4 * j < ep.rs_np) sum += (rsq[j][0] + rsq[j][1]) + (rsq[j][2] + rsq[j][3]);
       rs_inv = rsqrtf(sum / (float)K + ep.rs_eps);
     }
@@ -556,7 +556,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
                                 norm_w == nullptr || ss_out == nullptr || algo != 1))
     return -1;
   // row scale: the fused consumers only (qkv + RoPE, gate_up + SwiGLU), schedule 1
-  if (rs && (grouped || algo != 1 || rs_np < 4 || rs_np > 32 || rs_np % 4 != 0 ||
+  if (rs && (grouped || algo != 1 || rs_np < 4 || rs_np > 64 || rs_np % 4 != 0 ||
              (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
     return -1;
   const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,

@@ -133,6 +133,19 @@ def test_tile_rowscale_consumers_llama8b(M):
     assert _rel(a, F_.silu(gu[:, :F]) * gu[:, F:]) < 2e-2
 
 
+def test_tile_rowscale_64_partials_d8192():
+    """Llama-3-70B width (d = 8192): the row scale sums 64 partials per row."""
+    M, d, F = 1024, 8192, 1024
+    h = torch.randn(M, d, device=DEV, dtype=torch.bfloat16) * 2
+    nw = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+    hw = (h.float() * nw.float()).to(torch.bfloat16)
+    ss = (h.float() ** 2).view(M, d // 128, 128).sum(2).contiguous()
+    w13 = (torch.randn(2 * F, d, device=DEV) * 0.02).to(torch.bfloat16)
+    a = ops.gemm_tile(hw, ops.interleave_gate_up(w13).contiguous(), swiglu=True, algo=1, rowscale=(ss, 1e-5))
+    gu = (F_.rms_norm(h.float(), (d,), nw.float(), 1e-5) @ w13.float().t()).to(torch.bfloat16).float()
+    assert _rel(a, F_.silu(gu[:, :F]) * gu[:, F:]) < 2e-2
+
+
 def _fp32_forward(model, ids):
     """Plain fp32 forward of the same weights (no HIP kernels): last-token logits."""
     c = model.cfg
