@@ -1,6 +1,6 @@
 """Decode sampler timing: ops.sample over [B, V] bf16 logits (LM-head-like: x / T has std ~13 at
 T = 0.1 for a random-init Llama-3-8B head) - greedy, T = 0.1, T = 1.0; hipGraph replay of
-back-to-back calls.  K8SLLM_SAMPLE_SKIP=0 disables the Gumbel skip for an A/B in another process.
+back-to-back calls.
 
     python tools/bench_sampler.py [--b 64] [--v 128256]
 """
@@ -29,11 +29,10 @@ def main() -> None:
     logits = (torch.randn(a.b, a.v, device=dev) * 1.28).to(torch.bfloat16)
     out = torch.empty(a.b, dtype=torch.int32, device=dev)
     rng = torch.tensor([1, 0], device=dev, dtype=torch.int64)
-    skip = os.environ.get("K8SLLM_SAMPLE_SKIP", "1")
     for name, t in (("greedy", 0.0), ("T0.1", 0.1), ("T1.0", 1.0)):
         temps = torch.full((a.b,), t, device=dev)
         us = timeit(lambda i: ops.sample(logits, temps, None, None, rng, out=out, advance=True), 64, per_graph=8)
-        print(json.dumps({"op": "sample", "B": a.b, "V": a.v, "mode": name, "skip": skip, "us": round(us, 2)}),
+        print(json.dumps({"op": "sample", "B": a.b, "V": a.v, "mode": name, "us": round(us, 2)}),
               flush=True)
 
 
