@@ -13,6 +13,8 @@
 // with top-k / top-p need a row-wide threshold; part 0 of such a row runs the whole-row bisection
 // path and its answer is taken as is.  The per-element hash is 32-bit (two murmur3 finalisers of
 // a per-row 64-bit key) - 64-bit multiplies are multi-instruction sequences on CDNA.
+#include <type_traits>
+
 #include "common.h"
 #include <stdlib.h>
 
@@ -168,16 +170,27 @@ __global__ __launch_bounds__(kST) void sample_partial_kernel(float* __restrict__
     if (tid == 0) pi[row * P] = tok;
     return;
   }
-  const int chunk = (V + P - 1) / P;
-  const int lo = part * chunk, hi = min(V, lo + chunk);
+  // parts start on 8-element boundaries so that bf16 rows with an 8-aligned stride are read 16 B
+  // per lane (one load per 8 logits instead of eight dependent 2-byte loads)
+  const int chunk = ((V + P - 1) / P + 7) & ~7;
+  const int lo = min(V, part * chunk), hi = min(V, lo + chunk);
+  const bool vec = std::is_same<T, bf16_t>::value && (stride & 7) == 0;
+  const int hv = vec ? lo + ((hi - lo) & ~7) : lo;  // [lo, hv) in 8-element vectors, [hv, hi) scalar
   ArgMax a{-INFINITY, 0x7fffffff};
-  if (!(temp > 0.f)) {
-    for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i), i});
-  } else {
-    const float itemp = 1.f / temp;
-    const uint64_t key = row_key(rng, row);
-    for (int i = lo + tid; i < hi; i += kST) a = better(a, ArgMax{ld<T>(x, i) * itemp + gumbel(key, i), i});
+  const bool greedy = !(temp > 0.f);
+  const float itemp = greedy ? 1.f : 1.f / temp;
+  const uint64_t key = greedy ? 0ull : row_key(rng, row);
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    for (int i = lo + tid * 8; i < hv; i += kST * 8) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + i), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        a = better(a, ArgMax{greedy ? v[j] : v[j] * itemp + gumbel(key, i + j), i + j});
+    }
   }
+  for (int i = hv + tid; i < hi; i += kST)
+    a = better(a, ArgMax{greedy ? ld<T>(x, i) : ld<T>(x, i) * itemp + gumbel(key, i), i});
   a = block_argmax(a, sv, si);
   if (tid == 0) {
     pv[row * P + part] = a.v;
