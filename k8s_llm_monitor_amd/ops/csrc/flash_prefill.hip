@@ -289,15 +289,18 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   constexpr int D = 128, KS = D / 16, DT = D / 32;
   constexpr int WPH = 8 / G;      // waves per head
   constexpr int QR = 32 * WPH;    // query rows per workgroup
+  constexpr int Z = 128 / QR;     // workgroups per 128-row q-block
   constexpr int TILE = 32768;     // K (16 KiB) + V (16 KiB) of 64 keys
   constexpr int NBUF = 4;
   constexpr int MAXB = 2048;      // block ids per sequence staged in LDS (32k tokens)
   __shared__ __attribute__((aligned(16))) char fp2_smem[NBUF * TILE + MAXB * 4];  // ring + block ids
   int* s_blk = reinterpret_cast<int*>(fp2_smem + NBUF * TILE);
 
-  const int kvh = blockIdx.x, qb = blockIdx.y;
+  // grid (Hkv, q-blocks x Z): the Z workgroups of one q-block are dispatched back to back, on one
+  // XCD (x = kv head), so they share the block's K/V tiles in L2
+  const int kvh = blockIdx.x, qb = blockIdx.y / Z;
   const int seq = qb_seq[qb];
-  const int qs = qb_start[qb] + blockIdx.z * QR;  // first query row (new-token index) of the workgroup
+  const int qs = qb_start[qb] + (blockIdx.y % Z) * QR;  // first query row (new-token index) of the workgroup
   const int s0 = cu_seqlens[seq];
   const int L = cu_seqlens[seq + 1] - s0;
   if (qs >= L) return;  // uniform: the last q-block's upper part
@@ -512,10 +515,10 @@ extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv,
   const int G = Hq / Hkv;
   // bt_stride = the block-table width = most blocks a sequence can hold: <= 2048 - 3 fit the LDS copy
   if (ctx_start != nullptr && (G == 2 || G == 4 || G == 8) && bt_stride <= 2045) {
-    // v2: q-blocks of 128 rows split into 128 / QR workgroups (QR = 256 / G rows each)
+    // v2: q-blocks of 128 rows split into 128 / QR workgroups (QR = 256 / G rows each), adjacent in y
     const int z = 128 / (256 / G);
 #define K8S_FP2(GG)                                                                                                 \
-  hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG>), dim3(Hkv, n_qblocks, z), dim3(512), 0, s, (bf16_t*)out,   \
+  hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG>), dim3(Hkv, n_qblocks * z), dim3(512), 0, s, (bf16_t*)out,  \
                      out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,       \
                      ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride)
     switch (G) {

@@ -477,11 +477,13 @@ def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):
     return qkv, cu, cs, kc, vc, bt
 
 
+@pytest.mark.parametrize("order", ["seq", "work"])
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 8), (64, 8)])
 @pytest.mark.parametrize("cached,new", [([0, 0, 0], [1609, 7, 300]), ([48, 160, 1023], [1, 130, 129]), ([5000], [64])])
-def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new):
+def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new, order, monkeypatch):
     """The LDS-DMA paged prefill kernel (v2: tiles staged verbatim from the cache, GQA-shared) ==
-    the fp32 reference for G = 2, 4, 8 and cached prefixes."""
+    the fp32 reference for G = 2, 4, 8 and cached prefixes, under both q-block orders."""
+    monkeypatch.setenv("K8SLLM_QB_ORDER", order)
     D = 128
     qkv, cu, cs, kc, vc, bt = _paged_prefill_case(cached, new, hq, hkv, D)
     out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))

@@ -23,6 +23,7 @@ def main() -> None:
     ap.add_argument("--seqs", type=int, default=10)
     ap.add_argument("--len", type=int, default=1609)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--orders", default="work,seq", help="q-block orders to time (K8SLLM_QB_ORDER)")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     T = a.seqs * a.len
@@ -33,7 +34,7 @@ def main() -> None:
     out = torch.empty(T, Hq * D, device="cuda", dtype=torch.bfloat16)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     flops = 4 * D * Hq * a.seqs * a.len * a.len / 2
-    if True:  # the plain (cache-less) kernel
+    if os.environ.get("PLAIN", "1") == "1":  # the plain (cache-less) kernel
         for _ in range(3):
             ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out)
         torch.cuda.synchronize()
@@ -59,8 +60,16 @@ def main() -> None:
     ops.rope_and_cache(qkv, pos, torch.zeros(1, D, device="cuda"), kc, vc, slots, Hq, Hkv, D, apply_rope=False)
     cst = torch.zeros(a.seqs, dtype=torch.int32, device="cuda")
     res: dict = {}
+    qbo = {}
+    for order in a.orders.split(","):
+        os.environ["K8SLLM_QB_ORDER"] = order
+        qs, st = ops.prefill_qblocks(cu.tolist())
+        qbo[order] = (torch.tensor(qs, dtype=torch.int32, device="cuda"),
+                      torch.tensor(st, dtype=torch.int32, device="cuda"))
     for _ in range(3):
-        for tag in ("paged_v2",):
+        for order in qbo:
+            tag = f"paged_v2_{order}"
+            qb = qbo[order]
             for _ in range(3):
                 ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out, paged=(cst, kc, vc, bt))
             torch.cuda.synchronize()
