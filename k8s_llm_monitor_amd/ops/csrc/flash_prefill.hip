@@ -423,38 +423,39 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
 #pragma unroll
       for (int r = 2; r < 8; ++r) mq[c] = fmaxf(mq[c], sa[c >> 1][8 * (c & 1) + r]);
     const float mx = xor32_max(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
-    const float mnew = fmaxf(m, mx * scale_log2);
+    // Lazy max with headroom: the reference max m moves only when the tile's max exceeds it by
+    // more than 2^8 in probability (then to the exact max), so probabilities stay <= 256 - exact in
+    // fp32 and in their bf16 rounding - and O is rescaled only on such a jump, which after a row's
+    // first tiles is rare.  The rescale comes BEFORE the probabilities, so each 16-key group's
+    // exponentials -> bf16 -> 4 PV MFMAs can run back to back: the MFMAs of one group execute
+    // while the VALU computes the next group's exponentials.
+    const float mt = mx * scale_log2;
+    const float mnew = mt > m + 8.f ? mt : m;
     const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-    float rq[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i][r], scale_log2, -mnew));
-        sa[i][r] = p;
-        rq[(2 * i + (r >> 3))] += p;
-      }
-    const float rs = xor32_sum((rq[0] + rq[1]) + (rq[2] + rq[3]));
-    l = l * alpha + rs;
-    const bool grew = __builtin_amdgcn_ballot_w64(mnew > m) != 0;  // lazy rescale: O only when a max moved
-    m = mnew;
-    if (grew) {
+    if (__builtin_amdgcn_ballot_w64(mnew != m) != 0) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
     }
+    m = mnew;
+    float rq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sa[i][8 * s + j];
+        for (int j = 0; j < 8; ++j) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i][8 * s + j], scale_log2, -mnew));
+          rq[2 * i + s] += p;
+          pb[j] = (__bf16)p;
+        }
         // block 2 i + s: keys 32 i + 16 s ..
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[i][s][dt], pb, o[dt], 0, 0, 0);
       }
+    l = l * alpha + xor32_sum((rq[0] + rq[1]) + (rq[2] + rq[3]));
   };
 
   // Main loop: ONE barrier per tile; tiles t + 1 and t + 2 are in flight while tile t is
