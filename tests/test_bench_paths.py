@@ -2,6 +2,7 @@
 and POST /api/v1/analyze/pod-communication (LLM explanation) through the in-process server, the
 engine thread and continuous batching."""
 import os
+import threading
 
 import pytest
 
@@ -66,12 +67,24 @@ def test_query_client_keeps_connections(served):
     cl = QueryClient(workers=2)
     try:
         items = [(q, ctx[:300]) for ctx, q in (synthetic_context(s) for s in range(20, 22))]
+
+        def conns() -> set:
+            # one probe per worker thread (a barrier holds each worker until both have one), so
+            # every worker's connection is seen, whichever worker served the wave's requests
+            bar = threading.Barrier(2)
+
+            def probe():
+                bar.wait(timeout=10)
+                return getattr(cl._tls, "conn", None)
+
+            fs = [cl.ex.submit(probe) for _ in range(2)]
+            return {id(c) for c in (f.result() for f in fs) if c is not None}
+
         cl.post_queries(port, items, 2)
-        before = [cl.ex.submit(lambda: getattr(cl._tls, "conn", None)).result() for _ in range(4)]
+        before = conns()
         cl.post_queries(port, items, 2)
-        after = [cl.ex.submit(lambda: getattr(cl._tls, "conn", None)).result() for _ in range(4)]
-        live = [c for c in before if c is not None]
-        assert live and {id(c) for c in live} & {id(c) for c in after if c is not None}
+        after = conns()
+        assert before and before & after
     finally:
         cl.close()
 
