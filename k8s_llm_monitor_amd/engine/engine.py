@@ -947,13 +947,24 @@ class EngineService:
             if isinstance(s.user, Future) and not s.user.done():
                 s.user.set_exception(EngineOverloaded("the answer cannot finish before the deadline at the current load"))
 
-    def _drain(self, block: bool) -> None:
+    def _drain(self, block: bool, gather: bool = False) -> None:
+        """Move queued requests into the engine.  ``block``: the engine is idle - wait for one.
+        ``gather``: a full prefill step is running on the GPU and the next one is not full yet -
+        keep collecting a burst's arrivals (the wait is hidden behind the running step) so the
+        next pipelined prefill step is planned full, not with the part of the burst that happened
+        to be queued (which left a partial step plus a tiny tail step per burst)."""
+        cfg = self.engine.cfg
         try:
-            item = self._q.get(block=block, timeout=0.05 if block else None)
+            if block:
+                item = self._q.get(timeout=0.05)
+            elif gather:
+                item = self._q.get(timeout=cfg.admit_gap_ms * 1e-3)
+            else:
+                item = self._q.get_nowait()
         except queue.Empty:
             return
-        cfg = self.engine.cfg
-        coalesce = block and cfg.admit_window_ms > 0  # the engine was idle: let a burst gather
+        # the engine was idle, or gathering: let a burst gather
+        coalesce = (block or gather) and cfg.admit_window_ms > 0
         t_end = time.perf_counter() + cfg.admit_window_ms * 1e-3
         while item is not None:
             prompt, params, rid, fut, on_tokens, deadline = item
@@ -983,6 +994,27 @@ class EngineService:
     def _waiting_tokens(self) -> int:
         return sum(q.num_tokens for q in self.engine.sched.waiting)
 
+    def _gather_ok(self) -> bool:
+        """A prefill-only step at least as long as the admission window is in flight, no decode
+        step is, and the next prefill step would not be full: waiting up to the window for more of
+        the burst costs the GPU nothing."""
+        eng = self.engine
+        pf = eng._pf_inflight
+        # (on the CPU a launched step has already run: there is nothing to hide the wait behind)
+        if pf is None or eng._inflight is not None or eng.cfg.admit_window_ms <= 0 or eng.device.type != "cuda":
+            return False
+        if os.environ.get("K8SLLM_PREFILL_GATHER", "1") == "0":
+            return False
+        cap = eng.cfg.max_prefill_tokens
+        s = eng.sched
+        # the wait must be hidden: the in-flight step's estimated GPU time covers the admission
+        # window (before a prefill rate is measured: a nearly full step)
+        toks, tps = sum(pf[0].chunks), self._prefill_tps
+        hidden = toks * 1e3 / tps >= eng.cfg.admit_window_ms if tps else toks >= 0.9 * cap
+        # prefill_backlog: queued prompts that fit the free slots plus the unprefilled rest of
+        # running ones (a chunked prompt's remainder already fills the next step)
+        return hidden and len(s.running) < s.cfg.max_num_seqs and s.prefill_backlog() < cap
+
     def _push_streams(self) -> None:
         for sid, st in list(self._streams.items()):
             seq, sent, cb = st
@@ -1005,7 +1037,7 @@ class EngineService:
         eng = self.engine
         if not self._cancels.empty():
             self._apply_cancels()
-        self._drain(block=not eng.has_work())
+        self._drain(block=not eng.has_work(), gather=self._gather_ok())
         self._step_cache.clear()
         while eng.step_samples:  # GPU-event step times (back-to-back decode steps)
             self.tpot.record(*eng.step_samples.popleft())

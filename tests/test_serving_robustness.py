@@ -444,3 +444,47 @@ def test_admission_counts_the_burst_prefill_backlog():
             eng.sched.running.remove(queued)
     finally:
         svc.close()
+
+
+def test_gather_burst_behind_a_full_prefill_step():
+    """While a long enough prefill-only step runs on the GPU, the service keeps collecting a
+    burst's arrivals before planning the next (pipelined) prefill step - but only when that step
+    would not be full, no decode step is in flight, a sequence slot is free and the wait is hidden
+    (a GPU device, the step's estimated time covers the window).  (A stand-in engine: the
+    condition reads only this state.)"""
+    import types
+
+    cap = 64
+    backlog = [0]
+    sched = types.SimpleNamespace(running=[], cfg=types.SimpleNamespace(max_num_seqs=8),
+                                  prefill_backlog=lambda: backlog[0])
+    eng = types.SimpleNamespace(_pf_inflight=None, _inflight=None, sched=sched,
+                                cfg=types.SimpleNamespace(admit_window_ms=20.0, max_prefill_tokens=cap),
+                                device=types.SimpleNamespace(type="cpu"))
+    svc = types.SimpleNamespace(engine=eng, _prefill_tps=None)
+    ok = lambda: EngineService._gather_ok(svc)  # noqa: E731
+    full = types.SimpleNamespace(chunks=[cap])
+    assert not ok()  # nothing in flight
+    eng._pf_inflight = (full, None, 1)
+    assert not ok()  # CPU: a launched step has already run
+    eng.device.type = "cuda"
+    assert ok()  # a full step in flight, nothing queued behind it
+    eng._pf_inflight = (types.SimpleNamespace(chunks=[cap // 4]), None, 1)
+    assert not ok()  # a small step in flight: the wait would not be hidden
+    svc._prefill_tps = 400.0  # measured: 16 tokens take 40 ms >= the 20 ms window
+    assert ok()
+    svc._prefill_tps = 4000.0  # 4 ms: not hidden
+    assert not ok()
+    svc._prefill_tps = None
+    eng._pf_inflight = (full, None, 1)
+    eng._inflight = ([], None)
+    assert not ok()  # a decode step in flight
+    eng._inflight = None
+    backlog[0] = cap
+    assert not ok()  # the next step is already full
+    backlog[0] = 0
+    sched.running = [None] * 8
+    assert not ok()  # no free sequence slot: more arrivals could not join the next step
+    eng.cfg.admit_window_ms = 0.0
+    sched.running = []
+    assert not ok()  # coalescing disabled
