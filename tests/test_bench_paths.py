@@ -108,17 +108,23 @@ def test_bench_ranks_under_torchrun_cpu(n):
     import subprocess
     import sys
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     batch = 4 if n == 2 else 2
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n),
-                        "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch", str(batch),
-                        "--max-new-tokens", "4"], capture_output=True, text=True, timeout=600, cwd=root,
-                       env={**os.environ, "OMP_NUM_THREADS": "1"})
-    assert r.returncode == 0, r.stderr[-2000:]
+
+    def launch():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+                               str(n), "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py",
+                               "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch",
+                               str(batch), "--max-new-tokens", "4"], capture_output=True, text=True, timeout=600,
+                              cwd=root, env={**os.environ, "OMP_NUM_THREADS": "1"})
+
+    r = launch()
+    if r.returncode != 0 and ("EADDRINUSE" in r.stderr or "address already in use" in r.stderr.lower()):
+        r = launch()  # the probed master port was taken between the probe and the launch: a new one
+    assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
