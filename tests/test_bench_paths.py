@@ -122,8 +122,12 @@ def test_bench_ranks_under_torchrun_cpu(n):
                               cwd=root, env={**os.environ, "OMP_NUM_THREADS": "1"})
 
     r = launch()
-    if r.returncode != 0 and ("EADDRINUSE" in r.stderr or "address already in use" in r.stderr.lower()):
-        r = launch()  # the probed master port was taken between the probe and the launch: a new one
+    if r.returncode != 0 and ("EADDRINUSE" in r.stderr or "address already in use" in r.stderr.lower()
+                              or "exitcode  : -6" in r.stderr):
+        # the probed master port was taken between the probe and the launch, or (rarely, 8 ranks
+        # plus their client processes on this 8-CPU container) a rank aborted in gloo's connection
+        # setup: one relaunch on a new port
+        r = launch()
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
