@@ -465,9 +465,9 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   // basic block.)  The wave computes only its first nt_w tiles (later ones are in the future of
   // all its rows) but joins every barrier and issues its DMA pieces for every tile.
   const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD"
-  // item 4): waves w and w + 4 share a SIMD, and the younger half loses every arbitration
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  // (No static priority for the second-dispatched half: with each 16-key group's exponentials
+  // interleaved with the PV MFMAs it measured 1-2 % slower at 10 x 1609 and equal at 4k-16k,
+  // profiles/r04/flash_no_setprio_ab.jsonl.)
   issue(0, 0);
   if (ntiles > 1) issue(1, 1);
   if (ntiles > 2) issue(2, 2);
