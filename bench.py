@@ -35,7 +35,6 @@ import argparse
 import json
 import os
 import random
-import socket
 import statistics
 import subprocess
 import sys
@@ -88,22 +87,26 @@ def parse(argv=None):
 
 # --------------------------------------------------------------------------- launcher
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def spawn_ranks(n: int, argv: list, timeout_s: float = 0.0) -> int:
     """Run this script as ``n`` rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
     GPU each) and return the first non-zero exit code (0 when all succeed).  Called before this
     process touches any GPU; rank 0's stdout (the JSON line) is this process's stdout.  A rank that
-    fails takes the others down (they would otherwise wait in a collective forever)."""
-    port = _free_port()
+    fails takes the others down (they would otherwise wait in a collective forever).
+
+    Rendezvous: this process hosts the ranks' TCP store itself, on a port the OS picks at bind time
+    and that stays bound until the ranks are gone (K8SLLM_EXTERNAL_STORE tells init_parallel to
+    join it as a client) - no probe-then-release window in which another process can take it."""
+    import datetime
+
+    from torch.distributed import TCPStore  # CPU only: does not initialise the GPU
+
+    store = TCPStore("127.0.0.1", 0, n + 1, is_master=True, timeout=datetime.timedelta(seconds=600),
+                     wait_for_workers=False)
+    port = store.port
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), K8SLLM_EXTERNAL_STORE="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
                                       start_new_session=True))
     t0 = time.time()
@@ -432,6 +435,20 @@ def main(argv=None) -> None:
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, argv))
     run_rank(a)
+    _teardown()
+
+
+def _teardown() -> None:
+    """Orderly exit of a multi-rank run: every rank waits for every other at a barrier, then tears
+    its process groups down - no rank's process exits (closing its sockets) while a peer's
+    collective could still be talking to it."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        from k8s_llm_monitor_amd.parallel.state import barrier_all, destroy
+
+        barrier_all()
+        destroy()
 
 
 if __name__ == "__main__":

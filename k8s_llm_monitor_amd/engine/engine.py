@@ -29,7 +29,7 @@ import torch
 from ..models.checkpoint import config_from_hf, load_checkpoint
 from ..models.config import ModelConfig, get_config
 from ..models.llama import CausalLM
-from ..parallel.state import ParallelState, get_state
+from ..parallel.state import ParallelState, get_state, serving_timeouts
 from ..parallel.step_bus import KIND_DECODE, KIND_PICKLE, KIND_STOP, bus_slot_bytes, decode_message, make_step_bus
 from ..parallel.health import PeerMonitor, gather_identities
 from .block_manager import BlockManager
@@ -149,10 +149,12 @@ class LLMEngine:
 
     # ----------------------------------------------------------------- public API
     def warmup(self) -> None:
-        """Capture the decode hipGraphs (all buckets)."""
+        """Capture the decode hipGraphs (all buckets); then the TP groups take their serving
+        timeout (start-up is over: parallel/state.serving_timeouts)."""
         t0 = time.perf_counter()
         self.runner.capture_graphs()
         self.graph_s = time.perf_counter() - t0
+        serving_timeouts(self.ps)
 
     def add_request(self, prompt: Union[str, list[int]], params: Optional[SamplingParams] = None,
                     request_id: Optional[str] = None, user=None, deadline: Optional[float] = None) -> Sequence:
@@ -177,6 +179,8 @@ class LLMEngine:
         return self.sched.has_work() or self._inflight is not None or self._pf_inflight is not None
 
     PENDING = -1  # placeholder for a token sampled by the in-flight decode step
+    # tests install a callable(kind) here to inject faults into worker_loop (tests/test_tp_failure.py)
+    worker_step_hook = None
 
     def step(self) -> list[Sequence]:
         """One engine step; returns the sequences that finished.
@@ -457,14 +461,10 @@ class LLMEngine:
     def worker_loop(self) -> None:
         """Non-leader TP ranks: mirror the leader's steps (step bus) until it sends STOP."""
         pending = None
-        fault_at = int(os.environ.get("K8SLLM_FAULT_EXIT_PREFILL", "0"))  # test hook: die at the N-th prefill
-        n_prefill = 0
         while True:
             kind, payload = decode_message(self.bus.recv())
-            if kind == KIND_PICKLE and fault_at:
-                n_prefill += 1
-                if n_prefill == fault_at:
-                    os._exit(17)
+            if self.worker_step_hook is not None:  # fault injection (tests only; None in production)
+                self.worker_step_hook(kind)
             if kind == KIND_DECODE:
                 h = self.runner.decode_launch_raw(*payload)
                 if pending is not None:  # keep at most two steps enqueued (staging is double-buffered)
@@ -668,8 +668,9 @@ class EngineService:
     def __init__(self, engine: LLMEngine, max_queue: Optional[int] = None, max_failures: int = 3,
                  failure_window_s: float = 60.0, watchdog_s: Optional[float] = None):
         """``watchdog_s``: a step still in flight after this long marks the service unhealthy
-        (default ``K8SLLM_STEP_WATCHDOG_S`` or 30 s = twice the reference's 15 s write timeout;
-        a decode step takes milliseconds, a prefill step well under a second)."""
+        (default ``K8SLLM_STEP_WATCHDOG_S``, else 30 s = twice the reference's 15 s write timeout
+        at TP > 1 on the GPU - a decode step takes milliseconds, a prefill step well under a
+        second - and off otherwise; 0 disables)."""
         self.engine = engine
         self.max_queue = max_queue if max_queue is not None else 4 * engine.cfg.max_num_seqs
         self.max_failures, self.failure_window_s = max_failures, failure_window_s
@@ -696,7 +697,12 @@ class EngineService:
         self._gpu_tpot = False  # step times come from GPU events (ModelRunner._chain_event)
         engine.sched.admit_gate = self._admit_ok
         # failure detection (parallel/health.py): step watchdog + TP worker liveness
-        self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("K8SLLM_STEP_WATCHDOG_S", "30"))
+        # (default on only for TP > 1 on the GPU, where a wedged collective is what it catches; at
+        # TP = 1 or on the CPU a legitimately slow step must not 503 the service for good)
+        if watchdog_s is None:
+            env = os.environ.get("K8SLLM_STEP_WATCHDOG_S")
+            watchdog_s = float(env) if env else (30.0 if engine.ps.tp_size > 1 and engine.device.type == "cuda" else 0.0)
+        self.watchdog_s = watchdog_s
         self._step_t0: Optional[float] = None  # monotonic start of the step in flight
         self.peer_monitor = None
         if engine.ps.tp_size > 1 and engine.is_leader and engine.peer_idents:
@@ -712,7 +718,8 @@ class EngineService:
     def _watch(self) -> None:
         while not self._wd_stop.wait(0.25):
             t0 = self._step_t0
-            if self._error is None and t0 is not None and time.monotonic() - t0 > self.watchdog_s:
+            if (self._error is None and t0 is not None and self.watchdog_s > 0
+                    and time.monotonic() - t0 > self.watchdog_s):
                 self._declare_dead(EngineUnavailable(
                     f"engine step in flight for more than {self.watchdog_s:.0f} s (a TP collective is not completing)"))
             if self._error is not None:

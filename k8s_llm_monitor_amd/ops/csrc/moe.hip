@@ -90,6 +90,11 @@ __global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restric
         bv = lg[e];
         best = e;
       }
+    if (best < 0) {  // NaN logits: no comparison holds - take the first untaken expert (a valid id)
+      for (best = 0; (taken >> best) & 1u; ++best) {
+      }
+      bv = lg[best];
+    }
     taken |= 1u << best;
     pk[k] = __expf(bv - mx) / z;
     bk[k] = best;

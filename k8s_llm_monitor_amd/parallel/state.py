@@ -40,6 +40,7 @@ class ParallelState:
     dp_rank: int = 0
     tp_group: Optional[object] = None  # device collectives (RCCL on GPU, gloo on CPU)
     cpu_group: Optional[object] = None  # gloo group spanning the TP group, for control broadcast
+    bus_group: Optional[object] = None  # gloo group of the step bus: no serving timeout (idle waits)
     device: torch.device = torch.device("cpu")
     custom_ar: Optional[object] = None  # one-shot IPC all-reduce for small TP messages (custom_ar.py)
 
@@ -103,27 +104,51 @@ def init_parallel(tp_size: int = 1, device: Optional[str] = None, backend: Optio
             kw = {}
             if be == "nccl":
                 kw["device_id"] = dev
+            if os.environ.get("K8SLLM_EXTERNAL_STORE") == "1":
+                # the launcher (bench.py spawn_ranks) hosts the store on a port it holds bound
+                kw["store"] = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), ws + 1,
+                                            is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
             dist.init_process_group(be, rank=rank, world_size=ws,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         be = dist.get_backend()
-        # every rank must create every group, in the same order.  The TP groups carry the serving
-        # steps' collectives: their timeout (K8SLLM_TP_TIMEOUT_S, default 60 s) bounds how long a
-        # rank can block on a dead peer before the process-group watchdog aborts it (the engine's
-        # PeerMonitor / step watchdog mark /health 503 within seconds, parallel/health.py); the
-        # default group keeps ``timeout_s`` for start-up (model init, graph capture).
-        tp_to = datetime.timedelta(seconds=float(os.environ.get("K8SLLM_TP_TIMEOUT_S", "60")))
+        # every rank must create every group, in the same order.  The TP groups start with the
+        # start-up bound ``timeout_s``: their first collectives (custom all-reduce self-test and
+        # handle exchange, step-bus set-up, identity exchange, warm-up and graph-capture
+        # all-reduces) wait for the slowest rank's weight load.  serving_timeouts() lowers them to
+        # K8SLLM_TP_TIMEOUT_S once the engine is warm (LLMEngine.warmup).  The step bus has a group
+        # of its own that is never bounded: a worker waits in it for as long as the server is idle.
+        up = datetime.timedelta(seconds=timeout_s)
+        idle = datetime.timedelta(days=7)
         for g in range(ws // tp_size):
             ranks = list(range(g * tp_size, (g + 1) * tp_size))
-            grp = dist.new_group(ranks, timeout=tp_to) if tp_size > 1 else None
-            cpu = (dist.new_group(ranks, backend="gloo", timeout=tp_to) if (tp_size > 1 and be != "gloo")
+            grp = dist.new_group(ranks, timeout=up) if tp_size > 1 else None
+            cpu = (dist.new_group(ranks, backend="gloo", timeout=up) if (tp_size > 1 and be != "gloo")
                    else grp)
+            bus = dist.new_group(ranks, backend="gloo", timeout=idle) if tp_size > 1 else None
             if rank in ranks:
-                st.tp_group, st.cpu_group = grp, cpu
+                st.tp_group, st.cpu_group, st.bus_group = grp, cpu, bus
         from .custom_ar import maybe_create
 
         st.custom_ar = maybe_create(st)  # GPU, TP 2..8, self-test vs RCCL passed (K8SLLM_CUSTOM_AR=0: off)
     set_state(st)
     return st
+
+
+def serving_timeouts(st: Optional[ParallelState] = None) -> None:
+    """Lower the TP groups' collective timeout from the start-up bound to the serving bound
+    (K8SLLM_TP_TIMEOUT_S, default 60 s): how long a rank can block on a dead peer before the
+    process-group watchdog aborts it (the engine's PeerMonitor / step watchdog mark /health 503
+    within seconds, parallel/health.py).  The step-bus group keeps no bound."""
+    import datetime
+
+    st = st or get_state()
+    if st.tp_size == 1 or not (dist.is_available() and dist.is_initialized()):
+        return
+    to = datetime.timedelta(seconds=float(os.environ.get("K8SLLM_TP_TIMEOUT_S", "60")))
+    from torch.distributed.distributed_c10d import _set_pg_timeout
+
+    for g in {id(x): x for x in (st.tp_group, st.cpu_group) if x is not None}.values():
+        _set_pg_timeout(to, g)
 
 
 def barrier_all() -> None:

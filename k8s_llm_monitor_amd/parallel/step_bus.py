@@ -33,13 +33,20 @@ DECODE_HDR = 4  # int32 words in front of a raw decode message: kind, n, b, n_el
 
 
 class GlooStepBus:
+    """``broadcast_object_list`` over the TP group's step-bus gloo group (``ps.bus_group``).  That
+    group has no serving timeout: a worker sits in the broadcast for as long as the server is idle,
+    so a bounded group would kill every worker after an idle gap (the TP collective groups get the
+    short serving bound, parallel/state.py).  A dead leader still surfaces: gloo raises as soon as
+    the leader's socket closes."""
+
     def __init__(self, ps):
         self.ps = ps
         self.src = ps.rank - ps.tp_rank
+        self.group = getattr(ps, "bus_group", None) or ps.cpu_group
 
     def _bcast(self, obj):
         lst = [obj]
-        dist.broadcast_object_list(lst, src=self.src, group=self.ps.cpu_group)
+        dist.broadcast_object_list(lst, src=self.src, group=self.group)
         return lst[0]
 
     def send_raw(self, words: np.ndarray) -> None:
@@ -65,11 +72,14 @@ class ShmStepBus:
     """Leader publishes into a native shared-memory ring; worker ``tp_rank - 1`` is reader index
     ``tp_rank - 1``.  Collective over the TP group's CPU group (name exchange + barrier)."""
 
-    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 60.0, poll_s: float = 1.0):
+    def __init__(self, ps, slot_bytes: int, nslots: int = 4, timeout_s: float = 60.0, poll_s: float = 1.0,
+                 beat_s: float = 1.0, silent_s: float = 30.0):
         """``timeout_s`` bounds the LEADER's publish back-pressure (a worker that stopped consuming).
         A worker waits for the next step without a deadline - an idle server publishes nothing for
         as long as no request arrives - and polls the leader's liveness every ``poll_s`` instead,
-        so a dead leader still surfaces (ConnectionError) rather than hanging the worker."""
+        so a dead leader still surfaces (ConnectionError) rather than hanging the worker: through
+        /proc when the worker can see the leader's process, else through the ring's heartbeat word,
+        which a leader thread bumps every ``beat_s`` (a leader silent for ``silent_s`` is gone)."""
         from ..runtime import native_runtime
 
         rt = native_runtime()
@@ -77,8 +87,9 @@ class ShmStepBus:
             raise RuntimeError("native StepChannel unavailable")
         self.ps = ps
         self.timeout_s = timeout_s
-        self.idle_timeout_s = 600.0  # worker's bound on silence when it cannot observe the leader
+        self.silent_s = silent_s  # worker's bound on a still heartbeat when it cannot observe the leader
         self.poll_s = poll_s
+        self._beat_stop = None
         src = ps.rank - ps.tp_rank
         name = [f"/k8sllm_step_{os.getpid()}_{uuid.uuid4().hex[:12]}" if ps.tp_rank == 0 else None]
         ok = [True]
@@ -103,6 +114,17 @@ class ShmStepBus:
                 self.ch.close()
             raise RuntimeError("shared-memory step channel unavailable on some TP rank")
         self.reader = ps.tp_rank - 1
+        if ps.tp_rank == 0:
+            import threading
+
+            self._beat_stop = threading.Event()
+            self._beat = threading.Thread(target=self._beat_loop, args=(beat_s,), name="step-bus-heartbeat",
+                                          daemon=True)
+            self._beat.start()
+
+    def _beat_loop(self, beat_s: float) -> None:
+        while not self._beat_stop.wait(beat_s):
+            self.ch.heartbeat()
 
     def _publish(self, data) -> None:
         if not self.ch.publish(data, self.timeout_s):
@@ -118,9 +140,10 @@ class ShmStepBus:
         self._publish(struct.pack("<i", KIND_STOP))
 
     def set_leader(self, ident: tuple) -> None:
-        """The leader's (pid, start time, host) from the engine's identity exchange: the liveness
-        poll below is used only if this worker can see that process (same host and pid namespace,
-        matching start time); otherwise the wait for a step is bounded by ``timeout_s`` instead."""
+        """The leader's (pid, start time, host) from the engine's identity exchange: the /proc
+        liveness poll below is used only if this worker can see that process (same host and pid
+        namespace, matching start time); otherwise the ring's heartbeat word tells whether the
+        leader still runs (``silent_s``)."""
         from .health import visible
 
         self.leader_ident = ident
@@ -131,7 +154,7 @@ class ShmStepBus:
 
         import time
 
-        t0 = time.monotonic()
+        beat, t_beat = self.ch.beats, time.monotonic()
         while True:
             m = self.ch.recv(self.reader, self.poll_s)
             if m is not None:
@@ -143,11 +166,18 @@ class ShmStepBus:
             elif self.leader_visible:
                 if alive(ident) is False:
                     raise ConnectionError(f"TP leader (pid {ident[0]}) exited without sending STOP")
-            elif time.monotonic() - t0 > self.idle_timeout_s:
-                raise ConnectionError(f"no step from the TP leader for {self.idle_timeout_s:.0f} s "
-                                      "(leader process not observable from this worker)")
+            else:
+                b, now = self.ch.beats, time.monotonic()
+                if b != beat:
+                    beat, t_beat = b, now
+                elif now - t_beat > self.silent_s:
+                    raise ConnectionError(f"TP leader heartbeat silent for {self.silent_s:.0f} s "
+                                          "(leader process not observable from this worker)")
 
     def close(self) -> None:
+        if self._beat_stop is not None:  # the thread must be gone before the ring is unmapped
+            self._beat_stop.set()
+            self._beat.join()
         self.ch.close()
 
 

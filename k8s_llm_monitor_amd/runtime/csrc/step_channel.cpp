@@ -38,6 +38,7 @@ struct alignas(64) ChanHeader {
   uint64_t nslots, slot_bytes, nreaders;
   alignas(64) std::atomic<uint64_t> seq;  // messages published
   alignas(64) std::atomic<uint64_t> ack[CHAN_MAX_READERS + 1];  // per reader: messages consumed
+  alignas(64) std::atomic<uint64_t> beat;  // leader liveness: bumped every second while the leader runs
   uint64_t len[CHAN_MAX_SLOTS];           // byte length of the message in each slot
 };
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "lock-free 64-bit atomics required");
@@ -88,6 +89,7 @@ class StepChannel {
       hdr_->nreaders = (uint64_t)nreaders;
       hdr_->seq.store(0, std::memory_order_relaxed);
       for (auto& a : hdr_->ack) a.store(0, std::memory_order_relaxed);
+      hdr_->beat.store(0, std::memory_order_relaxed);
       std::atomic_thread_fence(std::memory_order_release);
       hdr_->magic = CHAN_MAGIC;
     } else if (hdr_->magic != CHAN_MAGIC || size_ < sizeof(ChanHeader) + hdr_->nslots * hdr_->slot_bytes) {
@@ -99,6 +101,12 @@ class StepChannel {
 
   int64_t slot_bytes() const { return (int64_t)hdr_->slot_bytes; }
   int64_t published() const { return (int64_t)hdr_->seq.load(std::memory_order_acquire); }
+
+  // Leader liveness without a message: an idle leader publishes no step for as long as no request
+  // arrives, so its heartbeat thread bumps this word instead; a worker that cannot observe the
+  // leader's process (another pid namespace) reads it to tell "idle" from "gone".
+  void heartbeat() { hdr_->beat.fetch_add(1, std::memory_order_release); }
+  int64_t beats() const { return (int64_t)hdr_->beat.load(std::memory_order_acquire); }
 
   // Leader: publish one message; waits (GIL released) while its slot still holds a message some
   // reader has not consumed.  False on timeout.
@@ -206,5 +214,7 @@ void register_step_channel(py::module_& m) {
       .def("unlink", &StepChannel::unlink)
       .def("close", &StepChannel::close_)
       .def_property_readonly("slot_bytes", &StepChannel::slot_bytes)
+      .def("heartbeat", &StepChannel::heartbeat)
+      .def_property_readonly("beats", &StepChannel::beats)
       .def_property_readonly("published", &StepChannel::published);
 }

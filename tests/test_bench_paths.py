@@ -104,30 +104,22 @@ def test_bench_ranks_under_torchrun_cpu(n):
     run's largest point), one JSON line from rank 0 with the whole-job value, n_gpus n and dp<n>
     parallelism."""
     import json
-    import socket
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     batch = 4 if n == 2 else 2
 
-    def launch():
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-                               str(n), "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py",
-                               "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "llama-tiny", "--batch",
-                               str(batch), "--max-new-tokens", "4"], capture_output=True, text=True, timeout=600,
-                              cwd=root, env={**os.environ, "OMP_NUM_THREADS": "1"})
-
-    r = launch()
-    if r.returncode != 0 and ("EADDRINUSE" in r.stderr or "address already in use" in r.stderr.lower()
-                              or "exitcode  : -6" in r.stderr):
-        # the probed master port was taken between the probe and the launch, or (rarely, 8 ranks
-        # plus their client processes on this 8-CPU container) a rank aborted in gloo's connection
-        # setup: one relaunch on a new port
-        r = launch()
+    # --standalone: torchrun binds its own rendezvous store on a port the OS picks (no probed port
+    # that another process can take before the launch); 127.0.0.1 as the task's rendezvous rule asks
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nnodes=1", "--nproc-per-node", str(n), "bench.py", "--gpus", str(n), "--steps", "1",
+                        "--warmup", "1", "--model", "llama-tiny", "--batch", str(batch), "--max-new-tokens", "4"],
+                       capture_output=True, text=True, timeout=600, cwd=root, env={**os.environ, "OMP_NUM_THREADS": "1"})
+    if r.returncode != 0:  # keep the failing ranks' stderr for the record (no relaunch)
+        os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(root, "gpurun_out", f"torchrun_{n}_ranks_failure.err"), "w") as f:
+            f.write(r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout

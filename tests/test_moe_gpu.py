@@ -141,3 +141,23 @@ def test_moe_router_matches_linear_route_scatter(T, E, K):
     torch.testing.assert_close(w, rw, rtol=1e-5, atol=1e-6)
     ref_wd = torch.zeros(T, E, device="cuda").scatter_(1, rids.long(), rw)
     torch.testing.assert_close(wd, ref_wd, rtol=1e-5, atol=1e-6)
+
+
+def test_moe_router_nan_rows_pick_valid_experts():
+    """A row whose router logits are NaN (a poisoned activation) must still yield K distinct, valid
+    expert ids and write only inside its own dense weight row (best = -1 indexed
+    wd[t*E - 1], the neighbouring row)."""
+    T, E, K, d = 4, 8, 2, 4096
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(T, d, device="cuda", generator=g).to(torch.bfloat16)
+    x[1, 5] = float("nan")
+    wr = (torch.randn(E, d, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    ids, w, wd = ops.moe_router(x, wr, K, True)
+    ids = ids.cpu()
+    assert ((ids >= 0) & (ids < E)).all()
+    assert all(len(set(r.tolist())) == K for r in ids)
+    # the healthy rows are untouched by the poisoned one: same result as routing them alone
+    keep = torch.tensor([0, 2, 3], device="cuda")
+    ids2, w2, wd2 = ops.moe_router(x[keep].contiguous(), wr, K, True)
+    assert torch.equal(ids[keep.cpu()], ids2.cpu())
+    torch.testing.assert_close(wd[keep], wd2)

@@ -38,10 +38,20 @@ def _get(port, path, body=None):
 def _rank(rank, world, port, mode, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), K8SLLM_STEP_BUS="shm")
-    if mode == "mid_prefill" and rank == 1:
-        os.environ["K8SLLM_FAULT_EXIT_PREFILL"] = "2"  # the worker dies on the second prefill step
     torch.set_num_threads(2)
     from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
+    from k8s_llm_monitor_amd.parallel.step_bus import KIND_PICKLE
+
+    if mode == "mid_prefill" and rank == 1:  # the worker dies on the second prefill step
+        seen = [0]
+
+        def hook(kind):
+            if kind == KIND_PICKLE:
+                seen[0] += 1
+                if seen[0] == 2:
+                    os._exit(17)
+
+        LLMEngine.worker_step_hook = staticmethod(hook)
     from k8s_llm_monitor_amd.parallel.state import init_parallel
 
     try:
@@ -114,3 +124,78 @@ def test_tp_worker_death_turns_health_503_and_fails_requests(mode):
     assert res["pending"] in ("EngineUnavailable", "EngineOverloaded", "RuntimeError"), res
     assert res["health1"] == 503, res
     assert res["query_status"] == 503, res
+
+
+def _idle_rank(rank, world, port, bus, q):
+    """A TP=2 engine that stays idle longer than the TP groups' serving timeout between two
+    requests: the workers wait on the step bus, which must not time out (the gloo bus
+    shared the bounded TP group; a worker that cannot observe its leader's process gave up after
+    10 idle minutes on the shm bus)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), K8SLLM_STEP_BUS=bus, K8SLLM_TP_TIMEOUT_S="2")
+    torch.set_num_threads(2)
+    from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine, SamplingParams
+    from k8s_llm_monitor_amd.parallel import step_bus
+    from k8s_llm_monitor_amd.parallel.state import init_parallel
+
+    if bus == "shm":  # as if the leader lived in another pid namespace: only the heartbeat tells
+        orig = step_bus.ShmStepBus.set_leader
+
+        def set_leader(self, ident):
+            orig(self, ident)
+            self.leader_visible, self.silent_s = False, 3.0
+
+        step_bus.ShmStepBus.set_leader = set_leader
+    try:
+        ps = init_parallel(tp_size=world, device="cpu")
+        eng = LLMEngine(EngineConfig(model="llama-tiny", max_num_seqs=4, max_model_len=256, num_blocks=64,
+                                     use_graphs=False, seed=5, dtype="float32", admit_window_ms=0),
+                        device="cpu", pstate=ps)
+        eng.warmup()  # the TP groups now carry the 2 s serving timeout
+        if ps.tp_rank != 0:
+            eng.worker_loop()
+            q.put((rank, "worker done"))
+            q.close()
+            q.join_thread()
+            os._exit(0)
+        svc = EngineService(eng, watchdog_s=30.0)
+        sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+        res = {"bus": type(eng.bus).__name__}
+        res["first"] = len(svc.submit("pod default/api CrashLoopBackOff", sp).result(timeout=120)[1].output_ids)
+        time.sleep(6.0)  # idle: 3x the serving timeout, 2x the worker's heartbeat bound
+        res["second"] = len(svc.submit("node-003 NotReady", sp).result(timeout=120)[1].output_ids)
+        res["healthy"] = svc.healthy
+        svc.close()
+        q.put((rank, res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "ERR " + repr(e) + traceback.format_exc()))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("bus", ["gloo", "shm"])
+def test_tp_idle_gap_longer_than_serving_timeout(bus):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_rank, args=(r, 2, port, bus, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        while len(got) < 2:
+            rank, res = q.get(timeout=240)
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    res = got[0]
+    assert not isinstance(res, str), res
+    assert res["bus"] == ("GlooStepBus" if bus == "gloo" else "ShmStepBus"), res
+    assert res["first"] == 4 and res["second"] == 4 and res["healthy"], res
+    assert got[1] == "worker done", got[1]
