@@ -242,13 +242,15 @@ class CausalLM:
             y += L["bo"]
         return tp_all_reduce(y, self.ps)
 
-    def _attn_core(self, L: dict, x: torch.Tensor, meta: AttnMeta, kv, slabs: Optional[tuple] = None,
+    def _attn_core(self, L: dict, x: Optional[torch.Tensor], meta: AttnMeta, kv, slabs: Optional[tuple] = None,
                    rows: Optional[int] = None, rownorm: Optional[tuple] = None,
-                   rowscale: Optional[tuple] = None) -> torch.Tensor:
+                   rowscale: Optional[tuple] = None, fused: Optional[tuple] = None) -> torch.Tensor:
         """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
         ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM over ``x`` (row-major
         or fragment-packed with ``rows`` valid rows), reduced inside rope_and_cache; the attention
-        output is then written fragment-packed for the o_proj skinny GEMM."""
+        output is then written fragment-packed for the o_proj skinny GEMM.  ``fused = (nslabs,
+        norm_w, residual)``: ``x`` is None and the QKV GEMM builds its own normed input from the
+        previous layer's down-projection slabs (_proj_slabs)."""
         c = self.cfg
         k_cache, v_cache = kv if kv is not None else (None, None)
         partial, ns = None, 0
@@ -257,7 +259,7 @@ class CausalLM:
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
         if slabs is not None:
             ws, splits = slabs
-            ns = self._proj_slabs(L, "wqkv", x, T, splits, rownorm)
+            ns = self._proj_slabs(L, "wqkv", x, T, splits, rownorm, fused=fused)
             if self._attn_rope and not meta.is_prefill and k_cache is not None and c.arch == "llama":
                 # the attention kernel reduces the slabs, applies RoPE and writes the new k / v
                 out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device)
@@ -627,6 +629,7 @@ class CausalLM:
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         self.lm_head_d = None
+        self._fuse_norm, self._seam = False, None
         for L in self.layers:  # (re)built below from the current weights
             for key in ("wqkv_d", "wo_d", "w13_d", "w2_d"):
                 L.pop(key, None)
@@ -670,6 +673,14 @@ class CausalLM:
         split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split
         self._init_dec()
+        # the add-RMSNorm between two decode projections inside the consuming GEMM (gate_up, the
+        # next layer's qkv): ops.dec_gemm_fused_norm.  TP=1 (at TP>1 the norm lives in the
+        # all-reduce tail), decode copies present, and the GPU not shared by several rank
+        # processes (a rehearsal: the fused launch's grid seam needs its workgroups resident)
+        self._fuse_norm = (self.tp == 1 and bool(self.layers) and "w13_d" in self.layers[0] and d % 512 == 0
+                           and os.environ.get("K8SLLM_FUSED_NORM", "1") != "0"
+                           and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0" and not os.environ.get("K8SLLM_DEVICE"))
+        self._seam = ops.SeamState(self.device) if self._fuse_norm else None
 
         def most(N: int, K: int) -> int:
             s_rm = split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
@@ -693,9 +704,11 @@ class CausalLM:
         M = residual.shape[0]
         # first = layer 0's (A operand, rownorm), already produced with the embedding (embed_norm_partial)
         xw, rn = first if first is not None else self._norm_tail(residual, None, 0, self.layers[0]["attn_norm"])
+        pend = None  # (nslabs, norm_w, residual): the next QKV GEMM runs the pending add-RMSNorm itself
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
-            op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
+            op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn, fused=pend)
+            pend = None
             ns = self._proj_slabs(L, "wo", op, M, self._split_o)
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
                 # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated
@@ -713,6 +726,12 @@ class CausalLM:
                 return self._logits(xr)
             if c.is_moe:
                 ns = self._moe_skinny(L, residual, ws, ns, M)
+            elif self._fuse_norm and "w13_d" in L:
+                # residual += o; the gate_up GEMM's first phase builds its own normed input
+                act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
+                ops.dec_gemm_fused_norm(L["w13_d"], 2, M, residual, ws, ns, L["mlp_norm"], eps,
+                                        self._seam.counters[1], self._seam.err, out=act)
+                ns = self._proj_slabs(L, "w2", act, M, self._split_d)
             else:
                 xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
                 if "w13_d" in L:
@@ -722,6 +741,9 @@ class CausalLM:
                     act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
                 ns = self._proj_slabs(L, "w2", act, M, self._split_d)
             if i + 1 < n:
+                if self._fuse_norm and not c.is_moe and "wqkv_d" in self.layers[i + 1]:
+                    pend, xw, rn = (ns, self.layers[i + 1]["attn_norm"], residual), None, None
+                    continue
                 xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
         # final norm feeds the LM head: fragment-packed for the decode GEMM (gemm_decode.hip), or
         # complete and row-major for hipBLASLt where no decode copy of the head exists
@@ -759,12 +781,18 @@ class CausalLM:
         act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 
-    def _proj_slabs(self, L: dict, key: str, x: torch.Tensor, rows: int, split: int,
-                    rownorm: Optional[tuple] = None) -> int:
+    def _proj_slabs(self, L: dict, key: str, x: Optional[torch.Tensor], rows: int, split: int,
+                    rownorm: Optional[tuple] = None, fused: Optional[tuple] = None) -> int:
         """Split-K slabs of a decode projection into the shared workspace: the shared-A decode
         GEMM over the packed copy ``L[key + "_d"]`` where one exists, else gemm_skinny over
-        ``L[key + "_p"]``.  Returns the slab count."""
+        ``L[key + "_p"]``.  ``fused = (nslabs, norm_w, residual)``: the GEMM first adds the
+        workspace's ``nslabs`` slabs to the residual and builds its own normed A (one launch,
+        ops.dec_gemm_fused_norm).  Returns the slab count."""
         wd = L.get(key + "_d")
+        if fused is not None:
+            nsl, norm_w, residual = fused
+            return ops.dec_gemm_fused_norm(wd, 0, rows, residual, self._skinny_ws, nsl, norm_w, self.cfg.norm_eps,
+                                           self._seam.counters[0], self._seam.err, workspace=self._skinny_ws)
         if wd is not None:
             return ops.dec_gemm(x, wd, 0, rows, workspace=self._skinny_ws, rownorm=rownorm)
         return ops.skinny_slabs(x, L[key + "_p"], self._skinny_ws, split, rows=rows, rownorm=rownorm)

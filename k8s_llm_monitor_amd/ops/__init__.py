@@ -428,10 +428,54 @@ def dec_gemm(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: 
         out.copy_(pack_activation((torch.nn.functional.silu(g) * u).to(a.dtype)))
         return 1
     rn = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
-    r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn)
+    r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn, None, 0, None, None, None, None)
     if r < 0:
         raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
     return r
+
+
+class SeamState:
+    """Device words of the fused-norm GEMMs' grid seam (gemm_decode.hip DecNorm): 8 monotonic
+    shard counters (int64, 128 B apart) per call site, and one give-up flag shared by all.
+    Zeroed once; the counters only grow, so hipGraph replays need no re-initialisation.  One
+    call site = one launch shape (every launch on a state must use the same grid)."""
+
+    def __init__(self, device, sites: int = 2):
+        self.counters = [torch.zeros(8 * 16, dtype=torch.int64, device=device) for _ in range(sites)]
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def failed(self) -> bool:
+        """True once any seam spin gave up (a workgroup was not resident: its outputs are wrong)."""
+        return bool(self.err.item())
+
+
+def dec_gemm_fused_norm(wp: torch.Tensor, epi: int, rows: int, residual: torch.Tensor, slabs: torch.Tensor,
+                        nslabs: int, norm_w: torch.Tensor, eps: float, seam: torch.Tensor, err: torch.Tensor,
+                        workspace: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> int:
+    """add_norm_partial + dec_gemm in ONE launch: the GEMM's first phase adds the previous
+    projection's ``nslabs`` split-K slabs to ``residual`` (in place) and builds this GEMM's A
+    operand (residual * norm_w, fragment-packed) and the rows' sums of squares, handed to every
+    workgroup through a grid seam (``seam`` counters, ``err`` give-up flag: SeamState); the GEMM
+    then runs on them with the deferred 1/rms row scale.  ``slabs`` may be the same workspace the
+    GEMM's own slab epilogue writes (epi 0): every slab read precedes the seam.  Falls back to the
+    two launches where the fused one cannot run (shape, configuration, more workgroups than CUs).
+    Returns what dec_gemm returns."""
+    M, d = residual.shape[0], residual.shape[1]
+    xw = packed_empty(rows, d, residual.dtype, residual.device)
+    ss = torch.empty(rows, d // 512, dtype=torch.float32, device=residual.device)
+    if _gpu(residual) and nslabs <= 8:
+        N, K = skinny_wdims(wp)
+        cfg = dec_config(N, K, epi)
+        if cfg is not None:
+            S, ntw, waves, depth = cfg
+            r = native().gemm_dec(xw, wp, workspace, out, S, epi, ntw, waves, depth, rows, ss, float(eps), slabs,
+                                  nslabs, residual, norm_w, seam, err)
+            if r >= 0:
+                return r
+            if r != -2:
+                raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
+    add_norm_partial(residual, slabs, nslabs, norm_w, out=xw, ss_part=ss)
+    return dec_gemm(xw, wp, epi, rows, workspace=workspace, out=out, rownorm=(ss, eps))
 
 
 def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int, norm_w: torch.Tensor,

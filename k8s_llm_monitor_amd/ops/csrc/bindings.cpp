@@ -54,6 +54,7 @@ int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, 
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
 int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K, int splits,
                     int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc, int rn_d, float rn_eps,
+                    const float* np_slabs, int np_S, void* np_resid, const void* np_w, void* np_seam, int* np_err,
                     hipStream_t s);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
@@ -565,9 +566,18 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
 // returns S = splits; epi 1: y [M, N] bf16 (row stride y.stride(0)); epi 2: packed SwiGLU
 // y [ceil(M/16), N/64, 64, 8].  Returns the slab count (1 for epi 1/2); -1 if the configuration
 // is not available (the caller falls back to gemm_skinny).
+//
+// Fused add-RMSNorm prologue (np_slabs given; gemm_decode.hip DecNorm): the launch first reduces
+// np_nslabs fp32 slabs [S][M][K] into the bf16 residual [M][K] (in place) and WRITES a (resid *
+// np_w, fragment-packed) and rn_ss ([M][K/512] sums of squares) before its GEMM reads them, through
+// a grid seam on np_seam (>= 8 x 16 int64, zeroed once, one per call site).  np_err (int32 [1])
+// turns 1 if a seam spin gave up.  Returns -2 when the prologue cannot run for this launch (grid
+// larger than the CU count, shape, configuration): the caller then runs add_norm_partial first.
 int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial, c10::optional<torch::Tensor> y,
                  int64_t splits, int64_t epi, int64_t ntw, int64_t waves, int64_t depth, int64_t rows,
-                 c10::optional<torch::Tensor> rn_ss, double rn_eps) {
+                 c10::optional<torch::Tensor> rn_ss, double rn_eps, c10::optional<torch::Tensor> np_slabs,
+                 int64_t np_nslabs, c10::optional<torch::Tensor> np_resid, c10::optional<torch::Tensor> np_w,
+                 c10::optional<torch::Tensor> np_seam, c10::optional<torch::Tensor> np_err) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   TORCH_CHECK(wp.dim() == 4 && wp.is_contiguous() && wp.size(2) == 64 && wp.size(3) == 8,
               "gemm_dec: wp must be fragment-packed [N/16, K/32, 64, 8]");
@@ -600,8 +610,35 @@ int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor>
   const float* rp = nullptr;
   int rn_nc = 0;
   rownorm_args(rn_ss, M, K, rp, rn_nc);
+  const float* nsp = nullptr;
+  void *nrp = nullptr, *nsm = nullptr;
+  const void* nwp = nullptr;
+  int* nerr = nullptr;
+  if (np_slabs.has_value()) {
+    TORCH_CHECK(np_slabs->is_cuda() && np_slabs->scalar_type() == torch::kFloat32 && np_slabs->is_contiguous() &&
+                    np_slabs->numel() >= np_nslabs * M * K && np_nslabs >= 1,
+                "gemm_dec: np_slabs must be contiguous fp32 with nslabs x M x K elements");
+    TORCH_CHECK(np_resid.has_value() && np_w.has_value() && np_seam.has_value() && np_err.has_value() &&
+                    rp != nullptr, "gemm_dec: the fused norm needs resid, w, seam, err and rn_ss");
+    dev_bf16(*np_resid, "np_resid");
+    dev_bf16(*np_w, "np_w");
+    TORCH_CHECK(np_resid->dim() == 2 && np_resid->is_contiguous() && np_resid->size(0) >= M && np_resid->size(1) == K,
+                "gemm_dec: np_resid [M, K]");
+    TORCH_CHECK(np_w->numel() == K && np_w->is_contiguous(), "gemm_dec: np_w [K]");
+    TORCH_CHECK(np_seam->is_cuda() && np_seam->scalar_type() == torch::kInt64 && np_seam->numel() >= 8 * 16,
+                "gemm_dec: np_seam int64 [>= 128]");
+    TORCH_CHECK(np_err->is_cuda() && np_err->scalar_type() == torch::kInt32 && np_err->numel() >= 1,
+                "gemm_dec: np_err int32 [1]");
+    nsp = np_slabs->data_ptr<float>();
+    nrp = np_resid->data_ptr();
+    nwp = np_w->data_ptr();
+    nsm = np_seam->data_ptr();
+    nerr = np_err->data_ptr<int>();
+  }
   const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, ldy, M, N, K, (int)splits, (int)epi, (int)ntw,
-                                 (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, cur());
+                                 (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, nsp, (int)np_nslabs, nrp, nwp,
+                                 nsm, nerr, cur());
+  if (rc == -6) return -2;
   if (rc < 0) return -1;
   check(rc, "gemm_dec");
   return epi == 0 ? splits : 1;
