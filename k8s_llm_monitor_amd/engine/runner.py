@@ -93,9 +93,22 @@ class ModelRunner:
         self.graph_pool = None
         self.n_steps = {"prefill": 0, "decode": 0}
         self.on_launched = None  # hook after every step's launch (TP: enqueue the custom-AR error readback)
+        # TP > 1 prefill as two micro-batches whose all-reduces overlap the other's compute
+        # (K8SLLM_TP_OVERLAP=0: one batch, serial all-reduces)
+        self.overlap = model.overlap_ok()
         self._last_ev = None  # end event of the last launched step (_chain_event)
 
     # --------------------------------------------------------------------- helpers
+    @staticmethod
+    def _micro_split(cu: np.ndarray, nd: int) -> int:
+        """First sequence of the second prefill micro-batch: the split nearest half the rows (0:
+        no split - a mixed step, or a single sequence)."""
+        S = len(cu) - 1
+        if nd or S < 2:
+            return 0
+        k = int(np.argmin(np.abs(cu[1:S] - cu[S] / 2))) + 1
+        return k
+
     def bucket_for(self, n: int) -> int:
         for b in self.buckets:
             if b >= n:
@@ -147,9 +160,20 @@ class ModelRunner:
         paged = any(starts)
         W = max(len(s.block_table) for s in seqs) if paged else 0
         Wd = max(len(q.block_table) for q in decode) if nd else 0
+        # TP > 1: two micro-batches of whole sequences, so one's row-parallel all-reduces overlap
+        # the other's compute (models/llama.py _prefill_overlap); their own cu_seqlens / q-block
+        # schedules / logits rows ride in the same staging copy
+        kA = self._micro_split(cu, nd) if self.overlap else 0
+        mb = None
+        if kA:
+            cuA, cuB = cu[: kA + 1], cu[kA:] - cu[kA]
+            mb = (ops.prefill_qblocks(cuA.tolist(), ctx_starts=starts[:kA]),
+                  ops.prefill_qblocks(cuB.tolist(), ctx_starts=starts[kA:]))
         # layout of the staging buffer (int32 words; the float sampling parameters bit-cast)
         sizes = dict(ids=T, pos=T, slots=T, cu=len(seqs) + 1, qs=nq, st=nq, lidx=R, temp=R, topk=R, topp=R,
-                     cst=len(seqs) if paged else 0, bt=len(seqs) * W, dbt=nd * Wd, dlen=nd)
+                     cst=len(seqs) if paged else 0, bt=len(seqs) * W, dbt=nd * Wd, dlen=nd,
+                     mcu=len(seqs) + 2 if kA else 0, mqs=nq if kA else 0, mst=nq if kA else 0,
+                     mlidx=len(seqs) if kA else 0)
         off, o = {}, 0
         for k, n in sizes.items():
             off[k] = o
@@ -192,6 +216,14 @@ class ModelRunner:
             for i, q in enumerate(decode):
                 dbt[i, : len(q.block_table)] = q.block_table
             v["dlen"][:] = [q.num_tokens for q in decode]
+        if kA:
+            v["mcu"][: kA + 1] = cuA
+            v["mcu"][kA + 1:] = cuB
+            nqA = len(mb[0][0])
+            v["mqs"][:nqA], v["mst"][:nqA] = mb[0]
+            v["mqs"][nqA:], v["mst"][nqA:] = mb[1]
+            v["mlidx"][:kA] = cuA[1:] - 1
+            v["mlidx"][kA:] = cuB[1:] - 1
         d = buf[: sum(sizes.values())].to(dev, non_blocking=True)
         dv = {k: d[off[k]:off[k] + n] for k, n in sizes.items()}
         meta = AttnMeta(is_prefill=True, positions=dv["pos"], slot_mapping=dv["slots"], cu_seqlens=dv["cu"],
@@ -199,6 +231,20 @@ class ModelRunner:
         if paged:
             meta.ctx_start = dv["cst"]
             meta.block_tables = dv["bt"].view(len(seqs), W)
+        if kA:
+            TA, S_ = int(cu[kA]), len(seqs)
+            parts = []
+            for (r0, r1), (s0, s1), (q0, q1) in ((((0, TA), (0, kA), (0, nqA))),
+                                                 ((TA, T), (kA, S_), (nqA, nq))):
+                m = AttnMeta(is_prefill=True, positions=dv["pos"][r0:r1], slot_mapping=dv["slots"][r0:r1],
+                             cu_seqlens=dv["mcu"][s0 + (s0 > 0): s1 + 1 + (s0 > 0)], qb_seq=dv["mqs"][q0:q1],
+                             qb_start=dv["mst"][q0:q1], logits_idx=dv["mlidx"][s0:s1].long())
+                if paged:
+                    m.ctx_start = dv["cst"][s0:s1]
+                    m.block_tables = dv["bt"].view(S_, W)[s0:s1]
+                parts.append(m)
+            meta.micro = (parts[0], parts[1], TA)
+            self.n_steps["overlapped"] = self.n_steps.get("overlapped", 0) + 1
         if nd:
             meta.num_decode = nd
             meta.dec_block_tables = dv["dbt"].view(nd, Wd)

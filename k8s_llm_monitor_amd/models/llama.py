@@ -37,7 +37,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import reference as ref
-from ..parallel.comm import kv_head_range, shard_range, tp_all_gather_last, tp_all_gather_rows, tp_all_reduce, tp_all_to_all
+from ..parallel.comm import (kv_head_range, shard_range, tp_all_gather_last, tp_all_gather_rows, tp_all_reduce,
+                             tp_all_reduce_async, tp_all_to_all)
 from ..parallel.state import ParallelState, get_state
 from .config import ModelConfig
 
@@ -69,6 +70,9 @@ class AttnMeta:
     # previous step sampled, still on the device), else ids[i]; resolved inside the first kernel
     dec_src: Optional[torch.Tensor] = None  # [B] int32
     dec_prev: Optional[torch.Tensor] = None  # [>= B] int32
+    # TP > 1 prefill as two micro-batches of whole sequences: (meta of rows [0, TA), meta of rows
+    # [TA, T), TA); their row-parallel all-reduces overlap each other's compute (_prefill_overlap)
+    micro: Optional[tuple] = None
 
 
 def _seed_for(name: str, seed: int) -> int:
@@ -526,6 +530,8 @@ class CausalLM:
                 return self._decode_layers_skinny(None, residual, meta, kv_caches)
             if self._fused_norm_ok(h):
                 return self._logits(self._prefill_fused_norm(residual, meta, kv_caches))
+            if meta.micro is not None and self.overlap_ok():
+                return self._logits(self._prefill_overlap(residual, meta, kv_caches))
             x = ops.rms_norm(h, self.layers[0]["attn_norm"], c.norm_eps)
             n = len(self.layers)
             for i, L in enumerate(self.layers):
@@ -541,6 +547,63 @@ class CausalLM:
                         residual = residual[meta.logits_idx].contiguous()
                     x = ops.fused_add_rms_norm(y.contiguous(), residual, self.final_norm, c.norm_eps)
         return self._logits(x)
+
+    def overlap_ok(self) -> bool:
+        """TP > 1 dense Llama prefill may run as two overlapped micro-batches (_prefill_overlap;
+        K8SLLM_TP_OVERLAP=0 disables)."""
+        return (self.tp > 1 and self.cfg.arch == "llama" and not self.cfg.is_moe and bool(self.layers)
+                and "bqkv" not in self.layers[0] and os.environ.get("K8SLLM_TP_OVERLAP", "1") != "0")
+
+    def _mlp_local(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+        """Dense SwiGLU MLP of this rank's F shard, before the row-parallel all-reduce."""
+        if self._w13_il:
+            h = ops.prefill_linear(x, L["w13"], swiglu=True)
+        else:
+            h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=False)
+        return ops.prefill_linear(h, L["w2"])
+
+    def _prefill_overlap(self, residual: torch.Tensor, meta: AttnMeta, kv_caches: Optional[list]) -> torch.Tensor:
+        """Tensor-parallel prefill with the row-parallel all-reduces hidden behind compute
+        (SURVEY.md §2.12 C-1 / C-2): the step's sequences form two micro-batches A and B (the
+        runner's split, meta.micro) and every all-reduce is issued asynchronously (RCCL runs it on
+        its own stream; the consumer waits on it just before use), so per layer
+
+            attn A, o A, [AR A] | attn B, o B, [AR B] | norm A, mlp A, [AR2 A] | norm B, mlp B, [AR2 B]
+
+        each all-reduce runs beside the other micro-batch's next compute segment (AR2 B beside the
+        next layer's attention of A).  Row-wise the arithmetic is the serial form's: the same
+        GEMMs, norms and sums per row, split by sequence (attention never crosses sequences)."""
+        c = self.cfg
+        eps = c.norm_eps
+        mA, mB, TA = meta.micro
+        metas = (mA, mB)
+        rs = (residual[:TA], residual[TA:])
+        x0 = ops.rms_norm(residual, self.layers[0]["attn_norm"], eps)
+        xs = [x0[:TA], x0[TA:]]
+        pend = [None, None]  # (y, work): a micro-batch's MLP output and its all-reduce in flight
+        for i, L in enumerate(self.layers):
+            kv = kv_caches[i] if kv_caches is not None else None
+            ys, works = [None, None], [None, None]
+            for b in (0, 1):
+                if pend[b] is not None:
+                    y2, w2 = pend[b]
+                    w2.wait()
+                    xs[b] = ops.fused_add_rms_norm(y2, rs[b], L["attn_norm"], eps)
+                o = self._attn_core(L, xs[b], metas[b], kv)
+                ys[b] = ops.prefill_linear(o, L["wo"])
+                works[b] = tp_all_reduce_async(ys[b], self.ps)
+            for b in (0, 1):
+                works[b].wait()
+                xb = ops.fused_add_rms_norm(ys[b], rs[b], L["mlp_norm"], eps)
+                y2 = self._mlp_local(L, xb)
+                pend[b] = (y2, tp_all_reduce_async(y2, self.ps))
+        outs = []
+        for b in (0, 1):
+            y2, w2 = pend[b]
+            w2.wait()
+            idx = metas[b].logits_idx
+            outs.append(ops.fused_add_rms_norm(y2[idx].contiguous(), rs[b][idx].contiguous(), self.final_norm, eps))
+        return torch.cat(outs)
 
     def _fused_norm_ok(self, h: torch.Tensor) -> bool:
         """Dense Llama-family prefill at TP=1 on the tile GEMMs: the RMSNorms between projections
@@ -629,7 +692,7 @@ class CausalLM:
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         self.lm_head_d = None
-        self._fuse_norm, self._seam = False, None
+        self._fuse_norm, self._seam, self._rc_o = False, None, False
         for L in self.layers:  # (re)built below from the current weights
             for key in ("wqkv_d", "wo_d", "w13_d", "w2_d"):
                 L.pop(key, None)
@@ -673,14 +736,6 @@ class CausalLM:
         split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split
         self._init_dec()
-        # the add-RMSNorm between two decode projections inside the consuming GEMM (gate_up, the
-        # next layer's qkv): ops.dec_gemm_fused_norm.  TP=1 (at TP>1 the norm lives in the
-        # all-reduce tail), decode copies present, and the GPU not shared by several rank
-        # processes (a rehearsal: the fused launch's grid seam needs its workgroups resident)
-        self._fuse_norm = (self.tp == 1 and bool(self.layers) and "w13_d" in self.layers[0] and d % 512 == 0
-                           and os.environ.get("K8SLLM_FUSED_NORM", "1") != "0"
-                           and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0" and not os.environ.get("K8SLLM_DEVICE"))
-        self._seam = ops.SeamState(self.device) if self._fuse_norm else None
 
         def most(N: int, K: int) -> int:
             s_rm = split if split else max(ops.skinny_auto_splits(m, N, K) for m in (1, 33, 64))
@@ -692,6 +747,28 @@ class CausalLM:
         # MoE: the EP all-to-all decode runs up to 128 received rows per grouped launch
         rows = ops.SKINNY_GROUPED_MAX_M if c.is_moe else ops.SKINNY_MAX_M
         self._skinny_ws = torch.empty(n * rows, dtype=torch.float32, device=self.device)
+        self.set_decode_fusion(seam=False, rc=False)
+
+    def set_decode_fusion(self, seam: bool = False, rc: bool = False) -> None:
+        """Two measured-and-shelved alternatives to the decode step's add_norm_partial launches
+        (profiles/r05/README.md; both bit-compatible with the default path, both off by default):
+
+        * ``seam`` - the add-RMSNorm runs as the first phase of the consuming GEMM (gate_up, the
+          next layer's qkv) behind an in-launch grid seam (ops.dec_gemm_fused_norm): neutral - the
+          seam's chain (slab reads, write-through stores, fan-in, A re-read) costs what the launch
+          it replaces did;
+        * ``rc`` - the o projection row-complete, residual add and the gate_up GEMM's norm operands
+          in its epilogue, no split-K slabs (ops.dec_gemm_rc): neutral - re-reading the attention
+          output from L2 in every workgroup costs what the slab round trip did.
+
+        Both need TP=1, the decode weight copies and a GPU not shared by several rank processes
+        (the seam's workgroups must be resident together)."""
+        c = self.cfg
+        ok = (self.tp == 1 and not c.is_moe and bool(self.layers) and "w13_d" in self.layers[0]
+              and c.d_model % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0")
+        self._fuse_norm = bool(seam) and ok and not os.environ.get("K8SLLM_DEVICE")
+        self._seam = ops.SeamState(self.device) if self._fuse_norm else None
+        self._rc_o = bool(rc) and ok and "wo_d" in self.layers[0]
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list], first: Optional[tuple] = None) -> torch.Tensor:
@@ -709,6 +786,22 @@ class CausalLM:
             kv = kv_caches[i] if kv_caches is not None else None
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn, fused=pend)
             pend = None
+            rc = None
+            if self._rc_o and "w13_d" in L:
+                # o projection row-complete: residual += o and the gate_up GEMM's normed input in
+                # the same launch (no split-K slabs, no add_norm launch)
+                rc = ops.dec_gemm_rc(op, L["wo_d"], M, residual, L["mlp_norm"], eps)
+            if rc is not None:
+                xw, rn = rc
+                act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
+                ops.dec_gemm(xw, L["w13_d"], 2, M, out=act, rownorm=rn)
+                ns = self._proj_slabs(L, "w2", act, M, self._split_d)
+                if i + 1 < n:
+                    if self._fuse_norm and "wqkv_d" in self.layers[i + 1]:
+                        pend, xw, rn = (ns, self.layers[i + 1]["attn_norm"], residual), None, None
+                    else:
+                        xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
+                continue
             ns = self._proj_slabs(L, "wo", op, M, self._split_o)
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
                 # EP all-to-all MoE: residual += o (all-reduced), then the complete, replicated

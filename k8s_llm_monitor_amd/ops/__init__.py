@@ -434,6 +434,37 @@ def dec_gemm(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: 
     return r
 
 
+def dec_gemm_rc(a: torch.Tensor, wp: torch.Tensor, rows: int, residual: torch.Tensor, norm_w: torch.Tensor,
+                eps: float) -> Optional[tuple]:
+    """Row-complete decode GEMM (gemm_dec_rc_kernel) for a residual-producing projection:
+    ``residual += a . W^T`` in place (no split-K slabs) and the next GEMM's deferred-RMSNorm
+    operands in the same launch: returns ``(xw, (ss, eps))`` - xw = residual * norm_w
+    fragment-packed, ss [rows, N/16] per-16-column sums of squares - or None where the kernel does
+    not tile the shape (the caller keeps slabs + add_norm_partial).  CPU: the fp32 reference with
+    the same 8 K-slices summed in slice order."""
+    N, K = skinny_wdims(wp)
+    M = rows
+    if K % 256 or N % 32 or M > 64:
+        return None
+    xw = packed_empty(M, N, residual.dtype, residual.device)
+    ss = torch.empty(M, N // 16, dtype=torch.float32, device=residual.device)
+    if not _gpu(a):
+        x = _cpu_a(a, rows).float()
+        w = _cpu_w(wp)
+        kc = K // 8
+        h = residual[:M].float()
+        for s in range(8):
+            h = h + x[:, s * kc:(s + 1) * kc] @ w[:, s * kc:(s + 1) * kc].t()
+        residual[:M] = h.to(residual.dtype)
+        v = residual[:M].float()
+        ss.copy_((v * v).view(M, N // 16, 16).sum(-1))
+        xw.copy_(pack_activation((v * norm_w.float()).to(residual.dtype)))
+        return xw, (ss, eps)
+    if not native().gemm_dec_rc(a, wp, residual, norm_w, xw, ss, rows):
+        return None
+    return xw, (ss, eps)
+
+
 class SeamState:
     """Device words of the fused-norm GEMMs' grid seam (gemm_decode.hip DecNorm): 8 monotonic
     shard counters (int64, 128 B apart) per call site, and one give-up flag shared by all.
@@ -969,8 +1000,8 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
                     out[a:b] = one(x[a:b], w[e])
         return out
     rs_part, rs_eps = rowscale if rowscale is not None else (None, 1e-5)
-    if rowscale is not None and algo != 1:
-        raise ValueError("gemm_tile: the row scale needs schedule 1")
+    if rowscale is not None and algo not in (1, 2):
+        raise ValueError("gemm_tile: the row scale needs schedule 1 or the ping-pong kernel (2)")
     if rope is not None:
         pos, cs, heads = rope
         native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads, rs_part, rs_eps)
@@ -1001,7 +1032,7 @@ def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_
         hw.copy_((h.float() * norm_w.float()).to(hw.dtype))
         ss.copy_((h.float() ** 2).view(M, N // 128, 128).sum(2))
         return hw, ss
-    native().gemm_tile(resid, x.contiguous(), w, None, False, 1, None, None, 0, None, 1e-5, resid, hw,
+    native().gemm_tile(resid, x.contiguous(), w, None, False, TILE_ALGO, None, None, 0, None, 1e-5, resid, hw,
                        norm_w.contiguous(), ss)
     return hw, ss
 
@@ -1018,7 +1049,9 @@ QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fuse
 # residual-add RMSNorm folded into the o / down epilogues and the qkv / gate_up row scale
 FUSED_NORM = os.environ.get("K8SLLM_FUSED_NORM", "1") != "0"
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
-TILE_ALGO = 1  # refill schedule: two barriers per k-tile
+# 1: the 4-wave kernel's two-barrier schedule; 2: the 8-wave ping-pong kernel (csrc/gemm_pp.hip,
+# bit-identical, 5-6 % slower at the Llama-3-8B shapes: profiles/r05/README.md)
+TILE_ALGO = 1
 
 
 def tile_shape_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:

@@ -56,6 +56,9 @@ int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long
                     int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc, int rn_d, float rn_eps,
                     const float* np_slabs, int np_S, void* np_resid, const void* np_w, void* np_seam, int* np_err,
                     hipStream_t s);
+void k8sllm_gemm_pp_sched(int sch);
+int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, const void* nw, void* xw, float* ss, int M, int N,
+                       int K, hipStream_t s);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
                             const void* w, int d, float* ss_part, hipStream_t s);
 int k8sllm_embed_norm_partial(void* out, long out_stride, void* residual, const int* ids, const int* src,
@@ -403,7 +406,7 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  TORCH_CHECK(algo == 0 || algo == 1, "gemm_tile: algo 0 (one barrier per k-tile) or 1 (two)");
+  TORCH_CHECK(algo >= 0 && algo <= 2, "gemm_tile: algo 0 (one barrier per k-tile), 1 (two) or 2 (8-wave ping-pong)");
   TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
               "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
   TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (swiglu ? N / 2 : N), "gemm_tile: y shape");
@@ -642,6 +645,31 @@ int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor>
   if (rc < 0) return -1;
   check(rc, "gemm_dec");
   return epi == 0 ? splits : 1;
+}
+
+// Row-complete decode GEMM + residual add + deferred-norm operands (gemm_decode.hip
+// gemm_dec_rc_kernel): a packed [ceil(M/16), K/32, 64, 8] (`rows` valid), wp packed [N/16, K/32,
+// 64, 8]; resid [M, N] bf16 += a . wp^T (in place); xw packed [ceil(M/16), N/32, 64, 8] = resid *
+// nw; ss [M, N/16] fp32 per-16-column sums of resid^2.  Returns false for a shape it does not tile.
+bool gemm_dec_rc(torch::Tensor a, torch::Tensor wp, torch::Tensor resid, torch::Tensor nw, torch::Tensor xw,
+                 torch::Tensor ss, int64_t rows) {
+  dev_bf16(a, "a"); dev_bf16(wp, "wp"); dev_bf16(resid, "resid"); dev_bf16(nw, "nw"); dev_bf16(xw, "xw");
+  TORCH_CHECK(wp.dim() == 4 && wp.is_contiguous() && wp.size(2) == 64 && wp.size(3) == 8, "gemm_dec_rc: wp packed");
+  const int N = (int)wp.size(0) * 16, K = (int)wp.size(1) * 32, M = (int)rows;
+  TORCH_CHECK(a.dim() == 4 && a.is_contiguous() && a.size(1) * 32 == K && a.size(2) == 64 && a.size(3) == 8 &&
+                  M > 0 && M <= 64 && (M + 15) / 16 <= a.size(0), "gemm_dec_rc: a packed [ceil(M/16), K/32, 64, 8]");
+  TORCH_CHECK(resid.dim() == 2 && resid.is_contiguous() && resid.size(0) >= M && resid.size(1) == N,
+              "gemm_dec_rc: resid [M, N]");
+  TORCH_CHECK(nw.numel() == N && nw.is_contiguous(), "gemm_dec_rc: nw [N]");
+  TORCH_CHECK(xw.dim() == 4 && xw.is_contiguous() && xw.size(0) == (M + 15) / 16 && xw.size(1) * 32 == N,
+              "gemm_dec_rc: xw packed [ceil(M/16), N/32, 64, 8]");
+  TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == torch::kFloat32 && ss.is_contiguous() && ss.dim() == 2 &&
+                  ss.size(0) >= M && ss.size(1) == N / 16, "gemm_dec_rc: ss [M, N/16] fp32");
+  const int rc = k8sllm_gemm_dec_rc(a.data_ptr(), wp.data_ptr(), resid.data_ptr(), nw.data_ptr(), xw.data_ptr(),
+                                    ss.data_ptr<float>(), M, N, K, cur());
+  if (rc == -1) return false;
+  check(rc, "gemm_dec_rc");
+  return true;
 }
 
 // Grouped (MoE) skinny GEMM: wp [E, N/16, K/32, 64, 8] (one packed weight per local expert).
@@ -897,6 +925,8 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
   m.def("gemm_dec", &gemm_dec);
+  m.def("gemm_dec_rc", &gemm_dec_rc);
+  m.def("gemm_pp_sched", [](int64_t sch) { k8sllm_gemm_pp_sched((int)sch); });
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);

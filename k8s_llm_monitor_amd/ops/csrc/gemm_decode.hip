@@ -65,7 +65,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dec_rsrc(const void* base, lon
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
 }
 constexpr int kSC1 = 16;  // buffer-op aux bits: sc1 (write-through stores / L1-bypassing loads)
-constexpr int kRnMax = 4;  // deferred-norm partials per thread (rows of up to 16 partials: K <= 8192)
+constexpr int kRnMax = 4;   // narrow deferred-norm rows: up to 16 partials (4 per thread)
+constexpr int kRnWide = 16;  // wide rows: up to 256 partials (16 x 16 B per thread)
 
 constexpr int kDecCH = 8;  // k-steps (32 deep) per A chunk
 
@@ -76,7 +77,7 @@ struct DecGeom {
   static constexpr int NLD = (PIECES + 64 * WAVES - 1) / (64 * WAVES);  // staging loads per thread
 };
 
-template <int MT, int NTW, int WAVES, int EPI, int DEPTH, bool NP>
+template <int MT, int NTW, int WAVES, int EPI, int DEPTH, bool NP, bool RNW = false>
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
@@ -176,17 +177,32 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
     asm volatile("" ::: "memory");  // no load of A is moved above the seam (s_barrier is no memory op)
   }
 
-  // ---- the A rows' partial sums of squares (deferred RMSNorm): up to 4 kRnMax per row, 4 per
-  // thread, loaded first so their wait below is a counted one (the NP seam: sc1 loads)
+  // ---- the A rows' partial sums of squares (deferred RMSNorm), 4 threads per row, loaded first so
+  // their wait below is a counted one (the NP seam: sc1 loads).  Narrow rows (<= 16 partials:
+  // add_norm_partial's per-512-column sums) one float per load; wide rows (16 | partials <= 256:
+  // gemm_dec_rc_kernel's per-16-column sums) 16-byte loads, each thread a quarter of the row.
+  // (RNW: the wide form, a compile-time choice - the host picks the instantiation by rn_nc)
   float rnv[kRnMax];  // no initial value: read only under the same condition (no join wait)
-  if (rn_ss != nullptr && threadIdx.x < MT * 64 && rn_nc <= 4 * kRnMax) {
+  f32x4 rnw[RNW ? kRnWide : 1];
+  const bool rn_narrow = !RNW && rn_nc <= 4 * kRnMax, rn_wide = RNW && rn_nc % 16 == 0 && rn_nc <= 16 * kRnWide;
+  if (rn_ss != nullptr && threadIdx.x < MT * 64 && (rn_narrow || rn_wide)) {
     const int row = min((int)(threadIdx.x >> 2), M - 1), part = threadIdx.x & 3;
     const __amdgpu_buffer_rsrc_t ss_rs = dec_rsrc(rn_ss, (long)M * rn_nc * 4);
+    if constexpr (!RNW) {
 #pragma unroll
-    for (int j = 0; j < kRnMax; ++j) {
-      const uint32_t off = (uint32_t)((row * rn_nc + min(part + 4 * j, rn_nc - 1)) * 4);
-      rnv[j] = __uint_as_float(NP ? __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, kSC1)
-                                  : __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, 0));
+      for (int j = 0; j < kRnMax; ++j) {
+        const uint32_t off = (uint32_t)((row * rn_nc + min(part + 4 * j, rn_nc - 1)) * 4);
+        rnv[j] = __uint_as_float(NP ? __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, kSC1)
+                                    : __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, 0));
+      }
+    } else {
+      const int q = rn_nc >> 2;  // this thread's quarter: floats part*q .. part*q + q - 1
+#pragma unroll
+      for (int j = 0; j < (RNW ? kRnWide : 1); ++j) {
+        const uint32_t off = (uint32_t)((row * rn_nc + part * q + min(4 * j, q - 4)) * 4);
+        rnw[j] = __builtin_bit_cast(f32x4, NP ? __builtin_amdgcn_raw_buffer_load_b128(ss_rs, off, 0, kSC1)
+                                              : __builtin_amdgcn_raw_buffer_load_b128(ss_rs, off, 0, 0));
+      }
     }
   }
 
@@ -238,13 +254,20 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   if (rn_ss != nullptr && threadIdx.x < MT * 64) {
     const int rl = threadIdx.x >> 2, part = threadIdx.x & 3;
     float ss = 0.f;
-    if (rn_nc <= 4 * kRnMax) {
+    if (rn_narrow) {
 #pragma unroll
       for (int j = 0; j < kRnMax; ++j) {
         asm volatile("" : "+v"(rnv[j]));  // keeps the first use (and its wait) here, past the ring issue
         ss += part + 4 * j < rn_nc ? rnv[j] : 0.f;
       }
-    } else {  // wide rows: a plain loop (no decode GEMM today)
+    } else if (rn_wide) {
+      const int q = rn_nc >> 2;
+#pragma unroll
+      for (int j = 0; j < (RNW ? kRnWide : 1); ++j) {
+        asm volatile("" : "+v"(rnw[j][0]), "+v"(rnw[j][1]), "+v"(rnw[j][2]), "+v"(rnw[j][3]));
+        if (4 * j < q) ss += (rnw[j][0] + rnw[j][1]) + (rnw[j][2] + rnw[j][3]);
+      }
+    } else {  // other widths: a plain loop (no decode GEMM today)
       const int row = min(rl, M - 1);
       for (int c = part; c < rn_nc; c += 4) ss += rn_ss[row * rn_nc + c];
     }
@@ -352,6 +375,97 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   }
 }
 
+
+// Row-complete decode GEMM for a row-parallel projection feeding a residual add (the o projection
+// of a TP=1 decode step): NO split-K slabs.  Each workgroup owns one 16-column n-tile for all M
+// rows and the whole K; its 8 waves split K (one eighth each, the slices the split-K kernel's 8
+// slabs had), stream their weight fragments AND their activation fragments straight into a
+// register ring (the activations are L2-resident: every workgroup reads all of them), and reduce
+// through LDS in slice order.  The epilogue then does what add_norm_partial_kernel did as its own
+// launch over 8 MB of fp32 slabs:
+//   resid <- bf16(resid + y)  (y summed slice by slice, in the slab kernel's order: bit-identical),
+//   xw    <- bf16(resid * w)  fragment-packed as the next GEMM's A operand,
+//   ss[row][tile] <- sum over the tile's 16 columns of resid^2 (the consumer's deferred RMSNorm
+//                    sums N/16 partials per row).
+// One launch and 16 MB of slab traffic fewer per layer; the price is the activation re-read from
+// L2 (M x K bf16 per workgroup).
+template <int MT, int DEPTH, int NKS>
+__global__ __launch_bounds__(512, 1) void gemm_dec_rc_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                             bf16_t* __restrict__ resid, const bf16_t* __restrict__ nw,
+                                                             bf16_t* __restrict__ xw, float* __restrict__ ss_out,
+                                                             int M, int N, int K) {
+  constexpr int WAVES = 8;
+  __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][MT][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int tile = blockIdx.x;
+  const int ksteps = K >> 5;  // host: ksteps == 8 NKS
+  constexpr int nks = NKS;     // k-steps per wave: compile-time, so every ring wait is a counted one
+  const int kb = wave * nks;
+  const u32x4* wp = reinterpret_cast<const u32x4*>(W) + ((long)tile * ksteps + kb) * 64 + lane;
+  const u32x4* ap[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) ap[m] = reinterpret_cast<const u32x4*>(A) + ((long)m * ksteps + kb) * 64 + lane;
+  u32x4 rw[DEPTH], ra[DEPTH][MT];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) {
+    rw[d] = __builtin_nontemporal_load(wp + d * 64);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) ra[d][m] = ap[m][d * 64];
+  }
+  f32x4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k0 = 0; k0 < nks; k0 += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, rw[d]);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[d][m]), b, acc[m], 0, 0, 0);
+      const int kn = k0 + d + DEPTH;
+      if (kn < nks) {  // compile-time
+        rw[d] = __builtin_nontemporal_load(wp + kn * 64);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) ra[d][m] = ap[m][kn * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) red[wave][m][lane] = acc[m];
+  __syncthreads();
+  if (wave >= MT) return;
+  // wave m: m-tile m.  C layout: col = lane & 15, rows (lane >> 4) * 4 + r
+  const int m = wave;
+  const int col = tile * 16 + (lane & 15);
+  const float wcol = bf2f(nw[col]);
+  float ssr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = m * 16 + (lane >> 4) * 4 + r;
+    const int rowc = min(row, M - 1);
+    float h = bf2f(resid[(long)rowc * N + col]);
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) h += red[w][m][lane][r];  // slice order = the slab kernel's
+    const bf16_t hb = f2bf(h);
+    const float hv = bf2f(hb);
+    ssr[r] = hv * hv;
+    if (row < M) {
+      resid[(long)row * N + col] = hb;
+      xw[act_index(row, col, -(long)(N >> 5))] = f2bf(hv * wcol);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = ssr[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, kWave);  // the 16 columns of the row
+    const int row = m * 16 + (lane >> 4) * 4 + r;
+    if ((lane & 15) == 0 && row < M) ss_out[(long)row * (N >> 4) + tile] = v;
+  }
+}
+
 }  // namespace k8sllm
 
 using namespace k8sllm;
@@ -394,10 +508,13 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
   }
   const DecNorm dn{np_slabs, np_S, (bf16_t*)np_resid, (const bf16_t*)np_w, (unsigned long long*)np_seam, np_err};
   int rc = -5;
-#define K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, NPV)                                                                      \
-  hipLaunchKernelGGL((gemm_dec_kernel<MTV, NTWV, WV, EPV, DV, NPV>), grid, blk, 0, s, (const bf16_t*)A,              \
+  const bool rnw = rn_ss != nullptr && rn_nc > 4 * kRnMax;  // the wide deferred-norm form (gemm_dec_rc sums)
+  if (rnw && (rn_nc % 16 || rn_nc > 16 * kRnWide || np)) return -1;
+#define K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, RW)                                                                 \
+  hipLaunchKernelGGL((gemm_dec_kernel<MTV, NTWV, WV, EPV, DV, NPV, RW>), grid, blk, 0, s, (const bf16_t*)A,          \
                      (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kchunk, rn_ss, rn_nc, inv_d, rn_eps, dn); \
   rc = 0
+#define K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, NPV) K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, false)
 #define K8S_DEC(MTV, NTWV, WV, EPV, DV) K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, false)
 #define K8S_DEC_M(NTWV, WV, EPV, DV) \
   switch (MT) {                      \
@@ -420,6 +537,20 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_MNP(1, 7, DEC_SWIGLU8, 16) }
 #undef K8S_DEC_MNP
     if (rc) return -6;
+    return (int)hipGetLastError();
+  }
+  if (rnw) {  // consumers of gemm_dec_rc's per-16-column partials: gate_up (the o projection's consumer)
+#define K8S_DEC_MW(NTWV, WV, EPV, DV) \
+  switch (MT) {                       \
+    case 1: K8S_DEC_NPW(1, NTWV, WV, EPV, DV, false, true); break; \
+    case 2: K8S_DEC_NPW(2, NTWV, WV, EPV, DV, false, true); break; \
+    case 3: K8S_DEC_NPW(3, NTWV, WV, EPV, DV, false, true); break; \
+    default: K8S_DEC_NPW(4, NTWV, WV, EPV, DV, false, true); break; \
+  }
+    if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 8) }
+    else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 16) }
+#undef K8S_DEC_MW
+    if (rc) return rc;
     return (int)hipGetLastError();
   }
   // configurations (ntw, waves, depth) per epilogue: the ones the launcher's table picks plus
@@ -451,6 +582,32 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
 #undef K8S_DEC_M
 #undef K8S_DEC
 #undef K8S_DEC_NP
+#undef K8S_DEC_NPW
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+
+// Row-complete decode GEMM (gemm_dec_rc_kernel): A packed [ceil(M/16)][K/32][64][8], Wp packed
+// [N/16][K/32][64][8]; resid [M][N] bf16 updated in place; xw packed [ceil(M/16)][N/32][64][8];
+// ss [M][N/16] fp32.  Returns -1 for a shape the kernel does not tile.
+extern "C" int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, const void* nw, void* xw, float* ss,
+                                  int M, int N, int K, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (M > 64 || N % 32 || K % 32 || (K / 32) % 8) return -1;
+  const int nks = K / 32 / 8;
+  const int MT = (M + 15) / 16;
+  const dim3 grid(N / 16), blk(512);
+#define K8S_RC(MTV, DV)                                                                                            \
+  hipLaunchKernelGGL((gemm_dec_rc_kernel<MTV, DV, 16>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp,    \
+                     (bf16_t*)resid, (const bf16_t*)nw, (bf16_t*)xw, ss, M, N, K)
+  if (nks != 16) return -1;  // K = 4096 (the o projection of Llama-3-8B / Mixtral at TP=1)
+  switch (MT) {
+    case 1: K8S_RC(1, 8); break;
+    case 2: K8S_RC(2, 8); break;
+    case 3: K8S_RC(3, 8); break;
+    default: K8S_RC(4, 8); break;
+  }
+#undef K8S_RC
   return (int)hipGetLastError();
 }

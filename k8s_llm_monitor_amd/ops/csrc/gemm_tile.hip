@@ -49,6 +49,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "tile_epi.h"
 
 namespace k8sllm {
 
@@ -61,45 +62,6 @@ __device__ __forceinline__ void vm_wait_n() {
 }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 }  // namespace
-
-enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2, TILE_EPI_RESID = 3 };
-
-// Fused epilogues of the dense prefill projections.
-//
-// TILE_EPI_ROPE (the qkv projection): the output columns are heads of 128; a wave's 128-column
-// quarter is exactly one head, and for q / k heads (head < rope_heads) the rotary embedding (neox
-// pairs i, i + 64) is applied to the staged bf16 rows before they are stored - rope_cache's
-// separate read-rotate-write pass over q / k disappears.
-//
-// TILE_EPI_RESID (o / down, the residual producers): resid <- bf16(resid + bf16(y)) in place,
-// hw <- bf16(resid * norm_w) (the next RMSNorm's weighted input, NOT yet divided by the row's rms)
-// and ss_out[row][c] <- sum of resid^2 over the 128 columns c*128 .. c*128+127 - the fused
-// residual-add RMSNorm pass between two projections becomes part of the producer's epilogue.
-//
-// RS (row scale, the consumers qkv / gate_up that read hw): every output row is multiplied by
-// rsqrt(sum_c rs_part[row][c] / K + rs_eps) before its epilogue - the deferred half of the RMSNorm
-// (a row scale commutes with the projection; SwiGLU and RoPE see the normalised values).
-struct TileEpi {
-  const int* positions;  // ROPE: [M] absolute position of each row
-  const float* cos_sin;  // ROPE: [max_pos][128]: cos (64) | sin (64)
-  int rope_heads;        // ROPE: Hq + Hkv: heads 0 .. rope_heads - 1 are rotated
-  const float* rs_part;  // RS: [M][rs_np] partial sums of squares of the A rows
-  int rs_np;             // RS: partials per row (K / 128, <= 64)
-  float rs_eps;
-  bf16_t* resid;         // RESID: [M][N] residual stream, updated in place
-  bf16_t* hw;            // RESID: [M][N] resid * norm_w
-  const bf16_t* norm_w;  // RESID: [N] the next RMSNorm's weight
-  float* ss_out;         // RESID: [M][N / 128]
-};
-
-// sum over the 16 lanes of a DPP row (lanes 16r .. 16r + 15), the total in every lane
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));  // row_ror:2
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));  // row_ror:1
-  return v;
-}
 
 template <int EPI, bool GROUPED, int SCH, bool RS = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
@@ -537,11 +499,23 @@ using namespace k8sllm;
 // Grouped: W [E][N][K] with expert stride w_es elements; M = total expert-sorted rows (the grid
 // bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
 // Shapes: N % 16 == 0 (SwiGLU: N % 256 == 0), K % 64 == 0.  algo: the refill schedule (0 or 1).
+extern "C" int k8sllm_gemm_pp(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
+                              long w_es, int epi, const int* rope_pos, const float* rope_cs, int rope_heads,
+                              const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw, const void* norm_w,
+                              float* ss_out, hipStream_t s);
+
+// algo 2: the 8-wave ping-pong schedule (gemm_pp.hip), same contract.
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
                                 long w_es, int epi, int algo, const int* rope_pos, const float* rope_cs,
                                 int rope_heads, const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw,
                                 const void* norm_w, float* ss_out, hipStream_t s) {
   if (M <= 0) return 0;
+  if (algo == 2) {
+    if (K >= 128 && !(epi == TILE_EPI_RESID && N % 256))
+      return k8sllm_gemm_pp(X, W, Y, M, N, K, offsets, E, w_es, epi, rope_pos, rope_cs, rope_heads, rs_part, rs_np,
+                            rs_eps, resid, hw, norm_w, ss_out, s);
+    algo = 1;  // shapes the ping-pong kernel does not take: the 4-wave kernel
+  }
   const bool grouped = offsets != nullptr;
   const bool rs = rs_part != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;

@@ -34,6 +34,32 @@ def tp_all_reduce(x: torch.Tensor, ps=None) -> torch.Tensor:
     return x
 
 
+class _Done:
+    """A completed collective (TP 1, or one that ran synchronously)."""
+
+    def wait(self) -> None:
+        pass
+
+
+_DONE = _Done()
+
+
+def tp_all_reduce_async(x: torch.Tensor, ps=None):
+    """In-place sum over the TP group, returned as a handle whose ``wait()`` must precede any use
+    of ``x``.  RCCL: the collective runs on the process group's own stream after the work already
+    queued on the current stream, and ``wait()`` makes the current stream (not the host) wait for
+    it - compute queued in between overlaps it.  The one-shot IPC all-reduce (small messages) runs
+    synchronously on the current stream."""
+    st = ps or get_state()
+    if st.tp_size == 1:
+        return _DONE
+    car = st.custom_ar
+    if car is not None and car.fits(x):
+        car.all_reduce_(x)
+        return _DONE
+    return dist.all_reduce(x, op=dist.ReduceOp.SUM, group=st.tp_group, async_op=True)
+
+
 def tp_all_gather_last(x: torch.Tensor, ps=None) -> torch.Tensor:
     """Concatenate the last dim across the TP group, rank order (C-4: vocab-parallel logits)."""
     st = ps or get_state()

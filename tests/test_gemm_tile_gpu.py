@@ -24,7 +24,7 @@ def _close(a, b, atol, rtol=0.0, what=""):
     assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.4g}"
 
 
-ALGOS = [0, 1]  # refill schedule of the 4-wave kernel: 0 one barrier per k-tile, 1 two
+ALGOS = [0, 1, 2]  # 4-wave kernel: 0 one barrier per k-tile, 1 two; 2 the 8-wave ping-pong kernel (gemm_pp.hip)
 DENSE_ALGOS = ALGOS
 
 
