@@ -316,6 +316,9 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
     ok = [r for r in res if r.get("http_status", 200) == 200]
     lats = [r["http_latency_ms"] for r in ok]
     p50 = comm.all_reduce_max_scalar(statistics.median(lats) if lats else 0.0)
+    # the longest sequence served (prompt + answer tokens): the config's real seq_len
+    seq_max = int(comm.all_reduce_max_scalar(float(max((r.get("prompt_tokens", 0) + r.get("completion_tokens", 0)
+                                                        for r in ok), default=0))))
     if ps.rank != 0:
         return
     dp = world // a.tp
@@ -344,7 +347,8 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
-        "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": 8192, "parallelism": par,
+        "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": seq_max, "max_model_len": 8192,
+                   "parallelism": par,
                    "prompt_tokens_mean": round(total_p / max(1.0, total_ans), 1),
                    "max_new_tokens": a.max_new_tokens, "path": a.path, "mode": a.mode,
                    "client": a.client if a.path != "engine" else None,

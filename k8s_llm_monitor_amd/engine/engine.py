@@ -251,7 +251,7 @@ class LLMEngine:
         77.1 us per layer for an arbitrary order, profiles/r03/decode_row_order.jsonl).  Other
         bucket sizes: longest first (74.6 us).  Row order is free: each row's input token is
         located through ``src`` and every per-row result is keyed by the sequence.
-        ``K8SLLM_DECODE_ROW_ORDER=0`` keeps the scheduler's order."""
+        ``_ROW_ORDER = False`` keeps the scheduler's order."""
         if not _ROW_ORDER or len(seqs) < 2:
             return seqs
         srt = sorted(seqs, key=lambda q: -q.num_tokens)
@@ -595,7 +595,7 @@ class TpotModel:
         return d
 
 
-_ROW_ORDER = os.environ.get("K8SLLM_DECODE_ROW_ORDER", "1") != "0"
+_ROW_ORDER = True  # decode rows paired long / short per CU (tests may turn it off)
 _CUS_PER_XCD = 32  # MI355X: 256 CUs in 8 XCDs
 
 
@@ -1009,8 +1009,6 @@ class EngineService:
         pf = eng._pf_inflight
         # (on the CPU a launched step has already run: there is nothing to hide the wait behind)
         if pf is None or eng._inflight is not None or eng.cfg.admit_window_ms <= 0 or eng.device.type != "cuda":
-            return False
-        if os.environ.get("K8SLLM_PREFILL_GATHER", "1") == "0":
             return False
         cap = eng.cfg.max_prefill_tokens
         s = eng.sched

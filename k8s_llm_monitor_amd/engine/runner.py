@@ -14,7 +14,6 @@ sized from ``kv_cache_gb`` (MI355X: 288 GB HBM per GPU - an 8B model leaves >250
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -55,9 +54,6 @@ class ModelRunner:
         self.v_cache = torch.zeros(L, nb, hkv, D, BLOCK_SIZE, dtype=model.dtype, device=self.device)
         self.kv = [(self.k_cache[i], self.v_cache[i]) for i in range(L)]
         self.is_gpu = self.device.type == "cuda"
-        blas = os.environ.get("K8SLLM_BLAS", "")
-        if self.is_gpu and blas:  # library for the library GEMMs (prefill projections, LM head)
-            torch.backends.cuda.preferred_blas_library({"rocblas": "cublas", "hipblaslt": "cublaslt"}.get(blas, blas))
         B = cfg.max_num_seqs
         self.B = B
         dev = self.device

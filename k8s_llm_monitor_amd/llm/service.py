@@ -180,7 +180,8 @@ class OpenAIBackend:
         with urllib.request.urlopen(req, timeout=self.timeout_s) as r:
             d = json.loads(r.read())
         usage = d.get("usage") or {}
-        return GenResult(text=d["choices"][0]["message"]["content"], model=self.model, provider=self.provider,
+        return GenResult(text=d["choices"][0]["message"]["content"], model=d.get("model") or self.model,
+                         provider=self.provider,
                          prompt_tokens=usage.get("prompt_tokens"), completion_tokens=usage.get("completion_tokens"),
                          latency_ms=round((time.perf_counter() - t0) * 1e3, 3), ttft_ms=None,
                          finish_reason=d["choices"][0].get("finish_reason"))
@@ -251,8 +252,13 @@ class RecordStore:
 
 class AnalysisService:
     def __init__(self, backend, manager=None, client=None, analyzer=None, store: Optional[RecordStore] = None,
-                 max_context_events: int = 100, token_budget: int = 6144, max_tokens: Optional[int] = None):
+                 max_context_events: int = 100, token_budget: int = 6144, max_tokens: Optional[int] = None,
+                 routes: Optional[dict] = None):
+        """``routes``: analysis type -> backend that answers it (``llm.routes``: the root-cause
+        model on a 70B TP=8 deployment, anomaly detection on Mixtral - ``models.go:86-90``); the
+        prompt is built here, from this server's cluster context, and only generation is remote."""
         self.backend = backend
+        self.routes = dict(routes or {})
         self.manager = manager
         self.client = client
         self.analyzer = analyzer
@@ -295,9 +301,10 @@ class AnalysisService:
                  ignore_eos: bool = False) -> AnalysisResponse:
         from ..engine import EngineOverloaded, EngineUnavailable
 
+        backend = self.routes.get(kind, self.backend)
         try:
-            g = self.backend.generate(prompt, max_tokens=max_tokens or self.max_tokens, request_id=rid,
-                                      ignore_eos=ignore_eos)
+            g = backend.generate(prompt, max_tokens=max_tokens or self.max_tokens, request_id=rid,
+                                 ignore_eos=ignore_eos)
             result = {"type": kind, "answer": g.pop("text"), **g, **extra}
             resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
         except (EngineOverloaded, EngineUnavailable):

@@ -4,20 +4,22 @@ GPT-2 (the CPU plumbing config), with Megatron tensor parallelism.
 Nothing here exists in the reference ("no LLM, no GPU code"); the model replaces
 the remote ``callLLMAPI`` step of the doc sketch ``docs/metrics-usage-example.md:244-306``.
 
-Hot path per layer (GPU), all on the current HIP stream so a decode step captures into one
-hipGraph:
+Prefill layer (GPU, >= 1024 rows, TP=1; ``_prefill_fused_norm``), every GEMM on the hand-written
+256 x 256 MFMA tile kernel (ops/csrc/gemm_tile.hip) with its epilogue doing the elementwise work:
 
-  fused_add_rms_norm (HIP) -> QKV GEMM -> rope_and_cache (HIP: RoPE + paged KV write)
-  -> flash_prefill | paged_decode (HIP MFMA) -> o_proj GEMM (+ RCCL all-reduce at TP>1)
-  -> fused_add_rms_norm (HIP) -> gate_up GEMM + SwiGLU -> down GEMM (+ all-reduce)
+  qkv (+ RoPE of q / k, rows scaled by 1/rms) -> rope_and_cache (paged KV write) -> flash_prefill
+  -> o (+ residual add, next norm's operand and sums of squares) -> gate_up (+ SwiGLU, row scale)
+  -> down (+ residual add, ...)
 
-Prefill GEMMs go through ops.prefill_linear: the hand-written 4-wave MFMA kernel
-(ops/csrc/gemm_tile.hip, SwiGLU fused in its epilogue) or hipBLASLt per measured shape.
+TP > 1 prefill runs as two micro-batches whose row-parallel all-reduces overlap each other's
+compute (``_prefill_overlap``).
 
-Dense decode runs all four projections through the skinny MFMA GEMM over the same row-major
-weights prefill uses (ops/csrc/gemm_skinny.hip, LDS-DMA whole-line staging; ``_init_skinny``):
-split-K slabs reduced by the next kernel (paged_decode_fused, add_norm_partial) and SwiGLU in the
-gate_up epilogue.
+Decode layer (``_decode_layers_skinny``, 7 launches inside one hipGraph): qkv (split-K slabs) ->
+paged_decode_fused (slab reduce + RoPE + KV write + attention) -> o (slabs) -> add_norm_partial
+(residual add, deferred norm) -> gate_up + SwiGLU -> down (slabs) -> add_norm_partial.  Dense
+models whose weights fit a quarter of the device run the projections and the LM head on the
+shared-A decode GEMM over decode-only fragment-packed copies (ops/csrc/gemm_decode.hip); larger
+ones (70B at TP=1) on the row-major skinny kernel over the prefill tensors (gemm_skinny.hip).
 
 Weights are stored fused and pre-sharded: ``wqkv`` [(Hq+2Hkv)/tp * D, d] (column-parallel),
 ``wo`` [d, Hq/tp * D] (row-parallel), ``w13`` [2F/tp, d] (this rank's gate and up rows, stored
@@ -81,6 +83,12 @@ def _seed_for(name: str, seed: int) -> int:
 
 
 class CausalLM:
+    # path selection for tests and tools (class attributes, not environment switches):
+    # SKINNY_DECODE False = decode through the plain row-major path (the fp32-reference form of the
+    # real-shape tests); DECODE_GEMM "auto" | "dec" | "rm" = the decode projections' kernel (_want_dec)
+    SKINNY_DECODE = True
+    DECODE_GEMM = "auto"
+
     def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16, seed: int = 0,
                  pstate: Optional[ParallelState] = None, init_std: float = 0.02, init: str = "random"):
         """``init``: "random" (seeded per tensor name) or "empty" (uninitialised storage, for
@@ -115,7 +123,7 @@ class CausalLM:
         # experts from the device-side offsets (gemm_tile.hip 256 x 256 tiles, SwiGLU fused; zero
         # host syncs, capturable); "loop" = one hipBLASLt GEMM per expert after a host sync of the
         # expert offsets.  Mixtral-8x7B end to end: 8.14 vs 8.11 q/s (profiles/r02)
-        self._moe_grouped = os.environ.get("K8SLLM_MOE_PREFILL", "grouped") == "grouped"
+        self._moe_grouped = True
         # MoE decode at TP>1: "allreduce" = every rank runs its experts on every (replicated)
         # token, dense-masked, then one all-reduce; "a2a" = expert-parallel dispatch / combine with
         # static-capacity all-to-alls (_moe_a2a_decode, graph-capturable)
@@ -222,7 +230,7 @@ class CausalLM:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
         for L in self.layers:
             for k, v in L.items():
-                if k.endswith(("_p", "_d", "_pg")):  # decode-layout copies (_init_skinny) are not parameters
+                if k.endswith(("_p", "_d", "_pg", "_dg")):  # decode-layout copies (_init_skinny) are not parameters
                     continue
                 if isinstance(v, tuple):
                     n += sum(t.numel() for t in v)
@@ -506,7 +514,7 @@ class CausalLM:
         c = self.cfg
         if meta.dec_src is not None:
             if (self.tp == 1 and ids.is_cuda and c.arch != "gpt2" and self._use_skinny(meta, ids)
-                    and c.d_model % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0"):
+                    and c.d_model % 512 == 0):
                 # decode front end in one launch: ids -> embedding -> layer 0's deferred-norm operands
                 residual, xw, ss = ops.embed_norm_partial(ids, self.embed, self.layers[0]["attn_norm"],
                                                           meta.dec_src, meta.dec_prev)
@@ -667,16 +675,16 @@ class CausalLM:
         """Dense Llama decode at TP=1 on the GPU with <= 64 rows runs every projection through
         gemm_skinny over fragment-packed weights (see _init_skinny)."""
         return (self._skinny_ws is not None and not meta.is_prefill and h.shape[0] <= ops.SKINNY_MAX_M
-                and meta.logits_idx is None and os.environ.get("K8SLLM_SKINNY", "1") != "0")
+                and meta.logits_idx is None and self.SKINNY_DECODE)
 
     def _init_skinny(self) -> None:
-        """Decode-path weights.  ONE resident copy of every projection: gemm_skinny_rm_kernel
-        (ops/csrc/gemm_skinny.hip) streams the row-major tensors prefill's hipBLASLt GEMMs read -
-        whole 128-B lines by LDS-DMA - within 1-3 % of the old fragment-packed duplicate at every
-        decode batch (tools/bench_skinny_rm.py, profiles/r02/skinny_rm_vs_packed.jsonl), so
-        Llama-3-8B holds 16 GB of weights, not 32, and 70B fits one GPU on the skinny path.
-        A shape the row-major kernel does not take (N or K not a multiple of 64) keeps
-        fragment-packed copies instead.
+        """Decode-path weights.  The row-major tensors prefill reads serve decode through
+        gemm_skinny_rm_kernel (ops/csrc/gemm_skinny.hip: whole 128-B lines by LDS-DMA; a shape it
+        does not take keeps fragment-packed copies).  On top of that, ``_init_dec`` adds
+        decode-only fragment-packed copies for the shared-A decode GEMM (gemm_decode.hip) where
+        the weights fit a quarter of the device: Llama-3-8B holds 16 GB row-major + 16.5 GB packed
+        (the decode step is ~8 % faster on them: profiles/r04/README.md); 70B at TP=1 keeps the one
+        141 GB copy.
 
         w13 is stored gate/up-interleaved per 128 rows ([64 gate | 64 up], the SwiGLU epilogue's
         pairing): called on canonical [gate; up] tensors (after _build or load_checkpoint), it
@@ -694,7 +702,7 @@ class CausalLM:
         self.lm_head_d = None
         self._fuse_norm, self._seam, self._rc_o = False, None, False
         for L in self.layers:  # (re)built below from the current weights
-            for key in ("wqkv_d", "wo_d", "w13_d", "w2_d"):
+            for key in ("wqkv_d", "wo_d", "w13_d", "w2_d", "w13_dg", "w2_dg"):
                 L.pop(key, None)
         c = self.cfg
         ff = c.ffn_dim if c.is_moe else self.f_local  # experts are sharded by count (EP), not by F
@@ -711,9 +719,9 @@ class CausalLM:
         # 5-6 us per layer-op SLOWER than the slab GEMM + separate reduce kernel on the row-major
         # kernel too (profiles/r03/fused_epilogues_rowmajor.jsonl) and were removed.)
         # decode RoPE + KV write inside the attention kernel (paged_decode_fused), reading the qkv
-        # GEMM's split-K slabs directly: one launch per layer fewer (K8SLLM_ATTN_ROPE=0 disables)
-        self._attn_rope = self.D == 128 and os.environ.get("K8SLLM_ATTN_ROPE", "1") != "0"
-        if c.arch != "llama" or os.environ.get("K8SLLM_SKINNY", "1") == "0" or not self._w13_il:
+        # GEMM's split-K slabs directly: one launch per layer fewer
+        self._attn_rope = self.D == 128
+        if c.arch != "llama" or not self.SKINNY_DECODE or not self._w13_il:
             self._attn_rope = False
             return
         d, nq = c.d_model, (self.hq + 2 * self.hkv) * self.D
@@ -732,8 +740,7 @@ class CausalLM:
             else:
                 L["w13_p"] = keep(L["w13"])
                 L["w2_p"] = keep(L["w2"])
-        env = os.environ.get("K8SLLM_SKINNY_SPLITS")
-        split = int(env) if env else 0  # 0: the launcher picks per call (kernel and batch dependent)
+        split = ops.SKINNY_SPLITS_FORCE  # 0: the launcher picks per call (kernel and batch dependent)
         self._split_qkv = self._split_o = self._split_d = split
         self._init_dec()
 
@@ -765,7 +772,7 @@ class CausalLM:
         (the seam's workgroups must be resident together)."""
         c = self.cfg
         ok = (self.tp == 1 and not c.is_moe and bool(self.layers) and "w13_d" in self.layers[0]
-              and c.d_model % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0")
+              and c.d_model % 512 == 0)
         self._fuse_norm = bool(seam) and ok and not os.environ.get("K8SLLM_DEVICE")
         self._seam = ops.SeamState(self.device) if self._fuse_norm else None
         self._rc_o = bool(rc) and ok and "wo_d" in self.layers[0]
@@ -871,6 +878,12 @@ class CausalLM:
             else:
                 xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
         _, _, wd = ops.moe_router(xn, L["router"], c.top_k_experts, True)
+        if "w13_dg" in L and M <= ops.SKINNY_MAX_M:  # shared-A decode GEMM over the packed expert copies
+            E = L["w13_dg"].shape[0]
+            act = torch.empty((E, -(-M // 16), L["w13_dg"].shape[1] // 4, 64, 8), dtype=self.dtype, device=self.device)
+            ops.dec_gemm_grouped(ops.pack_activation(xn), L["w13_dg"], 2, M, out=act)
+            return ops.dec_gemm_grouped(act, L["w2_dg"], 0, M, workspace=ws,
+                                        row_w=wd[:, self.e_lo:self.e_hi].contiguous())
         act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 
@@ -890,21 +903,23 @@ class CausalLM:
             return ops.dec_gemm(x, wd, 0, rows, workspace=self._skinny_ws, rownorm=rownorm)
         return ops.skinny_slabs(x, L[key + "_p"], self._skinny_ws, split, rows=rows, rownorm=rownorm)
 
-    def _want_dec(self) -> bool:
-        """Decode-only fragment-packed weight copies for gemm_decode.hip (``K8SLLM_DECODE_GEMM`` =
-        auto | dec | rm).  auto: dense Llama whose weights take at most a quarter of the device
-        (Llama-3-8B: 16 GB of 288; 70B at TP=1 keeps the single row-major copy and gemm_skinny)."""
-        mode = os.environ.get("K8SLLM_DECODE_GEMM", "auto")
+    def _want_dec(self) -> tuple:
+        """Which decode-only fragment-packed copies gemm_decode.hip gets (``DECODE_GEMM`` = auto |
+        dec | rm): (attention + dense MLP + LM head, MoE experts).  auto: a dense Llama whose
+        weights take at most a quarter of the device (Llama-3-8B: 16 GB of 288; 70B at TP=1 keeps
+        the single row-major copy and gemm_skinny); a MoE model always gets its attention and LM
+        head copies (a few GB) and the expert copies while weights + copies stay within 70 % of
+        the device (Mixtral-8x7B at TP=1: 93 + 93 GB of 288, leaving the KV pool ~100 GB)."""
+        mode = self.DECODE_GEMM
         if mode in ("rm", "0", "off") or self.cfg.arch != "llama":
-            return False
-        if mode in ("dec", "1", "on"):
-            return True
-        if self.cfg.is_moe:
-            return False
-        if self.device.type != "cuda":
-            return True
+            return False, False
+        if mode in ("dec", "1", "on") or self.device.type != "cuda":
+            return True, True
         total = torch.cuda.get_device_properties(self.device).total_memory
-        return self.num_local_params() * 2 * 2 <= total // 2
+        both = self.num_local_params() * 2 * 2
+        if self.cfg.is_moe:
+            return True, both <= 0.7 * total
+        return both <= total // 2, False
 
     def _init_dec(self) -> None:
         """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
@@ -912,11 +927,12 @@ class CausalLM:
         ([N/16, K/32, 64, 8]), w13_d (gate/up interleaved per 16 rows as [8 gate | 8 up]), and the
         LM head.  Prefill keeps reading the row-major tensors."""
         self.lm_head_d = None
-        if not self._want_dec():
+        dense, experts = self._want_dec()
+        if not dense:
             return
         c = self.cfg
         for L in self.layers:
-            for key in ("wqkv", "wo", "w2"):
+            for key in ("wqkv", "wo") if c.is_moe else ("wqkv", "wo", "w2"):
                 N, K = L[key].shape
                 if ops.dec_available(N, K, 0):
                     L[key + "_d"] = ops.pack_skinny(L[key])
@@ -925,6 +941,13 @@ class CausalLM:
                 if ops.dec_available(w.shape[0], w.shape[1], 2):
                     L["w13_d"] = ops.pack_skinny(ops.interleave_gate_up8(w))
                 del w
+            elif experts:  # [E, ...] stacks for the grouped (grid.z = expert) decode launches
+                E, F2, d = L["w13"].shape
+                if (ops.dec_config(F2, d, 2, experts=E) is not None
+                        and ops.dec_config(d, F2 // 2, 0, experts=E) is not None):
+                    L["w13_dg"] = torch.stack([ops.pack_skinny(ops.interleave_gate_up8(
+                        ops.deinterleave_gate_up(w) if self._w13_il else w)) for w in L["w13"]])
+                    L["w2_dg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
         N, K = self.lm_head.shape
         if N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
             self.lm_head_d = ops.pack_skinny(self.lm_head)
@@ -957,7 +980,7 @@ class CausalLM:
         y = self._row_parallel_sum(ws, ns, residual.shape[0], residual)
         if y is not None:  # TP>1: all-reduced partial sums, complete norm, packed A
             return ops.pack_activation(ops.fused_add_rms_norm(y, residual, norm_w, eps)), None
-        if residual.shape[1] % 512 == 0 and os.environ.get("K8SLLM_DEFER_NORM", "1") != "0":
+        if residual.shape[1] % 512 == 0:
             xw, ss = ops.add_norm_partial(residual, ws, ns, norm_w)
             return xw, (ss, eps)
         out = ops.packed_empty(residual.shape[0], residual.shape[1], residual.dtype, residual.device)

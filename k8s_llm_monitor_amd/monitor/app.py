@@ -100,6 +100,16 @@ def make_llm_backend(cfg: Config, pstate=None, device: Optional[str] = None):
     return RuleBackend(), None, None
 
 
+def make_routes(cfg: Config) -> dict:
+    """``llm.routes``: analysis type -> an OpenAIBackend on that deployment's OpenAI-compatible
+    endpoint (this server's own ``/v1/chat/completions`` when the upstream runs this framework)."""
+    from ..llm.service import OpenAIBackend
+
+    return {kind: OpenAIBackend(cfg.llm.api_key or "none", url, cfg.llm.model, cfg.llm.max_tokens,
+                                cfg.llm.temperature, float(cfg.llm.timeout))
+            for kind, url in (cfg.llm.routes or {}).items() if url}
+
+
 def build_monitor(cfg: Config, backend=None, start_manager: bool = True, llm: bool = True, pstate=None,
                   device: Optional[str] = None) -> Monitor:
     from ..llm.service import AnalysisService, RecordStore, RuleBackend
@@ -143,7 +153,8 @@ def build_monitor(cfg: Config, backend=None, start_manager: bool = True, llm: bo
     m.analysis = AnalysisService(backend_llm, manager=m.manager, client=m.client, analyzer=None,
                                  store=RecordStore(cfg.storage.type, cfg.storage.path),
                                  max_context_events=cfg.analysis.max_context_events,
-                                 token_budget=cfg.analysis.prompt_token_budget, max_tokens=cfg.llm.max_tokens)
+                                 token_budget=cfg.analysis.prompt_token_budget, max_tokens=cfg.llm.max_tokens,
+                                 routes=make_routes(cfg))
     m.app = MonitorApp(m.client, m.manager, m.analysis, m.engine_service, llm_timeout_s=float(cfg.llm.timeout))
     if hasattr(backend_llm, "answer_budget_s"):  # the engine stops generations before the write timeout
         backend_llm.answer_budget_s = m.app.answer_budget_s()

@@ -60,6 +60,10 @@ class LLMConfig:
     chunked_prefill: bool = True  # longer prompts prefill in chunks of that budget
     prefix_caching: bool = True  # reuse the KV blocks of shared prompt prefixes
     weights: str = ""  # Hugging Face model dir (config.json + *.safetensors); "" = random init
+    # analysis type -> OpenAI-compatible base URL of the deployment that serves it (e.g.
+    # root_cause -> a Llama-3-70B TP=8 server's ".../v1"); unrouted types use this server's backend.
+    # YAML mapping, or "type=url,type=url" from the environment (LLM_ROUTES)
+    routes: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -164,6 +168,17 @@ def _coerce(value: Any, default: Any, key: str) -> Any:
             return [str(x) for x in value]
         if isinstance(default, str):
             return "" if value is None else str(value)
+        if isinstance(default, dict):
+            if value is None or value == "":
+                return {}
+            if isinstance(value, str):
+                pairs = [p.split("=", 1) for p in value.split(",") if p.strip()]
+                if any(len(p) != 2 for p in pairs):
+                    raise ValueError(value)
+                return {k.strip(): v.strip() for k, v in pairs}
+            if not isinstance(value, dict):
+                raise ValueError(value)
+            return {str(k): str(v) for k, v in value.items()}
     except (TypeError, ValueError) as e:
         raise ConfigError(f"failed to unmarshal config: key {key!r}: cannot decode {value!r}") from e
     return value

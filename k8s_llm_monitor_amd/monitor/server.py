@@ -27,6 +27,7 @@ import os
 import signal
 import threading
 import time
+import uuid
 from concurrent.futures import TimeoutError as FutTimeout
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Optional
@@ -147,6 +148,7 @@ class MonitorApp:
                 "/api/v1/analyze": self.analyze,
                 "/api/v1/analysis": self.analysis_list,
                 "/api/v1/metrics/engine": self.metrics_engine,
+                "/v1/chat/completions": self.chat_completions,
                 "/metrics": self.prometheus,
             }
             fn = exact.get(path)
@@ -397,6 +399,46 @@ class MonitorApp:
                                     error="answer not ready within the server write timeout", timestamp=utcnow())
             return json_reply(resp, 504)
         return json_reply(resp, 200 if resp.status == "success" else 500)
+
+    def chat_completions(self, method, body, q) -> Reply:
+        """OpenAI-compatible generation (the wire format of the reference's ``callLLMAPI``,
+        ``provider: openai``): another deployment's ``llm.routes`` entry, or a reference server
+        whose ``llm.base_url`` points here, gets its answer from this server's backend.  The
+        prompt is the caller's: system message(s) then the user / assistant turns.  Non-streaming."""
+        _only(method, "POST")
+        if self.analysis is None:
+            raise http_error(503, "Analysis engine not available")
+        d = _decode_object(body)
+        msgs = d.get("messages") if d is not None else None
+        if not isinstance(msgs, list) or not msgs or not all(
+                isinstance(m, dict) and isinstance(m.get("content"), str) for m in msgs):
+            raise http_error(400, "messages must be a non-empty list of {role, content}")
+        from ..llm import prompt as P
+
+        parts = [m["content"] for m in msgs]
+        if msgs[0].get("role") == "system" and msgs[0]["content"] == P.SYSTEM_PREAMBLE:
+            parts = parts[1:]  # every backend adds this server's own preamble
+        mt = d.get("max_tokens")
+        mt = int(mt) if isinstance(mt, (int, float)) and mt > 0 else None
+        temp = d.get("temperature")
+        temp = float(temp) if isinstance(temp, (int, float)) else None
+        backend = self.analysis.backend
+        try:
+            g = self._bounded(lambda: backend.generate("\n\n".join(parts), max_tokens=mt, temperature=temp))
+        except _BUSY as e:
+            return self._busy_reply(e)
+        except FutTimeout:
+            raise http_error(504, "answer not ready within the server write timeout")
+        except Exception as e:  # noqa: BLE001
+            raise http_error(500, f"{type(e).__name__}: {e}")
+        pt, ct = g.get("prompt_tokens"), g.get("completion_tokens")
+        usage = {"prompt_tokens": pt, "completion_tokens": ct,
+                 "total_tokens": (pt or 0) + (ct or 0) if pt is not None or ct is not None else None}
+        return json_reply({"id": "chatcmpl-" + uuid.uuid4().hex, "object": "chat.completion",
+                           "created": int(time.time()), "model": g.get("model") or d.get("model", ""),
+                           "choices": [{"index": 0, "message": {"role": "assistant", "content": g.get("text", "")},
+                                        "finish_reason": g.get("finish_reason") or "stop"}],
+                           "usage": usage})
 
     def analyze(self, method, body, q) -> Reply:
         _only(method, "POST")

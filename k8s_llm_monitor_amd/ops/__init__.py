@@ -7,7 +7,6 @@ from __future__ import annotations
 
 import importlib
 import math
-import os
 from typing import Optional
 
 import torch
@@ -107,14 +106,20 @@ def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(F2 // 128, 2, 64, K).permute(1, 0, 2, 3).reshape(F2, K)
 
 
+# test / tool overrides (module attributes, not environment switches): a forced split-K factor for
+# the slab-epilogue projections (real split-K slicing on tiny test shapes), and a forced waves-per-
+# workgroup count for gemm_skinny (0 = the launcher's choice)
+SKINNY_SPLITS_FORCE = 0
+SKINNY_WAVES_FORCE = 0
+
+
 def skinny_splits(N: int, K: int, target_wgs: int = 256) -> int:
     """Split-K factor for a slab-epilogue gemm_skinny: (N/64) x S workgroups ~ one per CU, each K
     slice at least 512 deep (tools/bench_skinny.py on MI355X, decode batch 1-64: S = 4 beats 2, 6
     and 8 for Llama-3-8B o/down - more slices add slab traffic to the reduce faster than they add
-    weight-streaming parallelism).  ``K8SLLM_SKINNY_SPLITS`` overrides."""
-    env = os.environ.get("K8SLLM_SKINNY_SPLITS")
-    if env:
-        return max(1, int(env))
+    weight-streaming parallelism).  ``SKINNY_SPLITS_FORCE`` (tests, tools) overrides."""
+    if SKINNY_SPLITS_FORCE:
+        return max(1, SKINNY_SPLITS_FORCE)
     tiles = max(1, N // 64)
     return max(1, min(K // 512, round(target_wgs / tiles)))
 
@@ -193,8 +198,8 @@ def _rn_scale(rownorm, M: int, K: int) -> Optional[torch.Tensor]:
 
 def skinny_waves() -> int:
     """Waves per gemm_skinny workgroup: 0 = the launcher's choice (8 for split-K slabs, 4 for the
-    single-slice epilogues); ``K8SLLM_SKINNY_WAVES`` = 4 or 8 forces one."""
-    return int(os.environ.get("K8SLLM_SKINNY_WAVES", "0"))
+    single-slice epilogues); ``SKINNY_WAVES_FORCE`` = 4 or 8 forces one (tools)."""
+    return SKINNY_WAVES_FORCE
 
 
 def _rn_args(rownorm) -> tuple:
@@ -346,38 +351,30 @@ DEC_TABLE: dict = {
 }
 
 
-def _dec_table_env() -> None:
-    """``K8SLLM_DEC_TABLE`` = "N,K,EPI=S,NTW,WAVES,DEPTH;..." overrides table entries (A/B runs)."""
-    for item in filter(None, os.environ.get("K8SLLM_DEC_TABLE", "").split(";")):
-        shape, cfg = item.split("=")
-        DEC_TABLE[tuple(int(v) for v in shape.split(","))] = tuple(int(v) for v in cfg.split(","))
 
-
-_dec_table_env()
-
-
-def dec_config(N: int, K: int, epi: int) -> Optional[tuple]:
+def dec_config(N: int, K: int, epi: int, experts: int = 1) -> Optional[tuple]:
     """Launch configuration of gemm_dec for a weight [N, K]: (splits, ntw, waves, depth) or None
-    when no configuration tiles the shape (the caller keeps gemm_skinny).  ``K8SLLM_DEC_CFG`` =
-    "S,NTW,WAVES,DEPTH" forces one (tools)."""
-    env = os.environ.get("K8SLLM_DEC_CFG")
-    if env:
-        return tuple(int(v) for v in env.split(","))
-    hit = DEC_TABLE.get((N, K, epi))
+    when no configuration tiles the shape (the caller keeps gemm_skinny).  The candidates are the
+    (ntw, waves, depth) forms gemm_decode.hip instantiates: every Llama-3-8B / 70B / Mixtral
+    projection and LM head at TP 1..8 picks one of them (tools/bench_decode_gemm.py passes ``cfg``
+    to dec_gemm to time others).  ``experts`` > 1: a grouped launch (grid.z = expert), whose
+    workgroup count is per expert times experts (Mixtral down: 32 column groups x 8 experts, no
+    split - the expert slabs are the split)."""
+    hit = DEC_TABLE.get((N, K, epi)) if experts == 1 else None
     if hit is not None:
         return hit
     ntiles, ksteps = N // 16, K // 32
-    cands = ([(1, 1, 7, 8), (1, 1, 7, 16), (1, 1, 8, 16), (1, 2, 4, 8)] if epi == 2 else
-             [(1, 4, 8, 4), (1, 3, 8, 8), (1, 2, 8, 8), (1, 4, 4, 8)] if epi == 1 else
-             [(s, ntw, w, d) for s in (1, 2, 4, 8, 16) for (ntw, w, d) in
-              ((1, 8, 8), (1, 4, 16), (1, 4, 8), (2, 4, 8), (2, 8, 8), (3, 4, 8), (3, 8, 8), (4, 4, 8),
-                               (4, 4, 4))])
+    cands = ([(1, 1, 7, 8), (1, 1, 7, 16), (1, 1, 8, 16)] if epi == 2 else
+             [(1, 4, 8, 4), (1, 3, 8, 8), (1, 2, 8, 8), (1, 1, 8, 8)] if epi == 1 else
+             [(s, ntw, w, d) for s in (1, 2, 4, 8, 16) for (ntw, w, d) in ((1, 8, 8), (1, 4, 16), (1, 4, 8))])
     best = None
     for s, ntw, w, d in cands:
+        if experts > 1 and s > 1:  # grouped: the per-expert slabs are the split (workspace E x M x N)
+            continue
         it = max(d, 8)
         if (epi == 0 and ntiles % (ntw * w)) or K % s or (ksteps // s) % it or ksteps % s:
             continue
-        wgs = -(-ntiles // (ntw * w)) * s
+        wgs = -(-ntiles // (ntw * w)) * s * experts
         # ~256 workgroups; for split-K slabs 8-wave workgroups of one n-tile per wave were the
         # fastest within 64 workgroups of that (the sweep), then fewer K splits (slab traffic)
         far = abs(wgs - 256) if wgs <= 512 else 10_000 + wgs
@@ -431,6 +428,40 @@ def dec_gemm(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: 
     r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn, None, 0, None, None, None, None)
     if r < 0:
         raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
+    return r
+
+
+def dec_gemm_grouped(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None, row_w: Optional[torch.Tensor] = None,
+                     cfg: Optional[tuple] = None) -> int:
+    """gemm_dec over every local expert of a MoE layer in ONE launch (grid.z = expert): ``wp``
+    [E, N/16, K/32, 64, 8] (packed per expert, gate/up interleave_gate_up8 for epi 2); ``a`` packed
+    [ceil(M/16), K/32, 64, 8] shared by the experts (gate_up) or [E, ...] per expert (down).
+    epi 2: ``out`` [E, ceil(M/16), F/32, 64, 8] packed SwiGLU; epi 0: fp32 slabs [E * S, M, N] in
+    ``workspace`` scaled by ``row_w`` [M, E] (routing weights, 0 where a row skipped the expert),
+    returns E * S - the residual-add kernel's slab sum is the expert combine."""
+    E = wp.shape[0]
+    N, K = wp.shape[1] * 16, wp.shape[2] * 32
+    M = rows
+    if cfg is None:
+        cfg = dec_config(N, K, epi)
+    if cfg is None:
+        raise ValueError(f"gemm_dec_grouped: no configuration for N={N} K={K} epi={epi}")
+    S, ntw, waves, depth = cfg
+    if not _gpu(a):
+        for e in range(E):
+            ae = a[e] if a.dim() == 5 else a
+            if epi == 2:
+                dec_gemm(ae, wp[e], 2, M, out=out[e], cfg=cfg)
+            else:
+                ws = workspace[e * S * M * N: (e + 1) * S * M * N]
+                dec_gemm(ae, wp[e], 0, M, workspace=ws, cfg=cfg)
+                if row_w is not None:
+                    ws.view(S, M, N).mul_(row_w[:M, e].float().view(1, M, 1))
+        return E * S if epi == 0 else 1
+    r = native().gemm_dec_grouped(a, wp, workspace, out, S, epi, ntw, waves, depth, M, row_w)
+    if r < 0:
+        raise RuntimeError(f"gemm_dec_grouped: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
     return r
 
 
@@ -714,9 +745,6 @@ def decode_splits(batch: int, Hkv: int, n_cu: int = 256) -> int:
     Measured on MI355X (tools/bench_decode.py, ctx 1.8k-6k): batch 64 x 8 kv heads is best
     unsplit (83 us, 5.7 TB/s - a merge launch and extra partial traffic only cost), batch 8 at 4
     splits, batch 1 at 16-32 splits."""
-    env = os.environ.get("K8SLLM_DECODE_SPLITS")
-    if env:
-        return max(1, min(MAX_SPLITS, int(env)))
     return max(1, min(32, round(n_cu / max(1, batch * Hkv))))
 
 
@@ -774,13 +802,13 @@ def paged_decode_fused(slabs: torch.Tensor, nslabs: int, positions: torch.Tensor
     return out
 
 
-def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128,
-                    ctx_starts: Optional[list[int]] = None) -> tuple[list[int], list[int]]:
+def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128, ctx_starts: Optional[list[int]] = None,
+                    order: str = "seq") -> tuple[list[int], list[int]]:
     """Q-block schedule for flash_prefill: (seq index, first q row) per 128-row block.  A block's
     work is its causal key span: the sequence's cached prefix (``ctx_starts``, chunked prefill)
     plus its first row.
 
-    ``K8SLLM_QB_ORDER=seq`` (default, sequence-major): the longest sequence first, each sequence's
+    ``order="seq"`` (the engine's, sequence-major): the longest sequence first, each sequence's
     blocks heaviest first.  The workgroups resident on one XCD at a time (one kv head's) then cover
     one or two sequences, whose K/V stay in that XCD's 4 MiB L2, and the grid still ends on light
     blocks: 10 x 1609 tokens 276.7 vs 295.1 us, 64 x 1609 1788 vs 1934 us
@@ -792,7 +820,7 @@ def prefill_qblocks(cu_seqlens_cpu: list[int], block: int = 128,
         c = ctx_starts[i] if ctx_starts is not None else 0
         for s in range(0, n, block):
             items.append((c + s, s, i, c + n))
-    if os.environ.get("K8SLLM_QB_ORDER", "seq") == "seq":
+    if order == "seq":
         items.sort(key=lambda t: (-t[3], t[2], -t[0]))
     else:
         items.sort(key=lambda t: -t[0])
@@ -1044,10 +1072,11 @@ def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_
 # the all-tile routing measured +1.4 % (three interleaved pairs, profiles/r04/bench_pg2_*.json:
 # 25.06 vs 24.71 q/s), with qkv's RoPE fused into the tile epilogue.  "auto" = tile for the fused
 # epilogues only (gate_up + SwiGLU, qkv + RoPE), hipBLASLt for o / down; "blas" = hipBLASLt for all.
-PREFILL_GEMM = os.environ.get("K8SLLM_PREFILL_GEMM", "tile")
-QKV_ROPE_TILE = os.environ.get("K8SLLM_QKV_ROPE_TILE", "1") != "0"  # qkv + fused RoPE on the tile kernel
+# These are module constants (tools and tests set them for A/B runs), not environment switches.
+PREFILL_GEMM = "tile"
+QKV_ROPE_TILE = True  # qkv + fused RoPE on the tile kernel
 # residual-add RMSNorm folded into the o / down epilogues and the qkv / gate_up row scale
-FUSED_NORM = os.environ.get("K8SLLM_FUSED_NORM", "1") != "0"
+FUSED_NORM = True
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
 # 1: the 4-wave kernel's two-barrier schedule; 2: the 8-wave ping-pong kernel (csrc/gemm_pp.hip,
 # bit-identical, 5-6 % slower at the Llama-3-8B shapes: profiles/r05/README.md)

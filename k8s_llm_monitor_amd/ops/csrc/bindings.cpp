@@ -55,7 +55,7 @@ int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
 int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K, int splits,
                     int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc, int rn_d, float rn_eps,
                     const float* np_slabs, int np_S, void* np_resid, const void* np_w, void* np_seam, int* np_err,
-                    hipStream_t s);
+                    int experts, long a_es, long w_es, long y_es, const float* rw, int rw_ld, hipStream_t s);
 void k8sllm_gemm_pp_sched(int sch);
 int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, const void* nw, void* xw, float* ss, int M, int N,
                        int K, hipStream_t s);
@@ -640,11 +640,65 @@ int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor>
   }
   const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, ldy, M, N, K, (int)splits, (int)epi, (int)ntw,
                                  (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, nsp, (int)np_nslabs, nrp, nwp,
-                                 nsm, nerr, cur());
+                                 nsm, nerr, 1, 0, 0, 0, nullptr, 0, cur());
   if (rc == -6) return -2;
   if (rc < 0) return -1;
   check(rc, "gemm_dec");
   return epi == 0 ? splits : 1;
+}
+
+// Grouped decode GEMM over the local experts of a MoE layer (grid.z = expert): wp [E, N/16, K/32,
+// 64, 8]; a packed [ceil(M/16), K/32, 64, 8] shared by every expert (gate_up) or [E, ceil(M/16),
+// K/32, 64, 8] per expert (down).  epi 2: y [E, ceil(M/16), N/64, 64, 8] packed SwiGLU per expert;
+// epi 0: fp32 slabs [E * splits, M, N] scaled by row_w [M, E] (the routing weights of these
+// experts).  Returns the slab count (epi 0) or 1; -1 for a shape / configuration it does not take.
+int64_t gemm_dec_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial,
+                         c10::optional<torch::Tensor> y, int64_t splits, int64_t epi, int64_t ntw, int64_t waves,
+                         int64_t depth, int64_t rows, c10::optional<torch::Tensor> row_w) {
+  dev_bf16(a, "a"); dev_bf16(wp, "wp");
+  TORCH_CHECK(wp.dim() == 5 && wp.is_contiguous() && wp.size(3) == 64 && wp.size(4) == 8,
+              "gemm_dec_grouped: wp must be [E, N/16, K/32, 64, 8]");
+  const int E = (int)wp.size(0), N = (int)wp.size(1) * 16, K = (int)wp.size(2) * 32, M = (int)rows;
+  const int MT = (M + 15) / 16;
+  TORCH_CHECK(M > 0 && M <= 64 && E >= 1, "gemm_dec_grouped: 1..64 rows, >= 1 expert");
+  const bool per_e = a.dim() == 5;
+  TORCH_CHECK(a.is_contiguous() && (per_e ? (a.size(0) == E && a.size(1) >= MT && a.size(2) * 32 == K &&
+                                             a.size(3) == 64 && a.size(4) == 8)
+                                          : (a.dim() == 4 && a.size(0) >= MT && a.size(1) * 32 == K &&
+                                             a.size(2) == 64 && a.size(3) == 8)),
+              "gemm_dec_grouped: a packed [ceil(M/16), K/32, 64, 8] or [E, ...]");
+  const long a_es = per_e ? a.stride(0) : 0, w_es = wp.stride(0);
+  float* pp = nullptr;
+  void* yp = nullptr;
+  long y_es = 0;
+  const float* rw = nullptr;
+  int rw_ld = 0;
+  if (epi == 0) {
+    TORCH_CHECK(partial.has_value() && partial->is_cuda() && partial->scalar_type() == torch::kFloat32 &&
+                    partial->is_contiguous() && partial->numel() >= (long)E * splits * M * N,
+                "gemm_dec_grouped: partial must hold E x splits x M x N fp32");
+    pp = partial->data_ptr<float>();
+    if (row_w.has_value()) {
+      TORCH_CHECK(row_w->is_cuda() && row_w->scalar_type() == torch::kFloat32 && row_w->dim() == 2 &&
+                      row_w->size(0) >= M && row_w->size(1) == E && row_w->stride(1) == 1,
+                  "gemm_dec_grouped: row_w [M, E] fp32");
+      rw = row_w->data_ptr<float>();
+      rw_ld = (int)row_w->stride(0);
+    }
+  } else {
+    TORCH_CHECK(epi == 2 && splits == 1 && y.has_value(), "gemm_dec_grouped: SwiGLU output needs splits 1 and y");
+    dev_bf16(*y, "y");
+    TORCH_CHECK(y->dim() == 5 && y->is_contiguous() && y->size(0) == E && y->size(1) == MT && y->size(2) * 64 == N &&
+                    y->size(3) == 64 && y->size(4) == 8, "gemm_dec_grouped: y [E, ceil(M/16), N/64, 64, 8]");
+    yp = y->data_ptr();
+    y_es = y->stride(0);
+  }
+  const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, 0, M, N, K, (int)splits, (int)epi, (int)ntw,
+                                 (int)waves, (int)depth, nullptr, 0, K, 0.f, nullptr, 0, nullptr, nullptr, nullptr,
+                                 nullptr, E, a_es, w_es, y_es, rw, rw_ld, cur());
+  if (rc < 0) return -1;
+  check(rc, "gemm_dec_grouped");
+  return epi == 0 ? (int64_t)E * splits : 1;
 }
 
 // Row-complete decode GEMM + residual add + deferred-norm operands (gemm_decode.hip
@@ -925,6 +979,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
   m.def("gemm_dec", &gemm_dec);
+  m.def("gemm_dec_grouped", &gemm_dec_grouped);
   m.def("gemm_dec_rc", &gemm_dec_rc);
   m.def("gemm_pp_sched", [](int64_t sch) { k8sllm_gemm_pp_sched((int)sch); });
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);

@@ -55,6 +55,16 @@ struct DecNorm {
   int* err;                    // set to 1 when a seam spin gives up (a non-resident workgroup)
 };
 
+// Grouped launches (MoE experts, grid.z = local expert e): A, W and the SWIGLU8 output advance by
+// a per-expert stride; SLAB partials land in slab e * S + split, scaled by the routing weight
+// rw[row * rw_ld + e] (0 where the row did not pick the expert), so the residual-add kernel's slab
+// sum IS the expert combine.  Dense launches: all strides 0, rw null, grid.z 1.
+struct DecGroup {
+  long a_es, w_es, y_es;  // elements between experts' A / W / SWIGLU8 outputs
+  const float* rw;        // [M][rw_ld] routing weights (SLAB epilogue) or null
+  int rw_ld;
+};
+
 constexpr int kSeamStride = 16;  // u64 words between shard counters (128 B)
 constexpr unsigned kSeamSpins = 1u << 22;
 
@@ -81,8 +91,12 @@ template <int MT, int NTW, int WAVES, int EPI, int DEPTH, bool NP, bool RNW = fa
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
-    float rn_inv_d, float rn_eps, DecNorm np) {
+    float rn_inv_d, float rn_eps, DecNorm np, DecGroup grp) {
   using G = DecGeom<MT, WAVES>;
+  const int ex = blockIdx.z;  // expert of a grouped launch (0 otherwise)
+  A += ex * grp.a_es;
+  W += ex * grp.w_es;
+  if constexpr (EPI == DEC_SWIGLU8) Y += ex * grp.y_es;
   constexpr int ITER = DEPTH > kDecCH ? DEPTH : kDecCH;  // k-steps per unrolled main-loop iteration
   __shared__ __attribute__((aligned(16))) char sA[2 * G::SLOT];
   __shared__ float s_inv[MT * 16];
@@ -367,7 +381,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
             if constexpr (EPI == DEC_BF16)
               Y[(long)row * ldy + col] = f2bf(v);
             else
-              partial[((long)blockIdx.y * M + row) * N + col] = v;
+              partial[((long)(ex * gridDim.y + blockIdx.y) * M + row) * N + col] =
+                  grp.rw != nullptr ? v * grp.rw[(long)row * grp.rw_ld + ex] : v;
           }
         }
       }
@@ -482,8 +497,10 @@ using namespace k8sllm;
 extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                                int splits, int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc,
                                int rn_d, float rn_eps, const float* np_slabs, int np_S, void* np_resid,
-                               const void* np_w, void* np_seam, int* np_err, hipStream_t s) {
+                               const void* np_w, void* np_seam, int* np_err, int experts, long a_es, long w_es,
+                               long y_es, const float* rw, int rw_ld, hipStream_t s) {
   if (M <= 0) return 0;
+  if (experts < 1 || (experts > 1 && np_slabs != nullptr) || (rw != nullptr && epi != DEC_SLAB)) return -1;
   if (M > 64 || N % 16 || K % 32 || splits < 1 || K % splits) return -1;
   const int ntiles = N / 16, nwg_tiles = ntw * waves;
   const int kchunk = K / splits;
@@ -492,7 +509,7 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
   if (epi != DEC_SLAB && splits != 1) return -4;
   const float inv_d = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
   const int MT = (M + 15) / 16;
-  const dim3 grid((ntiles + nwg_tiles - 1) / nwg_tiles, splits), blk(64 * waves);
+  const dim3 grid((ntiles + nwg_tiles - 1) / nwg_tiles, splits, experts), blk(64 * waves);
   const bool np = np_slabs != nullptr;
   if (np) {
     static int cus = 0;
@@ -507,12 +524,13 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
       return -6;
   }
   const DecNorm dn{np_slabs, np_S, (bf16_t*)np_resid, (const bf16_t*)np_w, (unsigned long long*)np_seam, np_err};
+  const DecGroup dg{a_es, w_es, y_es, rw, rw_ld};
   int rc = -5;
   const bool rnw = rn_ss != nullptr && rn_nc > 4 * kRnMax;  // the wide deferred-norm form (gemm_dec_rc sums)
   if (rnw && (rn_nc % 16 || rn_nc > 16 * kRnWide || np)) return -1;
 #define K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, RW)                                                                 \
   hipLaunchKernelGGL((gemm_dec_kernel<MTV, NTWV, WV, EPV, DV, NPV, RW>), grid, blk, 0, s, (const bf16_t*)A,          \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kchunk, rn_ss, rn_nc, inv_d, rn_eps, dn); \
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kchunk, rn_ss, rn_nc, inv_d, rn_eps, dn, dg); \
   rc = 0
 #define K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, NPV) K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, false)
 #define K8S_DEC(MTV, NTWV, WV, EPV, DV) K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, false)
@@ -553,31 +571,22 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     if (rc) return rc;
     return (int)hipGetLastError();
   }
-  // configurations (ntw, waves, depth) per epilogue: the ones the launcher's table picks plus
-  // the sweep neighbours of tools/bench_decode_gemm.py
+  // configurations (ntw, waves, depth) per epilogue: exactly the ones ops.dec_config can pick - every
+  // Llama-3-8B / 70B / Mixtral projection and LM head at TP 1..8 lands on one of them
   if (epi == DEC_SLAB) {
-    if (ntw == 1 && waves == 4 && depth == 16) { K8S_DEC_M(1, 4, DEC_SLAB, 16) }
-    else if (ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_M(1, 8, DEC_SLAB, 8) }
-    else if (ntw == 2 && waves == 4 && depth == 8) { K8S_DEC_M(2, 4, DEC_SLAB, 8) }
-    else if (ntw == 2 && waves == 8 && depth == 8) { K8S_DEC_M(2, 8, DEC_SLAB, 8) }
-    else if (ntw == 3 && waves == 4 && depth == 8) { K8S_DEC_M(3, 4, DEC_SLAB, 8) }
-    else if (ntw == 4 && waves == 4 && depth == 4) { K8S_DEC_M(4, 4, DEC_SLAB, 4) }
-    else if (ntw == 4 && waves == 4 && depth == 8) { K8S_DEC_M(4, 4, DEC_SLAB, 8) }
-    else if (ntw == 3 && waves == 8 && depth == 8) { K8S_DEC_M(3, 8, DEC_SLAB, 8) }
-    else if (ntw == 1 && waves == 4 && depth == 8) { K8S_DEC_M(1, 4, DEC_SLAB, 8) }
-    // qkv at 4 splits: 384 n-tiles / 6 per workgroup = 64 column groups x 4 = 256 workgroups
-    else if (ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_M(1, 6, DEC_SLAB, 8) }
-    else if (ntw == 2 && waves == 3 && depth == 8) { K8S_DEC_M(2, 3, DEC_SLAB, 8) }
+    if (ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_M(1, 8, DEC_SLAB, 8) }         // o, down; TP 2-8 shapes
+    else if (ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_M(1, 6, DEC_SLAB, 8) }    // qkv: 64 groups x 4 splits
+    else if (ntw == 1 && waves == 4 && depth == 8) { K8S_DEC_M(1, 4, DEC_SLAB, 8) }    // narrow TP shards
+    else if (ntw == 1 && waves == 4 && depth == 16) { K8S_DEC_M(1, 4, DEC_SLAB, 16) }  // 70B TP=8 qkv
   } else if (epi == DEC_SWIGLU8) {
-    if (ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 16) }
-    else if (ntw == 1 && waves == 8 && depth == 16) { K8S_DEC_M(1, 8, DEC_SWIGLU8, 16) }
-    else if (ntw == 2 && waves == 4 && depth == 8) { K8S_DEC_M(2, 4, DEC_SWIGLU8, 8) }
-    else if (ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 8) }
+    if (ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 8) }      // gate_up
+    else if (ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_M(1, 7, DEC_SWIGLU8, 16) }
+    else if (ntw == 1 && waves == 8 && depth == 16) { K8S_DEC_M(1, 8, DEC_SWIGLU8, 16) }  // 70B TP=1 gate_up
   } else if (epi == DEC_BF16) {
-    if (ntw == 4 && waves == 8 && depth == 4) { K8S_DEC_M(4, 8, DEC_BF16, 4) }
-    else if (ntw == 2 && waves == 8 && depth == 8) { K8S_DEC_M(2, 8, DEC_BF16, 8) }
-    else if (ntw == 4 && waves == 4 && depth == 8) { K8S_DEC_M(4, 4, DEC_BF16, 8) }
+    if (ntw == 4 && waves == 8 && depth == 4) { K8S_DEC_M(4, 8, DEC_BF16, 4) }         // LM head, TP=1
+    else if (ntw == 2 && waves == 8 && depth == 8) { K8S_DEC_M(2, 8, DEC_BF16, 8) }    // vocab shards, TP 2-8
     else if (ntw == 3 && waves == 8 && depth == 8) { K8S_DEC_M(3, 8, DEC_BF16, 8) }
+    else if (ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_M(1, 8, DEC_BF16, 8) }    // Mixtral's 32000-row head
   }
 #undef K8S_DEC_M
 #undef K8S_DEC

@@ -804,11 +804,8 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
                                 SkinnyRmGeom<3, 4, 0, 4>::LDS, SkinnyRmGeom<4, 4, 0, 4>::LDS};
     // split-K slab projections whose 64-column grid leaves CUs idle (qkv: 96 tiles x 2 slices =
     // 192 workgroups) use 48-column tiles when that fills the chip (128 x 2 = 256).
-    // K8SLLM_SKINNY_TILE_COLS = 48 / 64 forces one.
-    static const int cols_env = getenv("K8SLLM_SKINNY_TILE_COLS") ? atoi(getenv("K8SLLM_SKINNY_TILE_COLS")) : 0;
     const bool nt3_ok = epi == EPI_SLAB && N % 48 == 0;
-    const bool nt3 = nt3_ok && (cols_env == 48 || (cols_env != 64 && (long)(N / 64) * slabs_rm * experts < 224 &&
-                                                 (long)(N / 48) * slabs_rm * experts <= 256));
+    const bool nt3 = nt3_ok && (long)(N / 64) * slabs_rm * experts < 224 && (long)(N / 48) * slabs_rm * experts <= 256;
     if (nt3) {
       dim3 grid3(N / 48, slabs_rm, experts), blk3(256);
 #define K8S_RM3(MTV)                                                                                              \

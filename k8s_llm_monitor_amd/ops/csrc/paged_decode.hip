@@ -398,10 +398,8 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
 
 // Tokens per wave per chunk: the double-buffered 32-token form once the grid fills the chip
 // (>= 384 workgroups, e.g. batch 64 x 8 kv heads), else the single-buffered 64-token form (small
-// batches, split grids: higher residency).  K8SLLM_DECODE_TW = 32 / 64 forces one.
+// batches, split grids: higher residency).
 static int decode_tw(int S, int Hkv, int B) {
-  static const int forced = getenv("K8SLLM_DECODE_TW") ? atoi(getenv("K8SLLM_DECODE_TW")) : 0;
-  if (forced == 32 || forced == 64) return forced;
   return (long)S * Hkv * B >= 384 ? 32 : 64;
 }
 

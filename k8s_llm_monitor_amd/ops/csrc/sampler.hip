@@ -227,8 +227,6 @@ __global__ __launch_bounds__(64) void sample_final_kernel(int* __restrict__ out,
 using namespace k8sllm;
 
 extern "C" int k8sllm_sample_parts(long B, int V) {
-  const char* e = getenv("K8SLLM_SAMPLE_PARTS");  // A/B runs (tools/bench_sampler.py)
-  if (e && atoi(e) > 0) return atoi(e) < V ? atoi(e) : 1;
   // ~2 workgroups per CU in total, at least 8K vocabulary entries per part
   long p = (512 + B - 1) / B;
   p = p < 1 ? 1 : p;

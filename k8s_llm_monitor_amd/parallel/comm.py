@@ -44,19 +44,53 @@ class _Done:
 _DONE = _Done()
 
 
+class _StreamWork:
+    """An all-reduce queued on the comm stream: ``wait()`` makes the current stream wait for it."""
+
+    __slots__ = ("ev",)
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+_COMM_STREAMS: dict = {}
+
+
+def comm_stream(device: torch.device):
+    """The process's high-priority stream for IPC collectives issued asynchronously (one per
+    device, so those collectives keep program order among themselves on every rank)."""
+    s = _COMM_STREAMS.get(device)
+    if s is None:
+        s = _COMM_STREAMS[device] = torch.cuda.Stream(device=device, priority=-1)
+    return s
+
+
 def tp_all_reduce_async(x: torch.Tensor, ps=None):
     """In-place sum over the TP group, returned as a handle whose ``wait()`` must precede any use
-    of ``x``.  RCCL: the collective runs on the process group's own stream after the work already
-    queued on the current stream, and ``wait()`` makes the current stream (not the host) wait for
-    it - compute queued in between overlaps it.  The one-shot IPC all-reduce (small messages) runs
-    synchronously on the current stream."""
+    of ``x``; compute queued on the current stream between the call and ``wait()`` overlaps the
+    collective, and ``wait()`` blocks the current stream, never the host.
+
+    RCCL runs the collective on the process group's own stream.  A message that fits the IPC
+    staging buffer goes to the one-launch custom all-reduce on ``comm_stream``: the comm stream
+    first waits for the work already queued on the current stream (the producer of ``x``), so
+    every rank issues its IPC collectives in program order - the same total order the synchronous
+    calls have - and the caller must wait() every handle before its next synchronous collective."""
     st = ps or get_state()
     if st.tp_size == 1:
         return _DONE
     car = st.custom_ar
     if car is not None and car.fits(x):
-        car.all_reduce_(x)
-        return _DONE
+        cs = comm_stream(x.device)
+        cs.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(cs):
+            car.all_reduce_(x)
+        x.record_stream(cs)  # the caching allocator must not hand x out again before the reduce ran
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return _StreamWork(ev)
     return dist.all_reduce(x, op=dist.ReduceOp.SUM, group=st.tp_group, async_op=True)
 
 

@@ -153,7 +153,7 @@ def maybe_create(ps) -> Optional[CustomAllReduce]:
     if not (enabled() and ps.tp_size > 1 and ps.tp_size <= 8 and ps.device.type == "cuda"):
         return None
     car = CustomAllReduce(ps.tp_rank, ps.tp_size, cpu_group=ps.cpu_group)
-    if os.environ.get("K8SLLM_CUSTOM_AR_SELFTEST", "1") != "0" and not self_test(car, ps):
+    if not self_test(car, ps):
         import logging
 
         logging.getLogger("parallel").warning("custom all-reduce failed its startup self-test: RCCL carries "

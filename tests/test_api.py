@@ -196,3 +196,43 @@ def test_web_console_pages(mon):
         if path in ("/api/v1/query", "/api/v1/metrics/engine"):  # POST-only / optional (no engine here)
             continue
         assert a.handle("GET", path).code == 200, path
+
+
+def test_llm_routes_send_analysis_types_to_their_deployment(monkeypatch):
+    """``llm.routes`` (models.go:86-90: root_cause on the 70B deployment, anomaly_detection on
+    Mixtral): a routed type is generated by the upstream's OpenAI-compatible /v1/chat/completions
+    (here a second server of this framework), an unrouted type by the local backend; the prompt is
+    built from the local cluster context either way."""
+    up_cfg = from_dict({"llm": {"provider": "none"}})
+    up = build_monitor(up_cfg, backend=FakeCluster.build(seed=5), start_manager=False, llm=True)
+    srv = make_server(up.app, "127.0.0.1", 0)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/v1"
+        monkeypatch.setenv("LLM_ROUTES", f"root_cause={url}")
+        cfg = from_dict({"llm": {"provider": "none", "model": "llama-3-70b"}})
+        assert cfg.llm.routes == {"root_cause": url}
+        m = build_monitor(cfg, backend=FakeCluster.build(seed=2), start_manager=False, llm=True)
+        m.manager.collect()
+        before = up.app.requests
+        d = J(m.app.handle("POST", "/api/v1/analyze", b'{"type":"root_cause"}'))
+        assert d["status"] == "success" and d["result"]["type"] == "root_cause"
+        assert d["result"]["provider"] == "openai" and d["result"]["model"] == "rule-engine"
+        assert up.app.requests == before + 1
+        d = J(m.app.handle("POST", "/api/v1/analyze", b'{"type":"anomaly_detection"}'))
+        assert d["result"]["provider"] == "rules" and up.app.requests == before + 1
+    finally:
+        srv.shutdown()
+
+
+def test_chat_completions_endpoint(mon):
+    a = mon.app
+    r = a.handle("POST", "/v1/chat/completions", b'{"messages": []}')
+    assert r.code == 400
+    assert a.handle("GET", "/v1/chat/completions").code == 405
+    body = json.dumps({"model": "x", "max_tokens": 16,
+                       "messages": [{"role": "user", "content": "节点 n1 状态=NotReady [不健康]"}]}).encode()
+    d = J(a.handle("POST", "/v1/chat/completions", body))
+    assert d["object"] == "chat.completion" and d["choices"][0]["message"]["role"] == "assistant"
+    assert "NotReady" in d["choices"][0]["message"]["content"] and d["usage"]["completion_tokens"] > 0

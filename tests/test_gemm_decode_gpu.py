@@ -30,15 +30,15 @@ def _w(N, K, s=0.02):
 
 
 CASES = [  # (N, K, cfg)  - the engine's picks plus ragged / edge configurations
-    (6144, 4096, (8, 3, 4, 8)),
     (6144, 4096, (4, 1, 6, 8)),  # the engine's qkv pick: 6-wave workgroups
-    (4096, 4096, (4, 2, 3, 8)),
+    (6144, 4096, (8, 1, 8, 8)),
     (4096, 4096, (8, 1, 8, 8)),
     (4096, 4096, (4, 1, 4, 16)),
-    (4096, 14336, (8, 2, 4, 8)),
+    (4096, 14336, (8, 1, 8, 8)),
     (4096, 14336, (4, 1, 4, 16)),
-    (1024, 512, (2, 2, 8, 8)),
-    (384, 1024, (1, 4, 4, 8)),  # 24 n-tiles, 16 per workgroup: the second workgroup is ragged
+    (1024, 512, (2, 1, 4, 8)),
+    (320, 1024, (1, 1, 8, 8)),  # 20 n-tiles, 8 per workgroup: the third workgroup is ragged
+    (1280, 8192, (16, 1, 4, 16)),  # Llama-3-70B qkv at TP=8
 ]
 
 
@@ -74,7 +74,7 @@ def test_dec_rownorm_scale(M):
 
 
 @pytest.mark.parametrize("M", [1, 20, 64])
-@pytest.mark.parametrize("cfg", [(1, 1, 7, 16), (1, 1, 8, 16), (1, 2, 4, 8), (1, 1, 7, 8)])
+@pytest.mark.parametrize("cfg", [(1, 1, 7, 16), (1, 1, 8, 16), (1, 1, 7, 8)])
 def test_dec_swiglu8_feeds_down(M, cfg):
     K, F = 4096, 14336
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -88,7 +88,7 @@ def test_dec_swiglu8_feeds_down(M, cfg):
 
 
 @pytest.mark.parametrize("M", [1, 64])
-@pytest.mark.parametrize("cfg", [(1, 4, 8, 4), (1, 3, 8, 8)])
+@pytest.mark.parametrize("cfg", [(1, 4, 8, 4), (1, 3, 8, 8), (1, 2, 8, 8)])
 def test_dec_bf16_lm_head(M, cfg):
     """LM-head shape: N = 128256 does not divide the workgroup tile - the last workgroup is ragged."""
     N, K = 128256, 4096
@@ -99,6 +99,48 @@ def test_dec_bf16_lm_head(M, cfg):
     ref = x.float() @ w.float().t()
     _check(y, ref, f"lm_head M{M} cfg{cfg}")
     assert not torch.isnan(y).any(), "every column written (the ragged last workgroup included)"
+
+
+@pytest.mark.parametrize("M", [1, 64])
+@pytest.mark.parametrize("N", [32000, 16032])
+def test_dec_bf16_head_one_tile_per_wave(M, N):
+    """Mixtral's head (32000 rows) and a TP=8 vocab shard on the 8-wave one-tile config (1, 1, 8, 8)."""
+    K = 4096
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = _w(N, K)
+    y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.dec_gemm(ops.pack_activation(x), ops.pack_skinny(w), 1, M, out=y, cfg=(1, 1, 8, 8))
+    _check(y, x.float() @ w.float().t(), f"head N{N} M{M}")
+    assert not torch.isnan(y).any()
+
+
+@pytest.mark.parametrize("M", [1, 23, 64])
+@pytest.mark.parametrize("E,F,d", [(2, 14336, 4096), (4, 1024, 512)])
+def test_dec_grouped_experts_match_fp32(M, E, F, d):
+    """The MoE decode MLP on the grouped shared-A GEMM (grid.z = expert):
+    gate_up + SwiGLU of every expert over the shared rows, then the experts' down projections into
+    slabs scaled by the routing weights - their sum is the expert combine.  Against fp32."""
+    x = torch.randn(M, d, device=DEV, dtype=torch.bfloat16)
+    w13 = [torch.cat([_w(F, d), _w(F, d)]) for _ in range(E)]  # [gate; up] per expert
+    w2 = [_w(d, F) for _ in range(E)]
+    wg = torch.stack([ops.pack_skinny(ops.interleave_gate_up8(w)) for w in w13])
+    wd = torch.stack([ops.pack_skinny(w) for w in w2])
+    rw = torch.rand(M, E, device=DEV)
+    rw[rw < 0.5] = 0.0  # rows that skipped an expert
+    act = torch.empty((E, -(-M // 16), 2 * F // 64, 64, 8), device=DEV, dtype=torch.bfloat16)
+    ops.dec_gemm_grouped(ops.pack_activation(x), wg, 2, M, out=act)
+    ws = torch.full((E * M * d,), float("nan"), device=DEV, dtype=torch.float32)
+    ns = ops.dec_gemm_grouped(act, wd, 0, M, workspace=ws, row_w=rw)
+    assert ns == E
+    y = ws[: ns * M * d].view(ns, M, d).sum(0)
+    ref = torch.zeros(M, d, device=DEV)
+    for e in range(E):
+        g = (x.float() @ w13[e][:F].float().t()).to(torch.bfloat16).float()
+        u = (x.float() @ w13[e][F:].float().t()).to(torch.bfloat16).float()
+        h = (F_.silu(g) * u).to(torch.bfloat16).float()
+        _check(ops.unpack_skinny(act[e])[:M], h, f"grouped swiglu e{e} M{M}")
+        ref += (h @ w2[e].float().t()) * rw[:, e:e + 1]
+    _check(y, ref, f"grouped down + combine M{M} E{E}")
 
 
 @pytest.mark.parametrize("M", [1, 37, 64])

@@ -372,7 +372,7 @@ def test_llama_decode_skinny_matches_generic(monkeypatch):
                     decode_ws=ops.decode_workspace(B, m.hq, m.D, device=DEV, Hkv=m.hkv))
     kv0 = [(k.clone(), v.clone()) for k, v in kv]  # the caches before this step writes the new token
     a = m.forward(ids, meta, kv).float()
-    monkeypatch.setenv("K8SLLM_SKINNY", "0")
+    monkeypatch.setattr(CausalLM, "SKINNY_DECODE", False)
     b = m.forward(ids, meta, kv).float()
     # fp32 CPU reference of the same decode step (same weights, the pre-step caches)
     rm = CausalLM(cfg, device="cpu", dtype=torch.float32, init="empty")
@@ -480,13 +480,14 @@ def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):
 @pytest.mark.parametrize("order", ["seq", "work"])
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (16, 8), (64, 8)])
 @pytest.mark.parametrize("cached,new", [([0, 0, 0], [1609, 7, 300]), ([48, 160, 1023], [1, 130, 129]), ([5000], [64])])
-def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new, order, monkeypatch):
+def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new, order):
     """The LDS-DMA paged prefill kernel (v2: tiles staged verbatim from the cache, GQA-shared) ==
     the fp32 reference for G = 2, 4, 8 and cached prefixes, under both q-block orders."""
-    monkeypatch.setenv("K8SLLM_QB_ORDER", order)
     D = 128
     qkv, cu, cs, kc, vc, bt = _paged_prefill_case(cached, new, hq, hkv, D)
-    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    qs, st = ops.prefill_qblocks(cu.tolist(), ctx_starts=cached, order=order)
+    qb = (torch.tensor(qs, dtype=torch.int32, device=DEV), torch.tensor(st, dtype=torch.int32, device=DEV))
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), qblocks=qb, paged=(cs, kc, vc, bt))
     exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
     _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what=f"paged prefill v2 G={hq // hkv}")
 

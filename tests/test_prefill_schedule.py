@@ -7,13 +7,12 @@ from k8s_llm_monitor_amd import ops
 
 
 @pytest.mark.parametrize("order", ["seq", "work"])
-def test_qblocks_cover_every_block_once(order, monkeypatch):
-    monkeypatch.setenv("K8SLLM_QB_ORDER", order)
+def test_qblocks_cover_every_block_once(order):
     lens, starts = [300, 1609, 7, 128, 1000], [0, 0, 50, 4096, 0]
     cu = [0]
     for n in lens:
         cu.append(cu[-1] + n)
-    seqs, firsts = ops.prefill_qblocks(cu, ctx_starts=starts)
+    seqs, firsts = ops.prefill_qblocks(cu, ctx_starts=starts, order=order)
     want = sorted((i, s) for i, n in enumerate(lens) for s in range(0, n, 128))
     assert sorted(zip(seqs, firsts)) == want
     work = [starts[i] + s for i, s in zip(seqs, firsts)]

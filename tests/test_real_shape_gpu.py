@@ -16,17 +16,11 @@ def _fp32_reference(gpu_model):
     from k8s_llm_monitor_amd.models import CausalLM
     from k8s_llm_monitor_amd.parallel.state import ParallelState
 
-    import os
-
-    old = os.environ.get("K8SLLM_SKINNY")
-    os.environ["K8SLLM_SKINNY"] = "0"  # the reference runs the plain row-major path only
+    CausalLM.SKINNY_DECODE = False  # the reference runs the plain row-major path only
     try:
         ref = CausalLM(gpu_model.cfg, device="cpu", dtype=torch.float32, pstate=ParallelState(), init="empty")
     finally:
-        if old is None:
-            os.environ.pop("K8SLLM_SKINNY", None)
-        else:
-            os.environ["K8SLLM_SKINNY"] = old
+        CausalLM.SKINNY_DECODE = True
     ref.embed.copy_(gpu_model.embed.float().cpu())
     if ref.lm_head is not ref.embed:
         ref.lm_head.copy_(gpu_model.lm_head.float().cpu())

@@ -54,12 +54,12 @@ def test_model_single_weight_copy_cpu():
 
 
 def test_skinny_splits_bounds(monkeypatch):
-    monkeypatch.delenv("K8SLLM_SKINNY_SPLITS", raising=False)
+    monkeypatch.setattr(ops, "SKINNY_SPLITS_FORCE", 0)
     assert ops.skinny_splits(4096, 4096) == 4
     assert ops.skinny_splits(4096, 14336) == 4
     assert ops.skinny_splits(6144, 4096) == 3
     assert ops.skinny_splits(64, 256) == 1
-    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")
+    monkeypatch.setattr(ops, "SKINNY_SPLITS_FORCE", 3)
     assert ops.skinny_splits(4096, 4096) == 3
 
 
@@ -82,11 +82,11 @@ def test_decode_skinny_path_matches_generic_cpu(monkeypatch, model):
     SwiGLU epilogue) equals the generic path, on the CPU forms of the ops (fp32)."""
     from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
 
-    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "3")  # force real split-K slicing on tiny shapes
+    monkeypatch.setattr(ops, "SKINNY_SPLITS_FORCE", 3)  # force real split-K slicing on tiny shapes
     cfg = get_config(model)
     m = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
     assert m._skinny_ws is not None and m._split_d == 3
-    monkeypatch.setenv("K8SLLM_SKINNY_SPLITS", "0")
+    monkeypatch.setattr(ops, "SKINNY_SPLITS_FORCE", 0)
     m0 = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=3)
     assert m0._split_d == 0  # automatic split-K per call
     B, bs, nb = 3, 16, 8
@@ -98,7 +98,7 @@ def test_decode_skinny_path_matches_generic_cpu(monkeypatch, model):
                     block_tables=torch.arange(B * 2, dtype=torch.int32).view(B, 2) % nb, seq_lens=lens)
     ids = torch.tensor([5, 77, 300], dtype=torch.int32)
     a = m.forward(ids, meta, kv)
-    monkeypatch.setenv("K8SLLM_SKINNY", "0")
+    monkeypatch.setattr(CausalLM, "SKINNY_DECODE", False)
     b = m.forward(ids, meta, kv)
     assert (a - b).abs().max().item() < 1e-4
 

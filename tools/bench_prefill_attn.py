@@ -23,7 +23,7 @@ def main() -> None:
     ap.add_argument("--seqs", type=int, default=10)
     ap.add_argument("--len", type=int, default=1609)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--orders", default="work,seq", help="q-block orders to time (K8SLLM_QB_ORDER)")
+    ap.add_argument("--orders", default="work,seq", help="q-block orders to time (ops.prefill_qblocks order)")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     T = a.seqs * a.len
@@ -62,8 +62,7 @@ def main() -> None:
     res: dict = {}
     qbo = {}
     for order in a.orders.split(","):
-        os.environ["K8SLLM_QB_ORDER"] = order
-        qs, st = ops.prefill_qblocks(cu.tolist())
+        qs, st = ops.prefill_qblocks(cu.tolist(), order=order)
         qbo[order] = (torch.tensor(qs, dtype=torch.int32, device="cuda"),
                       torch.tensor(st, dtype=torch.int32, device="cuda"))
     for _ in range(3):

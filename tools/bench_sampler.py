@@ -23,21 +23,16 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--b", type=int, default=64)
     ap.add_argument("--v", type=int, default=128256)
-    ap.add_argument("--parts", default="", help="comma list of K8SLLM_SAMPLE_PARTS values to time")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
     logits = (torch.randn(a.b, a.v, device=dev) * 1.28).to(torch.bfloat16)
     out = torch.empty(a.b, dtype=torch.int32, device=dev)
     rng = torch.tensor([1, 0], device=dev, dtype=torch.int64)
-    for parts in (a.parts.split(",") if a.parts else [""]):
-        if parts:
-            os.environ["K8SLLM_SAMPLE_PARTS"] = parts
-        for name, t in (("greedy", 0.0), ("T0.1", 0.1), ("T1.0", 1.0)):
-            temps = torch.full((a.b,), t, device=dev)
-            us = timeit(lambda i: ops.sample(logits, temps, None, None, rng, out=out, advance=True), 64, per_graph=8)
-            print(json.dumps({"op": "sample", "B": a.b, "V": a.v, "mode": name, "parts": parts or "auto",
-                              "us": round(us, 2)}), flush=True)
+    for name, t in (("greedy", 0.0), ("T0.1", 0.1), ("T1.0", 1.0)):
+        temps = torch.full((a.b,), t, device=dev)
+        us = timeit(lambda i: ops.sample(logits, temps, None, None, rng, out=out, advance=True), 64, per_graph=8)
+        print(json.dumps({"op": "sample", "B": a.b, "V": a.v, "mode": name, "us": round(us, 2)}), flush=True)
 
 
 if __name__ == "__main__":

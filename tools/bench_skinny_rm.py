@@ -50,7 +50,7 @@ def main() -> None:
                                      ("rowmajor_w4", wrm, "4")):
                     if tag not in a.impls.split(","):
                         continue
-                    os.environ["K8SLLM_SKINNY_WAVES"] = wv
+                    ops.SKINNY_WAVES_FORCE = int(wv)
                     if name.startswith("gate_up"):
                         fn = (lambda i, ws_=ws_: ops.skinny_swiglu(xp, ws_[i % ncopy], out=act, rows=M, packed_out=True))
                     else:

@@ -34,10 +34,10 @@ def main() -> None:
         for _ in range(3):
             for s in splits:
                 for wv in ("2", "4"):
-                    os.environ["K8SLLM_SKINNY_WAVES"] = wv
+                    ops.SKINNY_WAVES_FORCE = int(wv)
                     res.setdefault((s, wv), []).append(
                         timeit(lambda i, s=s: ops.skinny_slabs(xp, wrm[i % ncopy], ws, s, rows=M), 320))
-        os.environ.pop("K8SLLM_SKINNY_WAVES", None)
+        ops.SKINNY_WAVES_FORCE = 0
         for (s, wv), ts in sorted(res.items()):
             t = min(ts)
             print(json.dumps({"op": name, "M": M, "splits": s, "waves": int(wv), "us": round(t, 2),

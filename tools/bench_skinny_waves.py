@@ -39,7 +39,7 @@ def main() -> None:
             act = ops.packed_empty(M, F, torch.bfloat16, dev)
             wsp = ops.skinny_workspace(M, N, 16, dev)
             for waves in ("4", "8"):
-                os.environ["K8SLLM_SKINNY_WAVES"] = waves
+                ops.SKINNY_WAVES_FORCE = int(waves)
                 if name == "gate_up":
                     cases = [("swiglu", lambda i: ops.skinny_swiglu(xp, wps[i % ncopy], out=act, rows=M,
                                                                    packed_out=True))]
