@@ -444,7 +444,7 @@ def dec_gemm_grouped(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, wor
     N, K = wp.shape[1] * 16, wp.shape[2] * 32
     M = rows
     if cfg is None:
-        cfg = dec_config(N, K, epi)
+        cfg = dec_config(N, K, epi, experts=E)
     if cfg is None:
         raise ValueError(f"gemm_dec_grouped: no configuration for N={N} K={K} epi={epi}")
     S, ntw, waves, depth = cfg

@@ -337,11 +337,17 @@ static int car_check(CarState* st, long n) {
   return 0;
 }
 
-// workgroups for an n-element message: one per 2048 elements (8 per thread), at most CAR_MAX_WG -
-// the copy / reduce loops are bandwidth-bound, so a 16 MiB message uses every one of 256 CUs
+// workgroups for an n-element message: one per 2048 elements (8 per thread), at most CAR_GRID_CAP.
+// The cap keeps a call off most of the chip: a workgroup spinning on a peer's flag holds its CU's
+// wave slots, and a full-register GEMM workgroup (256 accumulators per wave: a whole SIMD register
+// file) cannot be placed beside it - with every CU holding one, the next GEMM of this rank (or,
+// ranks sharing a GPU, of the peer the spin waits for) could not start at all.  64 workgroups
+// leave >= 3/4 of the CUs to compute (the overlapped TP prefill runs its all-reduces on the comm
+// stream beside the other micro-batch's GEMMs) and still keep ~1 MiB of loads in flight.
+constexpr int CAR_GRID_CAP = 64;
 static int car_grid(long n) {
   const long nb = (n / 8 + 255) / 256;
-  return (int)(nb < 1 ? 1 : (nb > CAR_MAX_WG ? CAR_MAX_WG : nb));
+  return (int)(nb < 1 ? 1 : (nb > CAR_GRID_CAP ? CAR_GRID_CAP : nb));
 }
 
 // out = sum over ranks of in (n bf16, n % 8 == 0, n <= max_elems); in may alias out.

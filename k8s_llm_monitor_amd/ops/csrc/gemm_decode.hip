@@ -111,6 +111,25 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   // loads only (the seam protocol); otherwise plain loads
   const __amdgpu_buffer_rsrc_t a_rs = dec_rsrc(A, (long)MT * 16 * K * 2);
 
+  // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave.  The weights do not
+  // depend on this launch's norm phase, so with NP the ring is filled FIRST and its HBM latency
+  // runs beside the slab reduce and the seam; otherwise after chunk 0's staging loads (below).
+  const u32x4* wp[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+    wp[t] = reinterpret_cast<const u32x4*>(W) + ((long)min(tile0 + t, (N >> 4) - 1) * ksteps + kb) * 64 + lane;
+  u32x4 wr[DEPTH][NTW];
+  auto ring_fill = [&]() {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) wr[d][t] = __builtin_nontemporal_load(wp[t] + d * 64);
+  };
+  if constexpr (NP) {
+    ring_fill();
+    __builtin_amdgcn_sched_barrier(0);  // issued before the norm phase's slab loads
+  }
+
   // ---- NP: the fused add-RMSNorm phase and the grid seam (see DecNorm)
   if constexpr (NP) {
     const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -252,16 +271,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   // edge), so the counted vmcnt there leaves the weight ring in flight (with the staging loads
   // last, the merged wait drained the ring at every chunk boundary).
   stage_load(0);
-  // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave
-  const u32x4* wp[NTW];
-#pragma unroll
-  for (int t = 0; t < NTW; ++t)
-    wp[t] = reinterpret_cast<const u32x4*>(W) + ((long)min(tile0 + t, (N >> 4) - 1) * ksteps + kb) * 64 + lane;
-  u32x4 wr[DEPTH][NTW];
-#pragma unroll
-  for (int d = 0; d < DEPTH; ++d)
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) wr[d][t] = __builtin_nontemporal_load(wp[t] + d * 64);
+  if constexpr (!NP) ring_fill();
 
   // ---- deferred RMSNorm: 1/rms of each A row from its partial sums of squares (loads issued
   // above, ahead of the A staging and the weight ring, so this wait leaves both in flight)

@@ -1,14 +1,13 @@
-# round-5 checks on one GPU: the new decode / tile parity tests, then TP=2 on the one GPU:
-# (1) the serial-all-reduce rehearsal (K8SLLM_TP_OVERLAP=0) and the overlapped one, (2) the
-# overlapped-prefill timeline tool (8B shapes, 8 layers, IPC all-reduce on the comm stream) with
-# per-rank kernel traces.  A Python-level failure still runs the next step; a fault / abort / time
-# limit ends the script.
+# TP=2 on the one GPU after capping the IPC all-reduce grid: serial and overlapped engine
+# rehearsals, then the overlap timeline tool with per-rank kernel traces.
 set -o pipefail
 mkdir -p gpurun_out
 fatal() { case $1 in 124|134|137|139) echo "fatal rc $1"; exit 1;; esac; }
-timeout -k 10 600 python -u -m pytest tests/test_gemm_decode_gpu.py tests/test_tile_real_shapes_gpu.py \
-  tests/test_real_shape_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5_tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r5_tests.log; fatal $rc
+timeout -k 10 700 python -u -m pytest tests/test_gemm_decode_gpu.py tests/test_tile_real_shapes_gpu.py \
+  tests/test_real_shape_gpu.py "tests/test_ops_gpu.py::test_flash_prefill_paged_v2_long_prompts" \
+  "tests/test_ops_gpu.py::test_flash_prefill_paged_v2_moderate_max_jumps" -m gpu -q --timeout 300 \
+  --timeout-method thread > gpurun_out/r5_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/r5_tests.log | tail -12; fatal $rc
 K8SLLM_TP_OVERLAP=0 bash scripts/gpu/run.sh rehearse tp2serial --gpus 2 --tp 2 --model llama-tiny-d128 --steps 2 --warmup 1
 rc=$?; echo "rehearsal serial rc=$rc"; fatal $rc
 bash scripts/gpu/run.sh rehearse tp2ov --gpus 2 --tp 2 --model llama-tiny-d128 --steps 2 --warmup 1

@@ -449,7 +449,7 @@ def test_deferred_rmsnorm_chain(M):
     _close(ops.reduce_slabs(ws, ns, M, N).cpu(), y_ref, atol=3e-2, rtol=3e-2, what="deferred-norm slabs")
 
 
-def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):
+def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False, jumps=None):
     S = len(new)
     tot = [c + n for c, n in zip(cached, new)]
     nblk = [(t + bs - 1) // bs for t in tot]
@@ -468,6 +468,15 @@ def _paged_prefill_case(cached, new, hq, hkv, D=128, bs=16, spike=False):
     if spike:  # one query row against one key row: the running max jumps late in the sequence
         qkv[T - 1, :D] = 8.0
         qkv[T - 3, (hq) * D:(hq) * D + D] = 8.0
+    if jumps:  # q = e_0 on every head, so a score is scale * k[:, 0]; k[:, 0] steps up at given rows
+        q3 = qkv.view(T, hq + 2 * hkv, D)
+        q3[:, :hq].zero_()
+        q3[:, :hq, 0] = 1.0
+        q3[:, hq:hq + hkv, 0] = (torch.randn(T, hkv, device=DEV) * 0.5).to(torch.bfloat16)
+        level = 0.0
+        for row, log2_jump in jumps:  # the running max rises by 2^log2_jump (in exp units) at row
+            level += log2_jump * math.log(2) * math.sqrt(D)
+            q3[row, hq:hq + hkv, 0] = level
     cu = torch.tensor([0] + list(torch.tensor(new).cumsum(0).tolist()), dtype=torch.int32, device=DEV)
     cs = torch.tensor(cached, dtype=torch.int32, device=DEV)
     pos = torch.cat([torch.arange(c, c + n) for c, n in zip(cached, new)]).to(DEV, torch.int32)
@@ -490,6 +499,46 @@ def test_flash_prefill_paged_v2_gqa(hq, hkv, cached, new, order):
     out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), qblocks=qb, paged=(cs, kc, vc, bt))
     exp = ref.paged_prefill(qkv.cpu(), cu.cpu(), cs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), hq, hkv, D, 1 / math.sqrt(D))
     _close(out.cpu(), exp, atol=2e-2, rtol=2e-2, what=f"paged prefill v2 G={hq // hkv}")
+
+
+def _attn_rows_fp32(qkv, kc, vc, bt, cached, n_new, rows, hq, hkv, D):
+    """fp32 causal attention of the given query rows of ONE sequence (keys = cached prefix + new)."""
+    k, v = ref.gather_kv(kc, vc, bt[0], cached + n_new)
+    k, v = k.float(), v.float()  # [T, Hkv, D]
+    G = hq // hkv
+    q = qkv[rows, : hq * D].float().view(len(rows), hkv, G, D)
+    s = torch.einsum("rhgd,thd->hgrt", q, k) / math.sqrt(D)
+    pos = torch.tensor(rows, device=qkv.device) + cached
+    s = s.masked_fill(torch.arange(cached + n_new, device=qkv.device)[None, :] > pos[:, None], float("-inf"))
+    o = torch.einsum("hgrt,thd->rhgd", torch.softmax(s, -1), v)
+    return o.reshape(len(rows), hq * D)
+
+
+@pytest.mark.parametrize("cached,new", [(0, 8000), (0, 16000), (3000, 8000)])
+def test_flash_prefill_paged_v2_long_prompts(cached, new):
+    """the shapes the flash prefill is benchmarked on (8k / 16k new tokens, and a
+    chunk after a cached prefix) against fp32 - first, middle and last 256 query rows (the lazy
+    reference max sees its longest runs at the end of a long prompt)."""
+    hq, hkv, D = 32, 8, 128
+    qkv, cu, cs, kc, vc, bt = _paged_prefill_case([cached], [new], hq, hkv, D)
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    rows = list(range(256)) + list(range(new // 2, new // 2 + 256)) + list(range(new - 256, new))
+    exp = _attn_rows_fp32(qkv, kc, vc, bt, cached, new, rows, hq, hkv, D)
+    _close(out[rows].float(), exp, atol=2e-2, rtol=2e-2, what=f"paged prefill v2 {cached}+{new}")
+
+
+@pytest.mark.parametrize("jumps", [[(300, 4), (700, 7), (1300, 6)],           # below the 2^8 threshold
+                                   [(200, 7), (230, 7), (900, 10)],          # two in one 64-key tile, then over
+                                   [(64, 9), (640, 4), (641, 5), (1500, 8)]])  # exactly at the threshold
+def test_flash_prefill_paged_v2_moderate_max_jumps(jumps):
+    """The lazy rescale (the reference max moves only on a > 2^8 jump): tile maxima rising by
+    2^4 .. 2^10 at chosen rows, every query row against fp32."""
+    hq, hkv, D = 32, 8, 128
+    new = 1700
+    qkv, cu, cs, kc, vc, bt = _paged_prefill_case([37], [new], hq, hkv, D, jumps=jumps)
+    out = ops.flash_prefill(qkv, cu, hq, hkv, D, 1 / math.sqrt(D), paged=(cs, kc, vc, bt))
+    exp = _attn_rows_fp32(qkv, kc, vc, bt, 37, new, list(range(new)), hq, hkv, D)
+    _close(out.float(), exp, atol=2e-2, rtol=2e-2, what=f"paged prefill v2 jumps {jumps}")
 
 
 def test_flash_prefill_paged_v2_softmax_spike():
