@@ -96,11 +96,12 @@ class ModelRunner:
 
     # --------------------------------------------------------------------- helpers
     @staticmethod
-    def _micro_split(cu: np.ndarray, nd: int) -> int:
+    def _micro_split(cu: np.ndarray, nd: int, min_rows: int = 4096) -> int:
         """First sequence of the second prefill micro-batch: the split nearest half the rows (0:
-        no split - a mixed step, or a single sequence)."""
+        no split - a mixed step, a single sequence, or fewer than ``min_rows`` rows, where the
+        all-reduces are small and halving the GEMMs' M costs more than the overlap hides)."""
         S = len(cu) - 1
-        if nd or S < 2:
+        if nd or S < 2 or cu[S] < min_rows:
             return 0
         k = int(np.argmin(np.abs(cu[1:S] - cu[S] / 2))) + 1
         return k

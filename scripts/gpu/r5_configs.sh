@@ -1,5 +1,5 @@
 # every BASELINE config on the current tree, one GPU.  PART=a: Mixtral (bench +
-# kernel trace) and the 70B TP=1 proxy; PART=b: podcomm, latency, production 2000-token, Poisson.
+# kernel trace); PART=c: the 70B TP=1 proxy; PART=b: podcomm, latency, production 2000-token, Poisson.
 set -o pipefail
 mkdir -p gpurun_out
 part=${1:-a}
@@ -14,6 +14,7 @@ if [ "$part" = a ]; then
   bash scripts/gpu/run.sh prof mixtral --model mixtral-8x7b > gpurun_out/prof_mixtral_out.txt 2>&1 \
     || { tail -20 gpurun_out/prof_mixtral_out.txt; exit 1; }
   head -3 gpurun_out/prof_mixtral_steps.txt; grep -c "Cijk_" gpurun_out/prof_mixtral_summary.md || true
+elif [ "$part" = c ]; then
   b llama70b_tp1 700 --model llama-3-70b --steps 2 --warmup 1
 else
   b podcomm 400 --path podcomm --steps 3 --warmup 1

@@ -242,7 +242,7 @@ def _overlap_worker(rank, world, port, q):
                             logits_idx=torch.tensor(np.asarray(c[1:]) - 1, dtype=torch.int64))
 
         serial = m.forward(ids, meta_for(cu, pos), None)
-        kA = ModelRunner._micro_split(cu, 0)
+        kA = ModelRunner._micro_split(cu, 0, min_rows=0)
         TA = int(cu[kA])
         full = meta_for(cu, pos)
         full.micro = (meta_for(cu[: kA + 1], pos[:TA]), meta_for(cu[kA:] - cu[kA], pos[TA:]), TA)

@@ -56,13 +56,19 @@ def rank_main(a) -> None:
     ids = torch.randint(0, cfg.vocab_size, (T,), generator=g, dtype=torch.int32).to(dev)
     pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).to(dev)
 
+    from k8s_llm_monitor_amd import ops
+
     def meta_for(c, p):
+        # the q-block schedule on the device, as the engine's runner stages it (no per-call host copy)
+        qs, st = ops.prefill_qblocks([int(v) for v in c])
         return AttnMeta(is_prefill=True, positions=p,
                         slot_mapping=torch.full((len(p),), -1, dtype=torch.int32, device=dev),
                         cu_seqlens=torch.tensor(c, dtype=torch.int32, device=dev),
+                        qb_seq=torch.tensor(qs, dtype=torch.int32, device=dev),
+                        qb_start=torch.tensor(st, dtype=torch.int32, device=dev),
                         logits_idx=torch.tensor(np.asarray(c[1:]) - 1, dtype=torch.int64, device=dev))
 
-    kA = ModelRunner._micro_split(cu, 0)
+    kA = ModelRunner._micro_split(cu, 0, min_rows=0)
     TA = int(cu[kA])
     serial_meta = meta_for(cu, pos)
     over_meta = meta_for(cu, pos)
