@@ -104,6 +104,8 @@ class ModelRunner:
         if nd or S < 2 or cu[S] < min_rows:
             return 0
         k = int(np.argmin(np.abs(cu[1:S] - cu[S] / 2))) + 1
+        if min(cu[k], cu[S] - cu[k]) < min_rows // 4:
+            return 0  # too lopsided: the short half would leave the tile GEMM (TILE_MIN_M rows)
         return k
 
     def bucket_for(self, n: int) -> int:

@@ -111,9 +111,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   // loads only (the seam protocol); otherwise plain loads
   const __amdgpu_buffer_rsrc_t a_rs = dec_rsrc(A, (long)MT * 16 * K * 2);
 
-  // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave.  The weights do not
-  // depend on this launch's norm phase, so with NP the ring is filled FIRST and its HBM latency
-  // runs beside the slab reduce and the seam; otherwise after chunk 0's staging loads (below).
+  // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave, filled after chunk 0's
+  // staging loads (below).  (With NP, filling it before the norm phase - the weights do not depend
+  // on it - measured SLOWER: gate_up 49.9 vs 45.7 us, the ring's HBM loads queue ahead of the
+  // L2-resident slab loads the norm phase waits for; profiles/r05/README.md.)
   const u32x4* wp[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
@@ -125,10 +126,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
 #pragma unroll
       for (int t = 0; t < NTW; ++t) wr[d][t] = __builtin_nontemporal_load(wp[t] + d * 64);
   };
-  if constexpr (NP) {
-    ring_fill();
-    __builtin_amdgcn_sched_barrier(0);  // issued before the norm phase's slab loads
-  }
 
   // ---- NP: the fused add-RMSNorm phase and the grid seam (see DecNorm)
   if constexpr (NP) {
@@ -271,7 +268,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   // edge), so the counted vmcnt there leaves the weight ring in flight (with the staging loads
   // last, the merged wait drained the ring at every chunk boundary).
   stage_load(0);
-  if constexpr (!NP) ring_fill();
+  ring_fill();
 
   // ---- deferred RMSNorm: 1/rms of each A row from its partial sums of squares (loads issued
   // above, ahead of the A staging and the weight ring, so this wait leaves both in flight)
