@@ -435,6 +435,16 @@ def _print_trace(trace: list, t0: float) -> None:
     if dec:
         print(f"[trace] decode steps {len(dec)} first +{(dec[0][0] - t0) * 1e3:.1f} last +{(dec[-1][0] - t0) * 1e3:.1f} ms",
               file=sys.stderr)
+        # host side of the decode pipeline: launch-to-launch interval, host ms inside decode_launch,
+        # and ms blocked on the previous step's tokens (near 0 = the host, not the GPU, sets the pace)
+        iv = sorted((b[0] - a_[0]) * 1e3 for a_, b in zip(dec, dec[1:]) if b[0] - a_[0] < 0.05)
+        la = sorted(e[3] for e in ev if e[1] == "dlaunch")
+        wt = sorted(e[3] for e in ev if e[1] == "dwait")
+
+        def q(v, f):
+            return v[min(len(v) - 1, int(f * len(v)))] if v else float("nan")
+        print(f"[trace] decode interval p50 {q(iv, .5):.3f} p90 {q(iv, .9):.3f} ms; launch p50 {q(la, .5):.3f} "
+              f"p90 {q(la, .9):.3f} ms; wait p10 {q(wt, .1):.3f} p50 {q(wt, .5):.3f} ms", file=sys.stderr)
 
 
 def main(argv=None) -> None:

@@ -229,10 +229,13 @@ class LLMEngine:
         seqs = self._attention_row_order(seqs)
         prev_rows = self._inflight_rows
         src = [prev_rows.get(q.seq_id, -1) for q in seqs]
+        t_l = time.perf_counter() if self.trace is not None else 0.0
         handle = self.runner.decode_launch(seqs, src, publish=self._publish)
         self.counters["decode_steps"] += 1
         if self.trace is not None:
-            self.trace.append((time.perf_counter(), "decode", len(seqs), 0))
+            now = time.perf_counter()
+            self.trace.append((now, "decode", len(seqs), 0))
+            self.trace.append((now, "dlaunch", len(seqs), (now - t_l) * 1e3))  # host ms in decode_launch
         for q in seqs:
             q.output_ids.append(self.PENDING)
         prev = self._inflight
@@ -318,7 +321,10 @@ class LLMEngine:
             raise RuntimeError("custom all-reduce: a TP peer did not arrive (step output invalid)")
 
     def _resolve_step(self, seqs: list, handle) -> list[Sequence]:
+        t_w = time.perf_counter() if self.trace is not None else 0.0
         toks = self.runner.decode_collect(handle)
+        if self.trace is not None:  # host ms blocked on the step's tokens (0: the host is the bottleneck)
+            self.trace.append((time.perf_counter(), "dwait", len(seqs), (time.perf_counter() - t_w) * 1e3))
         self._check_collectives()
         ms = handle.gpu_ms() if hasattr(handle, "gpu_ms") else None
         if ms is not None:  # a back-to-back decode step: its GPU time at this row count and context
