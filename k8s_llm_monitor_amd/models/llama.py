@@ -903,23 +903,31 @@ class CausalLM:
             return ops.dec_gemm(x, wd, 0, rows, workspace=self._skinny_ws, rownorm=rownorm)
         return ops.skinny_slabs(x, L[key + "_p"], self._skinny_ws, split, rows=rows, rownorm=rownorm)
 
-    def _want_dec(self) -> tuple:
+    def _want_dec(self) -> set:
         """Which decode-only fragment-packed copies gemm_decode.hip gets (``DECODE_GEMM`` = auto |
-        dec | rm): (attention + dense MLP + LM head, MoE experts).  auto: a dense Llama whose
-        weights take at most a quarter of the device (Llama-3-8B: 16 GB of 288; 70B at TP=1 keeps
-        the single row-major copy and gemm_skinny); a MoE model always gets its attention and LM
-        head copies (a few GB) and the expert copies while weights + copies stay within 70 % of
-        the device (Mixtral-8x7B at TP=1: 93 + 93 GB of 288, leaving the KV pool ~100 GB)."""
+        dec | rm): a subset of {"head", "attn", "mlp", "experts"}.  auto, on the GPU, with W the
+        weights' bytes: the LM head always (<= 2.1 GB, Llama-3-70B); the attention projections
+        while W + their copies fit 70 % of the device; a dense MLP while 2W fits half of it
+        (Llama-3-8B: 16 GB of 288); MoE experts while 2W fits 70 % (Mixtral-8x7B at TP=1: 93 + 93
+        GB).  Llama-3-70B at TP=1 (141 GB) gets head + attention copies (+24 GB) and keeps its MLP
+        on the row-major skinny kernel."""
         mode = self.DECODE_GEMM
         if mode in ("rm", "0", "off") or self.cfg.arch != "llama":
-            return False, False
+            return set()
         if mode in ("dec", "1", "on") or self.device.type != "cuda":
-            return True, True
+            return {"head", "attn", "mlp", "experts"}
         total = torch.cuda.get_device_properties(self.device).total_memory
-        both = self.num_local_params() * 2 * 2
+        w = self.num_local_params() * 2
+        attn = sum((L["wqkv"].numel() + L["wo"].numel()) * 2 for L in self.layers)
+        parts = {"head"}
+        if w + attn <= 0.7 * total:
+            parts.add("attn")
         if self.cfg.is_moe:
-            return True, both <= 0.7 * total
-        return both <= total // 2, False
+            if 2 * w <= 0.7 * total:
+                parts.add("experts")
+        elif 2 * w <= total // 2:
+            parts.add("mlp")
+        return parts
 
     def _init_dec(self) -> None:
         """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
@@ -927,21 +935,20 @@ class CausalLM:
         ([N/16, K/32, 64, 8]), w13_d (gate/up interleaved per 16 rows as [8 gate | 8 up]), and the
         LM head.  Prefill keeps reading the row-major tensors."""
         self.lm_head_d = None
-        dense, experts = self._want_dec()
-        if not dense:
-            return
+        parts = self._want_dec()
         c = self.cfg
         for L in self.layers:
-            for key in ("wqkv", "wo") if c.is_moe else ("wqkv", "wo", "w2"):
+            keys = (("wqkv", "wo") if "attn" in parts else ()) + (("w2",) if "mlp" in parts and not c.is_moe else ())
+            for key in keys:
                 N, K = L[key].shape
                 if ops.dec_available(N, K, 0):
                     L[key + "_d"] = ops.pack_skinny(L[key])
-            if not c.is_moe:
+            if "mlp" in parts and not c.is_moe:
                 w = ops.deinterleave_gate_up(L["w13"]) if self._w13_il else L["w13"]
                 if ops.dec_available(w.shape[0], w.shape[1], 2):
                     L["w13_d"] = ops.pack_skinny(ops.interleave_gate_up8(w))
                 del w
-            elif experts:  # [E, ...] stacks for the grouped (grid.z = expert) decode launches
+            elif "experts" in parts and c.is_moe:  # [E, ...] stacks for the grouped (grid.z = expert) launches
                 E, F2, d = L["w13"].shape
                 if (ops.dec_config(F2, d, 2, experts=E) is not None
                         and ops.dec_config(d, F2 // 2, 0, experts=E) is not None):
@@ -949,7 +956,7 @@ class CausalLM:
                         ops.deinterleave_gate_up(w) if self._w13_il else w)) for w in L["w13"]])
                     L["w2_dg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
         N, K = self.lm_head.shape
-        if N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
+        if "head" in parts and N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
             self.lm_head_d = ops.pack_skinny(self.lm_head)
 
     def _tp_tail(self, ws, ns: int, residual: torch.Tensor, norm_w, packed: bool) -> Optional[torch.Tensor]:
