@@ -73,7 +73,8 @@ int k8sllm_car_handle_size();
 int k8sllm_car_open(void* state, const void* all_handles);
 int k8sllm_car_all_reduce(void* state, const void* in, void* out, long n, long spin_limit, int algo, hipStream_t s);
 int k8sllm_car_fused_tail(void* state, const float* slabs, int ns, long slab_stride, void* residual, const void* w,
-                          void* out, long ldo, int M, int d, float eps, int packed, long spin_limit, hipStream_t s);
+                          void* out, long ldo, int M, int d, float eps, int packed, long spin_limit, int algo,
+                          hipStream_t s);
 int k8sllm_car_error(void* state);
 int k8sllm_car_all_gather(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
 int k8sllm_car_all_to_all(void* state, const void* in, void* out, long n, long spin_limit, hipStream_t s);
@@ -907,7 +908,7 @@ void car_all_reduce(int64_t state, torch::Tensor in, torch::Tensor out, int64_t 
 // TP row-parallel tail in one launch: slabs [ns, M, d] fp32 -> reduced over ranks -> residual +=,
 // RMSNorm * w -> out (row-major [M, d] or fragment-packed when packed).
 void car_fused_tail(int64_t state, torch::Tensor slabs, int64_t ns, torch::Tensor residual, torch::Tensor w,
-                    torch::Tensor out, double eps, bool packed, int64_t spin_limit) {
+                    torch::Tensor out, double eps, bool packed, int64_t spin_limit, int64_t algo) {
   dev_bf16(residual, "residual"); dev_bf16(w, "w"); dev_bf16(out, "out");
   TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == torch::kFloat32 && slabs.is_contiguous(), "slabs fp32");
   TORCH_CHECK(residual.dim() == 2 && residual.is_contiguous() && w.is_contiguous() && out.is_contiguous(),
@@ -918,7 +919,7 @@ void car_fused_tail(int64_t state, torch::Tensor slabs, int64_t ns, torch::Tenso
               "car_fused_tail out size");
   check(k8sllm_car_fused_tail((void*)(intptr_t)state, slabs.data_ptr<float>(), (int)ns, (long)M * d,
                               residual.data_ptr(), w.data_ptr(), out.data_ptr(), d, M, d, (float)eps, packed ? 1 : 0,
-                              (long)spin_limit, cur()),
+                              (long)spin_limit, (int)algo, cur()),
         "car_fused_tail");
 }
 

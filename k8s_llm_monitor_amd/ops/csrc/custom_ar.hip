@@ -195,7 +195,12 @@ __global__ __launch_bounds__(256) void car_kernel(const bf16_t* in, bf16_t* out,
 //   out = bf16(residual * rsqrt(mean(residual^2) + eps) * w), row-major (ldo) or, when PACKED,
 //         in the fragment-packed A layout of the next skinny GEMM (act_index)
 // - exactly the arithmetic of reduce_slabs -> all-reduce -> fused_add_rms_norm -> pack_activation.
-template <int NC, bool PACKED>
+// TS (two-shot): rank r sums only its 1/world of the row's columns over the ranks (rank order, fp32,
+// rounded to bf16 in place in its staging row) and every rank then gathers the other ranks' reduced
+// parts - 2 (W - 1) / W of a row crosses the links per rank instead of W - 1 rows: at TP=8 decode
+// (64 x 8192 bf16 per tail) 1.75 MiB inbound per rank instead of 7.  Same sums in the same order:
+// bit-identical to the one-shot form.
+template <int NC, bool PACKED, bool TS = false>
 __global__ __launch_bounds__(256) void car_fused_tail_kernel(const float* __restrict__ slabs, int ns, long slab_stride,
                                                              bf16_t* __restrict__ residual,
                                                              const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
@@ -223,6 +228,17 @@ __global__ __launch_bounds__(256) void car_fused_tail_kernel(const float* __rest
     }
   }
   car_exchange<false>(p, rank, world, m, e, spin_limit);
+  const int cs = d / world;  // TS: columns per rank's part (host: d % (8 * world) == 0)
+  if constexpr (TS) {
+    // reduce-scatter: this rank's part [rank * cs, (rank + 1) * cs) of the row, in place
+    for (int i = tid * 8; i < cs; i += 256 * 8) {
+      const int idx = rank * cs + i;
+      float acc[8];
+      sum_ranks8(p, world, half, (row + idx) >> 3, acc);
+      *reinterpret_cast<uint4*>(mine + idx) = pack8(acc);
+    }
+    car_exchange<true>(p, rank, world, m, e, spin_limit);
+  }
   float v[NC][8];
   float ss = 0.f;
 #pragma unroll
@@ -230,7 +246,10 @@ __global__ __launch_bounds__(256) void car_fused_tail_kernel(const float* __rest
     const int idx = (c * 256 + tid) * 8;
     if (idx < d) {
       float acc[8], r[8];
-      sum_ranks8(p, world, half, (row + idx) >> 3, acc);
+      if constexpr (TS)  // all-gather: the owner's reduced (bf16) part
+        unpack8(*reinterpret_cast<const uint4*>(p.buf[idx / cs] + half + row + idx), acc);
+      else
+        sum_ranks8(p, world, half, (row + idx) >> 3, acc);
       unpack8(*reinterpret_cast<const uint4*>(residual + row + idx), r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -397,22 +416,33 @@ extern "C" int k8sllm_car_all_to_all(void* state, const void* in, void* out, lon
 // Fused TP row-parallel tail (see car_fused_tail_kernel): slabs [ns][M][d] fp32 (slab_stride
 // elements apart), residual [M][d] bf16 updated in place, w [d], out [M][ldo] row-major or
 // fragment-packed (packed != 0; ldo ignored).  M <= CAR_MAX_WG, d % 8 == 0, d <= 8192.
+// algo: 0 one-shot, 1 two-shot (needs d % (8 world) == 0), -1 auto: two-shot from 512 KiB at
+// world > 2 (the plain all-reduce's rule).
 extern "C" int k8sllm_car_fused_tail(void* state, const float* slabs, int ns, long slab_stride, void* residual,
                                      const void* w, void* out, long ldo, int M, int d, float eps, int packed,
-                                     long spin_limit, hipStream_t s) {
+                                     long spin_limit, int algo, hipStream_t s) {
   auto* st = (CarState*)state;
   if (M <= 0) return 0;
   if (M > CAR_MAX_WG || d % 8 || d > 8192 || ns < 1 || (packed && d % 32)) return -1;
   if (int rc = car_check(st, (long)M * d)) return rc;
+  const bool ts_ok = d % (8 * st->world) == 0;
+  if (algo == 1 && !ts_ok) return -1;
+  const bool ts = algo == 1 || (algo < 0 && ts_ok && st->world > 2 && (long)M * d * 2 >= (512L << 10));
   const int nc = (d + 2047) / 2048;
-#define K8_TAIL(NC_, PK_)                                                                                          \
-  hipLaunchKernelGGL((car_fused_tail_kernel<NC_, PK_>), dim3(M), dim3(256), 0, s, slabs, ns, slab_stride,        \
+#define K8_TAIL(NC_, PK_, TS_)                                                                                     \
+  hipLaunchKernelGGL((car_fused_tail_kernel<NC_, PK_, TS_>), dim3(M), dim3(256), 0, s, slabs, ns, slab_stride,   \
                      (bf16_t*)residual, (const bf16_t*)w, (bf16_t*)out, ldo, d, eps, st->max_elems, st->rank,    \
                      st->world, st->peers, spin_limit)
-  if (packed) {
-    if (nc <= 2) K8_TAIL(2, true); else K8_TAIL(4, true);
+  if (ts) {
+    if (packed) {
+      if (nc <= 2) K8_TAIL(2, true, true); else K8_TAIL(4, true, true);
+    } else {
+      if (nc <= 2) K8_TAIL(2, false, true); else K8_TAIL(4, false, true);
+    }
+  } else if (packed) {
+    if (nc <= 2) K8_TAIL(2, true, false); else K8_TAIL(4, true, false);
   } else {
-    if (nc <= 2) K8_TAIL(2, false); else K8_TAIL(4, false);
+    if (nc <= 2) K8_TAIL(2, false, false); else K8_TAIL(4, false, false);
   }
 #undef K8_TAIL
   return (int)hipGetLastError();

@@ -94,11 +94,14 @@ class CustomAllReduce:
         return 0 < M <= 256 and d % 32 == 0 and d <= 8192 and M * d <= self.max_elems
 
     def fused_tail(self, slabs: torch.Tensor, nslabs: int, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
-                   out: torch.Tensor, packed: bool) -> torch.Tensor:
+                   out: torch.Tensor, packed: bool, algo: int = -1) -> torch.Tensor:
         """The TP row-parallel tail of a decode layer in ONE launch: this rank's split-K slabs
         [nslabs, M, d] summed, all-reduced over the group, ``residual += `` the result, RMSNorm * w
-        written to ``out`` (row-major, or fragment-packed for the next skinny GEMM)."""
-        self._n.car_fused_tail(self.state, slabs, nslabs, residual, norm_w, out, eps, packed, self.spin_limit)
+        written to ``out`` (row-major, or fragment-packed for the next skinny GEMM).  ``algo``: 0
+        one-shot, 1 two-shot (each rank reduces 1/world of the columns, then gathers the rest:
+        2 (W - 1) / W rows over the links instead of W - 1), -1 auto (two-shot from 512 KiB at
+        TP > 2, e.g. Llama-3-70B TP=8 decode: 64 x 8192); both give bit-identical results."""
+        self._n.car_fused_tail(self.state, slabs, nslabs, residual, norm_w, out, eps, packed, self.spin_limit, algo)
         return out
 
     def error(self) -> bool:

@@ -123,18 +123,25 @@ def _rank_main(rank: int, world: int, port: int, q) -> None:
             y = ref_sum(part.reshape(-1)).reshape(M, d).float()
             r2 = (res.float() + y).bfloat16().float()
             ref_out = (r2 * torch.rsqrt(r2.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()).bfloat16()
-            rg = res.cuda()
-            out = ops.packed_empty(M, d, torch.bfloat16, "cuda") if packed else torch.empty(M, d, dtype=torch.bfloat16,
-                                                                                             device="cuda")
-            car.fused_tail(slabs.cuda().contiguous(), ns, rg, w.cuda(), 1e-5, out, packed)
-            got = out.cpu()
-            if packed:
-                got = ops.unpack_skinny(got.view(-1, d // 32, 64, 8))[:M]
-            if not torch.equal(rg.cpu(), r2.bfloat16()):
-                bad.append(("tail-residual", M, d))
-            err = (got.float() - ref_out.float()).abs().max().item()
-            if err > 2e-2 * ref_out.float().abs().max().item():
-                bad.append(("tail-out", M, d, packed, err))
+            outs = []
+            # one-shot and two-shot (each rank reduces 1/world of the columns, then gathers) must
+            # agree bit for bit; two-shot needs d % (8 * world) == 0
+            for algo in ((0, 1) if d % (8 * world) == 0 else (0,)):
+                rg = res.cuda()
+                out = (ops.packed_empty(M, d, torch.bfloat16, "cuda") if packed
+                       else torch.empty(M, d, dtype=torch.bfloat16, device="cuda"))
+                car.fused_tail(slabs.cuda().contiguous(), ns, rg, w.cuda(), 1e-5, out, packed, algo=algo)
+                got = out.cpu()
+                if packed:
+                    got = ops.unpack_skinny(got.view(-1, d // 32, 64, 8))[:M]
+                if not torch.equal(rg.cpu(), r2.bfloat16()):
+                    bad.append(("tail-residual", algo, M, d))
+                err = (got.float() - ref_out.float()).abs().max().item()
+                if err > 2e-2 * ref_out.float().abs().max().item():
+                    bad.append(("tail-out", algo, M, d, packed, err))
+                outs.append(got)
+            if len(outs) == 2 and not torch.equal(outs[0], outs[1]):
+                bad.append(("tail two-shot != one-shot", M, d, packed))
         # hipGraph: three captured calls per replay, fresh inputs every replay
         n = 64 * 4096
         sin = torch.empty(n, dtype=torch.bfloat16, device="cuda")
