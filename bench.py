@@ -351,7 +351,7 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic cluster-state prompts (reference prepareLLMContext format), random-init weights",
-        "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": seq_max, "max_model_len": 8192,
+        "config": {"model": a.model, "global_batch": a.batch * dp, "seq_len": seq_max, "max_model_len": eng.runner.max_len,
                    "parallelism": par,
                    "prompt_tokens_mean": round(total_p / max(1.0, total_ans), 1),
                    "max_new_tokens": a.max_new_tokens, "path": a.path, "mode": a.mode,

@@ -57,6 +57,15 @@ class LocalEngineBackend:
         self.timeout_s = timeout_s
         self.answer_budget_s = answer_budget_s if answer_budget_s is not None else (timeout_s if timeout_s > 0 else None)
         self.tokenizer = service.engine.tokenizer
+        eng = service.engine
+        mml = getattr(getattr(eng, "cfg", None), "max_model_len", None) or (1 << 30)
+        self.max_len = min(int(mml), int(eng.model_cfg.max_position))  # the engine's per-sequence cap
+
+    def max_prompt_tokens(self, max_tokens: Optional[int] = None) -> int:
+        """Prompt tokens that still leave room for ``max_tokens`` answer tokens (preamble included);
+        the answer's reservation is capped at half the window (llm.max_tokens 2000 against a
+        1024-token GPT-2 would otherwise leave no room for the cluster context)."""
+        return self.max_len - 1 - min(max_tokens or self.default.max_tokens, self.max_len // 2)
 
     def count_tokens(self, text: str) -> int:
         return len(self.tokenizer.encode(text, bos=False))
@@ -296,6 +305,21 @@ class AnalysisService:
             self._ctx_cache = (key, ctx)
         return ctx
 
+    def _fit(self, ctx: str, frame: str, max_tokens: Optional[int]) -> str:
+        """Trim the cluster context so that the whole prompt (``frame`` = the prompt without the
+        context) plus ``max_tokens`` answer tokens fit the model's window: a 1024-token GPT-2 would
+        otherwise get its prompt cut in the middle by the engine and room for one answer token.
+        Cheap when nothing can overflow: a byte-level BPE token covers >= 1 byte, so a prompt of
+        fewer bytes than the budget is never tokenized here."""
+        limit = getattr(self.backend, "max_prompt_tokens", None)
+        if limit is None:
+            return ctx
+        budget = limit(max_tokens or self.max_tokens) - len(P.SYSTEM_PREAMBLE.encode())
+        if len(ctx.encode()) + len(frame.encode()) <= budget:
+            return ctx
+        budget -= self.backend.count_tokens(frame) + 8
+        return P.trim_to_budget(ctx, lambda t: [0] * self.backend.count_tokens(t), max(budget, 16))
+
     # ------------------------------------------------------------------ entry points
     def _respond(self, rid: str, kind: str, prompt: str, extra: dict, max_tokens: Optional[int] = None,
                  ignore_eos: bool = False) -> AnalysisResponse:
@@ -322,9 +346,10 @@ class AnalysisService:
         AnalysisResponse.  Backends without token streaming yield the whole answer as one delta."""
         rid = uuid.uuid4().hex
         ctx = context_text if context_text else self.cluster_context()
+        mt = max_tokens or self.max_tokens
+        ctx = self._fit(ctx, P.build_query_prompt("", question), mt)
         prompt = P.build_query_prompt(ctx, question)
         extra = {"question": question}
-        mt = max_tokens or self.max_tokens
         try:
             if hasattr(self.backend, "stream"):
                 g = None
@@ -351,6 +376,7 @@ class AnalysisService:
         lets a caller supply the cluster state itself (e.g. another collector's snapshot)."""
         rid = uuid.uuid4().hex
         ctx = context_text if context_text else self.cluster_context()
+        ctx = self._fit(ctx, P.build_query_prompt("", question), max_tokens)
         prompt = P.build_query_prompt(ctx, question)
         return self._respond(rid, "query", prompt, {"question": question}, max_tokens, ignore_eos)
 
@@ -365,9 +391,10 @@ class AnalysisService:
             return self.explain_pod_communication(analysis)
         if kind not in ("anomaly_detection", "root_cause"):
             raise ValueError(f"unknown analysis type: {kind}")
-        prompt = P.build_analysis_prompt(kind, self.cluster_context(), params)
-        return self._respond(uuid.uuid4().hex, kind, prompt, {"parameters": params},
-                             int(params.get("max_tokens") or 0) or None)
+        mt = int(params.get("max_tokens") or 0) or None
+        ctx = self._fit(self.cluster_context(), P.build_analysis_prompt(kind, "", params), mt)
+        prompt = P.build_analysis_prompt(kind, ctx, params)
+        return self._respond(uuid.uuid4().hex, kind, prompt, {"parameters": params}, mt)
 
     def explain_pod_communication(self, analysis, max_tokens: Optional[int] = None,
                                   ignore_eos: bool = False) -> AnalysisResponse:

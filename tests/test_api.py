@@ -236,3 +236,27 @@ def test_chat_completions_endpoint(mon):
     d = J(a.handle("POST", "/v1/chat/completions", body))
     assert d["object"] == "chat.completion" and d["choices"][0]["message"]["role"] == "assistant"
     assert "NotReady" in d["choices"][0]["message"]["content"] and d["usage"]["completion_tokens"] > 0
+
+
+def test_context_fits_a_short_model_window():
+    """A 1024-token model (GPT-2) with a long cluster context: the service trims the context so the
+    prompt leaves room for the requested answer, instead of the engine cutting the prompt's middle
+    and leaving room for one token (BASELINE config 1)."""
+    from k8s_llm_monitor_amd.engine import EngineConfig, EngineService, LLMEngine
+    from k8s_llm_monitor_amd.llm.service import AnalysisService, LocalEngineBackend
+
+    eng = LLMEngine(EngineConfig(model="gpt2-tiny", max_num_seqs=2, max_model_len=512, num_blocks=64, seed=1),
+                    device="cpu")
+    svc = EngineService(eng)
+    try:
+        be = LocalEngineBackend(svc, max_tokens=32, temperature=0.0, timeout_s=60.0)
+        assert be.max_len == 512
+        an = AnalysisService(be, max_tokens=32)
+        ctx = "\n".join(f"- node-{i:03d} CPU={i % 97}% MEM={i % 89}% pods={i % 31}" for i in range(400))
+        assert be.count_tokens(ctx) > 512
+        r = an.query("哪个节点最忙?", max_tokens=32, ignore_eos=True, context_text=ctx)
+        assert r.status == "success", r.error
+        assert r.result["completion_tokens"] == 32 and r.result["finish_reason"] == "length"
+        assert r.result["prompt_tokens"] + 32 <= 512
+    finally:
+        svc.close()
