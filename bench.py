@@ -75,8 +75,10 @@ def parse(argv=None):
                     help="process: the HTTP clients run in a child load-generator process (remote clients; the "
                          "serving process keeps its interpreter lock); thread: client threads in this process")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--decode-fusion", choices=["none", "seam", "rc"], default="none",
-                    help="A/B runs of the shelved decode-step fusions (CausalLM.set_decode_fusion)")
+    ap.add_argument("--decode-fusion", choices=["auto", "none", "seam", "rc"], default="auto",
+                    help="A/B runs of the decode-step fusions (CausalLM.set_decode_fusion): auto = the "
+                         "default (row-complete o only for the smallest buckets), none = off, seam / rc = "
+                         "that fusion in every bucket")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
@@ -196,7 +198,7 @@ def run_rank(a) -> None:
                                  chunked_prefill=bool(a.chunked_prefill), tp_size=a.tp,
                                  kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
                                  seed=a.seed + ps.dp_rank, **admit), pstate=ps)
-    if a.decode_fusion != "none":
+    if a.decode_fusion != "auto":
         eng.model.set_decode_fusion(seam=a.decode_fusion == "seam", rc=a.decode_fusion == "rc")
     eng.warmup()
     devices = [str(ps.device)] * world

@@ -700,7 +700,7 @@ class CausalLM:
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         self.lm_head_d = None
-        self._fuse_norm, self._seam, self._rc_o = False, None, False
+        self._fuse_norm, self._seam, self._rc_o = False, None, 0
         for L in self.layers:  # (re)built below from the current weights
             for key in ("wqkv_d", "wo_d", "w13_d", "w2_d", "w13_dg", "w2_dg"):
                 L.pop(key, None)
@@ -754,9 +754,15 @@ class CausalLM:
         # MoE: the EP all-to-all decode runs up to 128 received rows per grouped launch
         rows = ops.SKINNY_GROUPED_MAX_M if c.is_moe else ops.SKINNY_MAX_M
         self._skinny_ws = torch.empty(n * rows, dtype=torch.float32, device=self.device)
-        self.set_decode_fusion(seam=False, rc=False)
+        self.set_decode_fusion()
 
-    def set_decode_fusion(self, seam: bool = False, rc: bool = False) -> None:
+    # decode buckets up to this many rows take the row-complete o projection by default: per decode
+    # step 1.4 % faster at 1-2 rows, 0.9 % at 4-16, 0.4 % at 32 (profiles/r05/rc_rows_ab.jsonl;
+    # batch-1 TPOT 3.14 vs 3.18 ms, latency_b1_rc_ab.md); at 64 rows its per-workgroup re-read of
+    # the attention output cancels the gain (neutral)
+    RC_O_MAX_ROWS = 32
+
+    def set_decode_fusion(self, seam: bool = False, rc=None) -> None:
         """Two measured-and-shelved alternatives to the decode step's add_norm_partial launches
         (profiles/r05/README.md; both bit-compatible with the default path, both off by default):
 
@@ -766,7 +772,10 @@ class CausalLM:
           it replaces did;
         * ``rc`` - the o projection row-complete, residual add and the gate_up GEMM's norm operands
           in its epilogue, no split-K slabs (ops.dec_gemm_rc): neutral - re-reading the attention
-          output from L2 in every workgroup costs what the slab round trip did.
+          output from L2 in every workgroup costs what the slab round trip did at 64 rows; at batch 1
+          that re-read is 8 KB per workgroup and rc wins 1.3% per token, so ``rc=None`` (the
+          default) turns it on for decode buckets of at most RC_O_MAX_ROWS rows (the hipGraphs are
+          captured per bucket, so the choice is static per graph); True: every bucket; False: off.
 
         Both need TP=1, the decode weight copies and a GPU not shared by several rank processes
         (the seam's workgroups must be resident together)."""
@@ -775,7 +784,8 @@ class CausalLM:
               and c.d_model % 512 == 0)
         self._fuse_norm = bool(seam) and ok and not os.environ.get("K8SLLM_DEVICE")
         self._seam = ops.SeamState(self.device) if self._fuse_norm else None
-        self._rc_o = bool(rc) and ok and "wo_d" in self.layers[0]
+        rows = self.RC_O_MAX_ROWS if rc is None else (1 << 30 if rc is True else int(rc))
+        self._rc_o = rows if ok and "wo_d" in self.layers[0] else 0
 
     def _decode_layers_skinny(self, x: torch.Tensor, residual: torch.Tensor, meta: AttnMeta,
                               kv_caches: Optional[list], first: Optional[tuple] = None) -> torch.Tensor:
@@ -794,7 +804,7 @@ class CausalLM:
             op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn, fused=pend)
             pend = None
             rc = None
-            if self._rc_o and "w13_d" in L:
+            if M <= self._rc_o and "w13_d" in L:
                 # o projection row-complete: residual += o and the gate_up GEMM's normed input in
                 # the same launch (no split-K slabs, no add_norm launch)
                 rc = ops.dec_gemm_rc(op, L["wo_d"], M, residual, L["mlp_norm"], eps)

@@ -14,14 +14,25 @@ def _run(seam: bool, rc: bool) -> list:
     eng = LLMEngine(EngineConfig(model="llama-tiny-d128", max_num_seqs=4, max_model_len=256, num_blocks=64,
                                  use_graphs=False, seed=3, dtype="float32"), device="cpu")
     eng.model.set_decode_fusion(seam=seam, rc=rc)
-    assert eng.model._rc_o == rc and eng.model._fuse_norm == seam
+    assert bool(eng.model._rc_o) == (rc is None or bool(rc)) and eng.model._fuse_norm == seam
     assert eng.model._skinny_ws is not None  # the decode steps take the fused-tail (skinny) path
     sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     seqs = eng.generate(["node-003 NotReady: kubelet stopped posting status", "pod default/api CrashLoopBackOff"], sp)
     return [s.output_ids for s in seqs]
 
 
-@pytest.mark.parametrize("seam,rc", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("seam,rc", [(True, False), (False, True), (True, True), (False, None), (False, 2)])
 def test_decode_fusions_match_default(seam, rc):
     torch.manual_seed(0)
     assert _run(seam, rc) == _run(False, False)
+
+
+def test_rc_auto_only_small_buckets():
+    eng = LLMEngine(EngineConfig(model="llama-tiny-d128", max_num_seqs=4, max_model_len=256, num_blocks=64,
+                                 use_graphs=False, seed=3, dtype="float32"), device="cpu")
+    m = eng.model
+    assert m._rc_o == m.RC_O_MAX_ROWS  # the default: the smallest buckets only
+    m.set_decode_fusion(rc=False)
+    assert m._rc_o == 0
+    m.set_decode_fusion(rc=True)
+    assert m._rc_o >= 1 << 20

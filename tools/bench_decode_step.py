@@ -6,7 +6,7 @@ graphs re-captured between phases.
 
     python tools/bench_decode_step.py --switch seam [--rounds 3 --tokens 96]
 
-Switches: ``seam`` / ``rc`` - the shelved decode fusions (CausalLM.set_decode_fusion).  (Round 5
+Switches: ``seam`` / ``rc`` - the decode fusions, on in every bucket vs off (CausalLM.set_decode_fusion).  (Round 5
 also A/B'd write-through (sc1) epilogue stores in gemm_decode.hip with this tool: 6.107 vs 6.068
 ms per step, slower - profiles/r05/decode_step_writethrough_ab.jsonl.)
 """
@@ -22,7 +22,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=False),
+SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=None if on is None else False),
+            "seam_auto_rc": lambda m, on: m.set_decode_fusion(seam=bool(on)),
             "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on)}
 
 
@@ -30,38 +31,40 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--switch", default="seam", choices=sorted(SWITCHES))
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--rows", type=int, default=64)
+    ap.add_argument("--rows", default="64", help="decode batch; a comma list runs each in turn")
     ap.add_argument("--ctx", type=int, default=1700)
     ap.add_argument("--tokens", type=int, default=96)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     from k8s_llm_monitor_amd.engine import EngineConfig, LLMEngine, SamplingParams
 
-    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.rows, max_model_len=4096, kv_cache_gb=48.0, seed=1),
-                    device="cuda")
+    rows_list = [int(r) for r in a.rows.split(",")]
+    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=max(rows_list), max_model_len=4096, kv_cache_gb=48.0,
+                                 seed=1), device="cuda")
     eng.warmup()
     g = torch.Generator().manual_seed(5)
-    prompts = [torch.randint(100, 120000, (a.ctx + (i * 37) % 200,), generator=g).tolist() for i in range(a.rows)]
     sp = SamplingParams(max_tokens=a.tokens, temperature=0.0, ignore_eos=True)
     set_sw = SWITCHES[a.switch]
-    res: dict = {True: [], False: []}
-    for rnd in range(a.rounds):
-        for on in (True, False):
-            set_sw(eng.model, on)
-            eng.runner.graphs.clear()
-            eng.runner.capture_graphs()
-            eng.step_samples.clear()
-            eng.generate(prompts, sp)
-            ms = [m for (n, m, _) in eng.step_samples if n == a.rows]
-            med = statistics.median(ms) if ms else float("nan")
-            res[on].append(med)
-            print(json.dumps({"switch": a.switch, "on": on, "round": rnd, "steps": len(ms),
-                              "median_step_ms": round(med, 4)}), flush=True)
-    set_sw(eng.model, False)
-    print(json.dumps({"switch": a.switch, "on_ms": [round(x, 4) for x in res[True]],
-                      "off_ms": [round(x, 4) for x in res[False]],
-                      "on_median": round(statistics.median(res[True]), 4),
-                      "off_median": round(statistics.median(res[False]), 4)}), flush=True)
+    for rows in rows_list:
+        prompts = [torch.randint(100, 120000, (a.ctx + (i * 37) % 200,), generator=g).tolist() for i in range(rows)]
+        res: dict = {True: [], False: []}
+        for rnd in range(a.rounds):
+            for on in (True, False):
+                set_sw(eng.model, on)
+                eng.runner.graphs.clear()
+                eng.runner.capture_graphs()
+                eng.step_samples.clear()
+                eng.generate(prompts, sp)
+                ms = [m for (n, m, _) in eng.step_samples if n == rows]
+                med = statistics.median(ms) if ms else float("nan")
+                res[on].append(med)
+                print(json.dumps({"switch": a.switch, "rows": rows, "on": on, "round": rnd, "steps": len(ms),
+                                  "median_step_ms": round(med, 4)}), flush=True)
+        print(json.dumps({"switch": a.switch, "rows": rows, "on_ms": [round(x, 4) for x in res[True]],
+                          "off_ms": [round(x, 4) for x in res[False]],
+                          "on_median": round(statistics.median(res[True]), 4),
+                          "off_median": round(statistics.median(res[False]), 4)}), flush=True)
+    set_sw(eng.model, None)
 
 
 if __name__ == "__main__":
