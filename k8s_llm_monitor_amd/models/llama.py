@@ -763,8 +763,8 @@ class CausalLM:
     RC_O_MAX_ROWS = 32
 
     def set_decode_fusion(self, seam: bool = False, rc=None) -> None:
-        """Two measured-and-shelved alternatives to the decode step's add_norm_partial launches
-        (profiles/r05/README.md; both bit-compatible with the default path, both off by default):
+        """Two alternatives to the decode step's add_norm_partial launches (profiles/r05/README.md;
+        both bit-compatible with the slab path; the seam is off by default, rc on for small buckets):
 
         * ``seam`` - the add-RMSNorm runs as the first phase of the consuming GEMM (gate_up, the
           next layer's qkv) behind an in-launch grid seam (ops.dec_gemm_fused_norm): neutral - the
@@ -772,8 +772,8 @@ class CausalLM:
           it replaces did;
         * ``rc`` - the o projection row-complete, residual add and the gate_up GEMM's norm operands
           in its epilogue, no split-K slabs (ops.dec_gemm_rc): neutral - re-reading the attention
-          output from L2 in every workgroup costs what the slab round trip did at 64 rows; at batch 1
-          that re-read is 8 KB per workgroup and rc wins 1.3% per token, so ``rc=None`` (the
+          output from L2 in every workgroup costs what the slab round trip did at 64 rows; at 1-32
+          rows that re-read is small and rc wins 0.4-1.4 % per step, so ``rc=None`` (the
           default) turns it on for decode buckets of at most RC_O_MAX_ROWS rows (the hipGraphs are
           captured per bucket, so the choice is static per graph); True: every bucket; False: off.
 

@@ -1,4 +1,4 @@
-"""The shelved decode-step fusions (CausalLM.set_decode_fusion: the add-RMSNorm inside the
+"""The decode-step fusions (CausalLM.set_decode_fusion: the add-RMSNorm inside the
 consuming GEMM behind a grid seam, and the row-complete o projection) are drop-in replacements for
 add_norm_partial: on the CPU (their fp32 reference forms, the same control flow the GPU takes)
 an engine generates the same greedy tokens with each of them as with the default path.  The
