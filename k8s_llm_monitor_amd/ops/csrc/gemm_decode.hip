@@ -114,7 +114,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave, filled after chunk 0's
   // staging loads (below).  (With NP, filling it before the norm phase - the weights do not depend
   // on it - measured SLOWER: gate_up 49.9 vs 45.7 us, the ring's HBM loads queue ahead of the
-  // L2-resident slab loads the norm phase waits for; profiles/r05/README.md.)
+  // L2-resident slab loads the norm phase waits for; and filling it after the norm phase, beside
+  // the seam wait, too: 6.19 vs 6.01 ms per 64-row decode step - the early workgroups' ring loads
+  // slow the late ones' norm phase, which the seam waits for; profiles/r05/README.md.)
   const u32x4* wp[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
