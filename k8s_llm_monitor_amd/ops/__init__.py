@@ -748,11 +748,18 @@ def decode_splits(batch: int, Hkv: int, n_cu: int = 256) -> int:
     return max(1, min(32, round(n_cu / max(1, batch * Hkv))))
 
 
+# split partials of paged_decode_fused merged inside the attention launch by the last-arriving
+# split (no paged_decode_reduce launch); the decode workspace carries the hand-off counters
+DECODE_MERGE = True
+
+
 def decode_workspace(max_batch: int, Hq: int, D: int, max_model_len: int = 0, device=None, Hkv: Optional[int] = None):
-    """fp32 partials of the split-K decode kernel: [B, Hq, MAX_SPLITS, D] and [.., 2]."""
+    """fp32 partials of the split-K decode kernel: [B, Hq, MAX_SPLITS, D] and [.., 2], plus the
+    in-launch merge's (sequence, kv head) counters (int32, zero; each launch leaves them zero)."""
     part_out = torch.empty(max_batch, Hq, MAX_SPLITS, D, dtype=torch.float32, device=device)
     part_ml = torch.empty(max_batch, Hq, MAX_SPLITS, 2, dtype=torch.float32, device=device)
-    return part_out, part_ml
+    ctr = torch.zeros(max_batch * Hq, dtype=torch.int32, device=device)
+    return part_out, part_ml, ctr
 
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
@@ -795,10 +802,11 @@ def paged_decode_fused(slabs: torch.Tensor, nslabs: int, positions: torch.Tensor
     if out is None:
         out = torch.empty(B, Hq * D, dtype=k_cache.dtype, device=slabs.device)
     S = splits or decode_splits(B, Hkv)
+    merge = workspace[2] if DECODE_MERGE and len(workspace) > 2 else _empty_i32(slabs.device)
     native().paged_decode_fused(out, slabs, nslabs, positions, cos_sin,
                                 slot_mapping if slot_mapping is not None else _empty_i32(slabs.device),
                                 k_cache, v_cache, block_tables, seq_lens, workspace[0], workspace[1], Hq, Hkv, D,
-                                scale, S)
+                                scale, S, merge)
     return out
 
 

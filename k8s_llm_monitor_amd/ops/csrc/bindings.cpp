@@ -24,7 +24,8 @@ int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part
 int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml, const float* slabs,
                               int nslabs, const int* positions, const float* cos_sin, const int* slot_mapping,
                               void* k_cache, void* v_cache, const int* block_tables, int bt_stride,
-                              const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
+                              const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, int* merge_ctr,
+                              hipStream_t s);
 int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride, const int* cu_seqlens,
                          const int* qb_seq, const int* qb_start, int n_qblocks, int Hq, int Hkv, int D, float scale,
                          const int* ctx_start, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -229,7 +230,7 @@ void paged_decode_fused(torch::Tensor out, torch::Tensor slabs, int64_t nslabs, 
                         torch::Tensor cos_sin, torch::Tensor slot_mapping, torch::Tensor k_cache,
                         torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor seq_lens,
                         torch::Tensor part_out, torch::Tensor part_ml, int64_t Hq, int64_t Hkv, int64_t D,
-                        double scale, int64_t splits) {
+                        double scale, int64_t splits, torch::Tensor merge_ctr) {
   dev_bf16(out, "out"); dev_bf16(k_cache, "k_cache"); dev_bf16(v_cache, "v_cache");
   dev_i32(block_tables, "block_tables"); dev_i32(seq_lens, "seq_lens"); dev_i32(positions, "positions");
   TORCH_CHECK(D == 128, "paged_decode_fused: head_dim 128");
@@ -257,13 +258,19 @@ void paged_decode_fused(torch::Tensor out, torch::Tensor slabs, int64_t nslabs, 
   TORCH_CHECK(splits >= 1 && splits <= 64, "splits must be in [1, 64]");
   TORCH_CHECK(part_out.numel() >= (int64_t)B * Hq * splits * D && part_ml.numel() >= (int64_t)B * Hq * splits * 2,
               "decode workspace too small for batch x splits");
+  // merge_ctr (numel > 0): B x Hkv int32 counters, zero between launches (the kernel resets them)
+  const bool merge = merge_ctr.numel() > 0;
+  if (merge) {
+    dev_i32(merge_ctr, "merge_ctr");
+    TORCH_CHECK(merge_ctr.numel() >= (int64_t)B * Hkv, "paged_decode_fused: merge_ctr must hold B x Hkv counters");
+  }
   check(k8sllm_paged_decode_fused(out.data_ptr(), packed ? -(long)(Hq * D / 32) : (long)out.stride(0),
                                   part_out.data_ptr<float>(), part_ml.data_ptr<float>(), slabs.data_ptr<float>(),
                                   (int)nslabs, positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
                                   has_slots ? slot_mapping.data_ptr<int>() : nullptr, k_cache.data_ptr(),
                                   v_cache.data_ptr(), block_tables.data_ptr<int>(), (int)block_tables.stride(0),
                                   seq_lens.data_ptr<int>(), B, (int)Hq, (int)Hkv, (int)D, (int)splits, (float)scale,
-                                  cur()),
+                                  merge ? merge_ctr.data_ptr<int>() : nullptr, cur()),
         "paged_decode_fused");
 }
 

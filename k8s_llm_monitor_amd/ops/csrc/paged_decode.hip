@@ -21,9 +21,12 @@
 //    before the first MFMA (block ids past the sequence end are clamped to a valid block and
 //    masked), i.e. 32 KiB in flight per wave.
 //  * if a sequence's chunks fit one split, that workgroup writes the normalised output;
-//    otherwise each split writes (max, sum, O) partials that paged_decode_reduce_kernel merges
-//    in a second launch (an in-kernel last-arriver merge with agent release/acquire fences
-//    measured 2.3x slower at batch 64 x 1.8k context: every workgroup paid the L2 write-back).
+//    otherwise each split writes (max, sum, O) partials that are merged either by the LAST
+//    arriving split of the (sequence, kv head) inside this launch (MERGE: partials stored
+//    write-through, one agent-scope counter per (sequence, kv head) - the hand-off protocol of the
+//    decode GEMM's grid seam, no L2 write-back) or by paged_decode_reduce_kernel in a second
+//    launch.  (An earlier in-kernel merge with agent release/acquire FENCES measured 2.3x slower at
+//    batch 64 x 1.8k context: every workgroup paid an L2 write-back.)
 // Everything is static-shaped so the decode step can be captured in a hipGraph.
 #include "common.h"
 #include <stdlib.h>
@@ -31,6 +34,14 @@
 namespace k8sllm {
 
 constexpr int kBS = 16;   // tokens per KV-cache block
+constexpr int kPdSC1 = 16;  // buffer-op aux bits: sc1 (write-through stores / L2-coherent loads)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pd_rsrc(const void* base, long bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)min(bytes, 0x7fffffffL));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
 
 // kch: tokens per chunk (4 waves x TW tokens)
 __device__ __forceinline__ void split_range(int seq_len, int S, int split, int kch, int* c0, int* c1, int* nvalid) {
@@ -62,7 +73,7 @@ struct DecodeFuse {
 // ~240 VGPRs: 2 waves per SIMD) for grids that fill the chip (batch 64: 512 workgroups);
 // TW = 64: one buffer of 64 tokens (~120 VGPRs: up to 4 workgroups per CU) for small, split
 // grids, where residency, not the per-wave pipeline, hides the memory latency.
-template <int D, int G, bool FQ, int TW>
+template <int D, int G, bool FQ, int TW, bool MERGE = false>
 __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf16_t* __restrict__ out, long out_stride,
                                                            float* __restrict__ part_out,  // [B][Hq][S][D]
                                                            float* __restrict__ part_ml,   // [B][Hq][S][2]
@@ -71,7 +82,8 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ seq_lens, int Hq, int Hkv, int S,
-                                                           float scale_log2, DecodeFuse fz) {
+                                                           float scale_log2, DecodeFuse fz,
+                                                           int* __restrict__ merge_ctr) {  // MERGE: [B][Hkv], zero between launches
   constexpr int KS = D / 32;  // QK k-steps
   constexpr int DT = D / 16;  // PV output tiles (16 dims each)
   __shared__ float s_max[4][16];
@@ -329,11 +341,72 @@ __global__ __launch_bounds__(256, TW == 32 ? 2 : 1) void paged_decode_kernel(bf1
       out[act_index(b, (kvh * G + h) * D + d, out_stride)] = f2bf(o / L);
     } else {
       const long ph = ((long)b * Hq + kvh * G + h) * S + split;
-      part_out[ph * D + d] = o;
-      if (d == 0) {
-        part_ml[ph * 2] = M;
-        part_ml[ph * 2 + 1] = L;
+      if constexpr (MERGE) {  // write-through: read by another workgroup of this launch
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), pd_rsrc(part_out, 0x7fffffffL),
+                                              (uint32_t)((ph * D + d) * 4), 0, kPdSC1);
+        if (d == 0) {
+          const __amdgpu_buffer_rsrc_t ml = pd_rsrc(part_ml, 0x7fffffffL);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), ml, (uint32_t)(ph * 8), 0, kPdSC1);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(L), ml, (uint32_t)(ph * 8 + 4), 0, kPdSC1);
+        }
+      } else {
+        part_out[ph * D + d] = o;
+        if (d == 0) {
+          part_ml[ph * 2] = M;
+          part_ml[ph * 2 + 1] = L;
+        }
       }
+    }
+  }
+  if constexpr (MERGE) {
+    if (nvalid == 1) return;  // uniform
+    // hand-off (the grid seam's protocol, gemm_decode.hip DecNorm): every wave drains its
+    // write-through stores, a barrier, ONE lane takes a ticket on the (sequence, kv head) counter;
+    // the split holding the last ticket resets the counter for the next launch and merges every
+    // split's partials with L2-coherent (sc1) loads
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (threadIdx.x == 0) {
+      int* c = merge_ctr + (long)b * gridDim.y + kvh;
+      const int t = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == nvalid - 1;
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const __amdgpu_buffer_rsrc_t po_rs = pd_rsrc(part_out, 0x7fffffffL), ml_rs = pd_rsrc(part_ml, 0x7fffffffL);
+    float* s_w = &s_o[0][0][0];  // [G][64] split weights (s_o is free now)
+    for (int h = wave; h < G; h += 4) {
+      const long ph = ((long)b * Hq + kvh * G + h) * S;
+      float mp = -1e30f, lp = 0.f;
+      if (lane < nvalid) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(ml_rs, (uint32_t)((ph + lane) * 8), 0, kPdSC1);
+        mp = __uint_as_float(x[0]);
+        lp = __uint_as_float(x[1]);
+      }
+      const float mm = wave_max(mp);
+      const float w = lane < nvalid ? exp2f(mp - mm) : 0.f;
+      const float lw = wave_sum(w * lp);
+      s_w[h * 64 + lane] = w / lw;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * D; i += 256) {
+      const int h = i / D, d = i - h * D;
+      const long base = (((long)b * Hq + kvh * G + h) * S * D + d) * 4;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int p = 0;
+      for (; p + 4 <= nvalid; p += 4) {  // the reduce kernel's summation order: bit-identical
+        a0 += s_w[h * 64 + p] * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(po_rs, (uint32_t)(base + (long)p * D * 4), 0, kPdSC1));
+        a1 += s_w[h * 64 + p + 1] * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(po_rs, (uint32_t)(base + (long)(p + 1) * D * 4), 0, kPdSC1));
+        a2 += s_w[h * 64 + p + 2] * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(po_rs, (uint32_t)(base + (long)(p + 2) * D * 4), 0, kPdSC1));
+        a3 += s_w[h * 64 + p + 3] * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(po_rs, (uint32_t)(base + (long)(p + 3) * D * 4), 0, kPdSC1));
+      }
+      for (; p < nvalid; ++p)
+        a0 += s_w[h * 64 + p] * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(po_rs, (uint32_t)(base + (long)p * D * 4), 0, kPdSC1));
+      out[act_index(b, (kvh * G + h) * D + d, out_stride)] = f2bf((a0 + a1) + (a2 + a3));
     }
   }
 }
@@ -394,7 +467,7 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
                                          const float* slabs, int nslabs, const int* positions, const float* cos_sin,
                                          const int* slot_mapping, void* k_cache, void* v_cache,
                                          const int* block_tables, int bt_stride, const int* seq_lens, int B, int Hq,
-                                         int Hkv, int D, int S, float scale, hipStream_t s);
+                                         int Hkv, int D, int S, float scale, int* merge_ctr, hipStream_t s);
 
 // Tokens per wave per chunk: the double-buffered 32-token form once the grid fills the chip
 // (>= 384 workgroups, e.g. batch 64 x 8 kv heads), else the single-buffered 64-token form (small
@@ -417,7 +490,7 @@ extern "C" int k8sllm_paged_decode(void* out, long out_stride, float* part_out, 
 #define K8S_DEC_T(DD, GG, TWV)                                                                                       \
   hipLaunchKernelGGL((paged_decode_kernel<DD, GG, false, TWV>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, \
                      part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,            \
-                     block_tables, bt_stride, seq_lens, Hq, Hkv, S, sl2, fz)
+                     block_tables, bt_stride, seq_lens, Hq, Hkv, S, sl2, fz, nullptr)
 #define K8S_DEC(DD, GG)                                                                                              \
   if (tw == 32) K8S_DEC_T(DD, GG, 32); else K8S_DEC_T(DD, GG, 64);                                                  \
   if (S > 1)                                                                                                         \
@@ -452,7 +525,7 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
                                          const float* slabs, int nslabs, const int* positions, const float* cos_sin,
                                          const int* slot_mapping, void* k_cache, void* v_cache,
                                          const int* block_tables, int bt_stride, const int* seq_lens, int B, int Hq,
-                                         int Hkv, int D, int S, float scale, hipStream_t s) {
+                                         int Hkv, int D, int S, float scale, int* merge_ctr, hipStream_t s) {
   if (B <= 0) return 0;
   if (S < 1 || S > 64) return -2;
   if (D != 128 || slabs == nullptr || nslabs < 1 || positions == nullptr || cos_sin == nullptr) return -3;
@@ -460,16 +533,22 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
   const float sl2 = scale * 1.4426950408889634f;
   const DecodeFuse fz{slabs, nslabs, positions, cos_sin, slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache};
   const int tw = decode_tw(S, Hkv, B);
+  // merge_ctr (B x Hkv ints, zero): split partials merged in-launch by the last arriving split
+  const bool merge = merge_ctr != nullptr && S > 1;
   dim3 grid(S, Hkv, B), blk(256);
-#define K8S_DECF_T(GG, TWV)                                                                                          \
-  hipLaunchKernelGGL((paged_decode_kernel<128, GG, true, TWV>), grid, blk, 0, s, (bf16_t*)out, out_stride, part_out, \
-                     part_ml, nullptr, 0, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride,   \
-                     seq_lens, Hq, Hkv, S, sl2, fz)
+#define K8S_DECF_T(GG, TWV, MG)                                                                                      \
+  hipLaunchKernelGGL((paged_decode_kernel<128, GG, true, TWV, MG>), grid, blk, 0, s, (bf16_t*)out, out_stride,       \
+                     part_out, part_ml, nullptr, 0, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,    \
+                     bt_stride, seq_lens, Hq, Hkv, S, sl2, fz, merge_ctr)
 #define K8S_DECF(GG)                                                                                                 \
-  if (tw == 32) K8S_DECF_T(GG, 32); else K8S_DECF_T(GG, 64);                                                        \
-  if (S > 1)                                                                                                         \
-    hipLaunchKernelGGL((paged_decode_reduce_kernel<128, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,     \
-                       part_out, part_ml, seq_lens, Hq, S, 4 * tw);
+  if (merge) {                                                                                                       \
+    if (tw == 32) K8S_DECF_T(GG, 32, true); else K8S_DECF_T(GG, 64, true);                                          \
+  } else {                                                                                                           \
+    if (tw == 32) K8S_DECF_T(GG, 32, false); else K8S_DECF_T(GG, 64, false);                                        \
+    if (S > 1)                                                                                                       \
+      hipLaunchKernelGGL((paged_decode_reduce_kernel<128, GG>), dim3(Hkv, B), blk, 0, s, (bf16_t*)out, out_stride,   \
+                         part_out, part_ml, seq_lens, Hq, S, 4 * tw);                                                \
+  }
   switch (G) {
     case 1: K8S_DECF(1); break;
     case 2: K8S_DECF(2); break;

@@ -157,6 +157,42 @@ def test_paged_decode_fused_matches_rope_then_decode(lens, hq, hkv, splits, nsla
     _close(y.cpu(), rr, atol=2e-2, rtol=2e-2, what="fused decode vs fp32 reference")
 
 
+def test_paged_decode_fused_in_launch_merge_bit_identical():
+    """The split partials merged by the last-arriving split inside the attention launch (write-
+    through partials, one agent-scope counter per (sequence, kv head)) == the separate
+    paged_decode_reduce launch, bit for bit - over back-to-back launches whose lengths change the
+    number of valid splits each time, leaving every counter at zero."""
+    d, bs, hq, hkv = 128, 16, 32, 8
+    B, nslabs = 4, 2
+    max_blocks = 2304 // bs + 1
+    nb = B * max_blocks + 4
+    kc, vc = _make_cache(nb, hkv, d, bs)
+    bt = torch.randperm(nb, device=DEV)[: B * max_blocks].view(B, max_blocks).to(torch.int32)
+    n = (hq + 2 * hkv) * d
+    cs = ref.rope_cos_sin(4096, d, 500000.0, None, device=DEV)
+    scale = 1.0 / math.sqrt(d)
+    ws = ops.decode_workspace(B, hq, d, device=DEV, Hkv=hkv)
+    ws_sep = (torch.empty_like(ws[0]), torch.empty_like(ws[1]))  # no counters: the two-launch path
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for it, lens in enumerate([[1800, 5, 300, 2300], [40, 1999, 1, 257], [2300, 2300, 2300, 2300], [0, 700, 64, 1100],
+                               [1800, 5, 300, 2300], [3, 4, 5, 6]]):
+        for splits in (None, 16, 64):
+            lens_t = torch.tensor(lens, dtype=torch.int32, device=DEV)
+            pos = (lens_t - 1).clamp(min=0)
+            slots = torch.stack([bt[b, max(lens[b] - 1, 0) // bs] * bs + max(lens[b] - 1, 0) % bs
+                                 for b in range(B)]).to(torch.int32)
+            slabs = (torch.randn(nslabs, B, n, generator=g) * 0.5).to(DEV)
+            kc2, vc2 = kc.clone(), vc.clone()
+            y = ops.paged_decode_fused(slabs.reshape(-1), nslabs, pos, cs, slots, kc, vc, bt, lens_t, hq, hkv, d,
+                                       scale, workspace=ws, splits=splits)
+            r = ops.paged_decode_fused(slabs.reshape(-1), nslabs, pos, cs, slots, kc2, vc2, bt, lens_t, hq, hkv, d,
+                                       scale, workspace=ws_sep, splits=splits)
+            torch.cuda.synchronize()
+            live = [b for b in range(B) if lens[b] > 0]
+            assert torch.equal(y[live], r[live]), f"launch {it} splits {splits}: merge != reduce launch"
+            assert int(ws[2].abs().sum()) == 0, f"launch {it}: counters not reset"
+
+
 @pytest.mark.parametrize("lens,hq,hkv", [([1], 32, 8), ([128], 32, 8), ([300, 77, 1024], 32, 8),
                                          ([513, 200], 64, 8), ([129, 64], 8, 8)])
 def test_flash_prefill(lens, hq, hkv):

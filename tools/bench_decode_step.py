@@ -6,7 +6,8 @@ graphs re-captured between phases.
 
     python tools/bench_decode_step.py --switch seam [--rounds 3 --tokens 96]
 
-Switches: ``seam`` / ``rc`` - the decode fusions, on in every bucket vs off (CausalLM.set_decode_fusion).  (Round 5
+Switches: ``seam`` / ``rc`` - the decode fusions, on in every bucket vs off; ``merge`` - the
+attention's split partials merged in-launch (ops.DECODE_MERGE) vs a paged_decode_reduce launch (CausalLM.set_decode_fusion).  (Round 5
 also A/B'd write-through (sc1) epilogue stores in gemm_decode.hip with this tool: 6.107 vs 6.068
 ms per step, slower - profiles/r05/decode_step_writethrough_ab.jsonl.)
 """
@@ -24,7 +25,13 @@ import torch  # noqa: E402
 
 SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=None if on is None else False),
             "seam_auto_rc": lambda m, on: m.set_decode_fusion(seam=bool(on)),
-            "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on)}
+            "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on),
+            "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False)}
+
+
+def _ops():
+    from k8s_llm_monitor_amd import ops
+    return ops
 
 
 def main() -> None:
