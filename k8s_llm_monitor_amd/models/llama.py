@@ -761,6 +761,11 @@ class CausalLM:
     # batch-1 TPOT 3.14 vs 3.18 ms, latency_b1_rc_ab.md); at 64 rows its per-workgroup re-read of
     # the attention output cancels the gain (neutral)
     RC_O_MAX_ROWS = 32
+    # the down projection row-complete as well (K = 14336: Llama-3-8B; residual add + the next
+    # qkv's operands in its epilogue): bit-identical, but measured neutral at 1 row and 0.2-4.5 %
+    # slower at 4-32 (its waves split K, so each re-reads its slice of the activations that the
+    # slab kernel stages once per workgroup; profiles/r05/rc_down_*_ab.jsonl) - off
+    RC_DOWN = False
 
     def set_decode_fusion(self, seam: bool = False, rc=None) -> None:
         """Two alternatives to the decode step's add_norm_partial launches (profiles/r05/README.md;
@@ -812,6 +817,14 @@ class CausalLM:
                 xw, rn = rc
                 act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
                 ops.dec_gemm(xw, L["w13_d"], 2, M, out=act, rownorm=rn)
+                if self.RC_DOWN and i + 1 < n and "w2_d" in L and "wqkv_d" in self.layers[i + 1]:
+                    # the down projection row-complete too: residual += down and the next layer's
+                    # qkv operands in its epilogue (no slabs, no add_norm launch); None where the
+                    # kernel does not tile the shape
+                    rc = ops.dec_gemm_rc(act, L["w2_d"], M, residual, self.layers[i + 1]["attn_norm"], eps)
+                    if rc is not None:
+                        xw, rn = rc
+                        continue
                 ns = self._proj_slabs(L, "w2", act, M, self._split_d)
                 if i + 1 < n:
                     if self._fuse_norm and "wqkv_d" in self.layers[i + 1]:

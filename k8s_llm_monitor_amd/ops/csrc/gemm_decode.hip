@@ -419,6 +419,7 @@ __global__ __launch_bounds__(512, 1) void gemm_dec_rc_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ xw, float* __restrict__ ss_out,
                                                              int M, int N, int K) {
   constexpr int WAVES = 8;
+  static_assert(NKS % DEPTH == 0, "the ring consumes whole DEPTH groups of k-steps");
   __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][MT][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tile = blockIdx.x;
@@ -566,7 +567,7 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     if (rc) return -6;
     return (int)hipGetLastError();
   }
-  if (rnw) {  // consumers of gemm_dec_rc's per-16-column partials: gate_up (the o projection's consumer)
+  if (rnw) {  // consumers of gemm_dec_rc's per-16-column partials: gate_up (behind o) and qkv (behind down)
 #define K8S_DEC_MW(NTWV, WV, EPV, DV) \
   switch (MT) {                       \
     case 1: K8S_DEC_NPW(1, NTWV, WV, EPV, DV, false, true); break; \
@@ -576,6 +577,9 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
   }
     if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 8) }
     else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 16) }
+    // the next layer's qkv behind a row-complete down projection
+    else if (epi == DEC_SLAB && ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_MW(1, 6, DEC_SLAB, 8) }
+    else if (epi == DEC_SLAB && ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_MW(1, 8, DEC_SLAB, 8) }
 #undef K8S_DEC_MW
     if (rc) return rc;
     return (int)hipGetLastError();
@@ -614,17 +618,26 @@ extern "C" int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, co
   if (M <= 0) return 0;
   if (M > 64 || N % 32 || K % 32 || (K / 32) % 8) return -1;
   const int nks = K / 32 / 8;
+  if (nks == 56 && M > 32) return -1;  // the down projection's form: buckets of <= 32 rows
   const int MT = (M + 15) / 16;
   const dim3 grid(N / 16), blk(512);
-#define K8S_RC(MTV, DV)                                                                                            \
-  hipLaunchKernelGGL((gemm_dec_rc_kernel<MTV, DV, 16>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp,    \
+#define K8S_RC(MTV, DV, NK)                                                                                        \
+  hipLaunchKernelGGL((gemm_dec_rc_kernel<MTV, DV, NK>), grid, blk, 0, s, (const bf16_t*)A, (const bf16_t*)Wp,    \
                      (bf16_t*)resid, (const bf16_t*)nw, (bf16_t*)xw, ss, M, N, K)
-  if (nks != 16) return -1;  // K = 4096 (the o projection of Llama-3-8B / Mixtral at TP=1)
-  switch (MT) {
-    case 1: K8S_RC(1, 8); break;
-    case 2: K8S_RC(2, 8); break;
-    case 3: K8S_RC(3, 8); break;
-    default: K8S_RC(4, 8); break;
+  if (nks == 16) {  // K = 4096: the o projection of Llama-3-8B / Mixtral at TP=1
+    switch (MT) {
+      case 1: K8S_RC(1, 8, 16); break;
+      case 2: K8S_RC(2, 8, 16); break;
+      case 3: K8S_RC(3, 8, 16); break;
+      default: K8S_RC(4, 8, 16); break;
+    }
+  } else if (nks == 56) {  // K = 14336: the down projection of Llama-3-8B (small decode buckets)
+    switch (MT) {
+      case 1: K8S_RC(1, 14, 56); break;
+      default: K8S_RC(2, 14, 56); break;
+    }
+  } else {
+    return -1;
   }
 #undef K8S_RC
   return (int)hipGetLastError();

@@ -259,3 +259,46 @@ def test_dec_rc_matches_slabs_and_norm(M):
     gu = xn @ w13.float().t()
     ref = F_.silu(gu[:, :F].to(torch.bfloat16).float()) * gu[:, F:].to(torch.bfloat16).float()
     _check(ops.unpack_skinny(a_rc)[:M], ref, f"rc gate_up vs fp32 M{M}")
+
+
+@pytest.mark.parametrize("M", [1, 9, 32])
+def test_dec_rc_down_matches_slabs_and_feeds_qkv(M):
+    """The row-complete form at K = 14336 (the down projection of Llama-3-8B in decode buckets of
+    <= 32 rows): the residual and the normed A operand BIT-identical to the 8-slab path +
+    add_norm_partial (same K slices, same order), and the next layer's qkv GEMM consuming the
+    wide (256-partial) row scale within rounding of the narrow form and of fp32."""
+    d, F, eps = 4096, 14336, 1e-5
+    nq = 6144
+    g = torch.Generator(device=DEV).manual_seed(100 + M)
+    act = torch.randn(M, F, device=DEV, generator=g).to(torch.bfloat16)
+    w2 = (torch.randn(d, F, device=DEV, generator=g) * 0.01).to(torch.bfloat16)
+    w2p = ops.pack_skinny(w2)
+    resid0 = torch.randn(M, d, device=DEV, generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(d, device=DEV, generator=g)).to(torch.bfloat16)
+    ap = ops.pack_activation(act)
+    for _ in range(3):
+        r_rc = resid0.clone()
+        out = ops.dec_gemm_rc(ap, w2p, M, r_rc, nw, eps)
+        assert out is not None, "K = 14336 row-complete form must be compiled"
+        xw_rc, (ss_rc, _) = out
+        ws = torch.empty(8 * M * d, device=DEV)
+        ns = ops.dec_gemm(ap, w2p, 0, M, workspace=ws, cfg=(8, 1, 8, 8))
+        r_sl = resid0.clone()
+        xw_sl, ss_sl = ops.add_norm_partial(r_sl, ws, ns, nw)
+        torch.cuda.synchronize()
+        assert torch.equal(r_rc, r_sl)
+        assert torch.equal(ops.unpack_skinny(xw_rc)[:M], ops.unpack_skinny(xw_sl)[:M])
+        torch.testing.assert_close(ss_rc.view(M, 8, 32).sum(-1), ss_sl, rtol=1e-4, atol=1e-3)
+    wq = (torch.randn(nq, d, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    wqp = ops.pack_skinny(wq)
+    cfg = ops.dec_config(nq, d, 0)
+    ws_rc = torch.empty(cfg[0] * M * nq, device=DEV)
+    ws_sl = torch.empty(cfg[0] * M * nq, device=DEV)
+    s1 = ops.dec_gemm(xw_rc, wqp, 0, M, workspace=ws_rc, rownorm=(ss_rc, eps))
+    s2 = ops.dec_gemm(xw_sl, wqp, 0, M, workspace=ws_sl, rownorm=(ss_sl, eps))
+    y_rc = ws_rc[: s1 * M * nq].view(s1, M, nq).sum(0)
+    y_sl = ws_sl[: s2 * M * nq].view(s2, M, nq).sum(0)
+    _check(y_rc, y_sl, f"rc vs slab qkv M{M}", tol=1e-2)
+    h = r_rc.float()
+    xn = h * torch.rsqrt((h * h).mean(-1, keepdim=True) + eps) * nw.float()
+    _check(y_rc, xn @ wq.float().t(), f"rc qkv vs fp32 M{M}")

@@ -26,7 +26,8 @@ import torch  # noqa: E402
 SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=None if on is None else False),
             "seam_auto_rc": lambda m, on: m.set_decode_fusion(seam=bool(on)),
             "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on),
-            "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False)}
+            "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False),
+            "rc_down": lambda m, on: setattr(m, "RC_DOWN", on is not False)}
 
 
 def _ops():
