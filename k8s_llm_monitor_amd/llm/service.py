@@ -238,22 +238,31 @@ class RecordStore:
             log.warning("storage.type %r is not available offline; using memory", kind)
 
     def put(self, resp: AnalysisResponse) -> None:
-        plain = gojson.to_plain(resp)
+        """Keep the record as it is (a finished response is never mutated): the Go-encoding round
+        trip into plain values happens when a record is read back (``get`` / ``list``, rare), not
+        on every answer's path - it cost as much as encoding the HTTP reply itself."""
+        line = gojson.dumps(resp) + "\n" if self.path else None
         with self._lock:
-            self._d[resp.request_id] = plain
+            self._d[resp.request_id] = resp
             while len(self._d) > self.capacity:
                 self._d.popitem(last=False)
-            if self.path:
+            if line is not None:
                 with open(self.path, "a", encoding="utf-8") as fh:
-                    fh.write(gojson.dumps(resp) + "\n")
+                    fh.write(line)
+
+    @staticmethod
+    def _plain(rec):
+        return rec if isinstance(rec, dict) else gojson.to_plain(rec)
 
     def get(self, rid: str) -> Optional[dict]:
         with self._lock:
-            return self._d.get(rid)
+            rec = self._d.get(rid)
+        return None if rec is None else self._plain(rec)
 
     def list(self, limit: int = 50) -> list:
         with self._lock:
-            return list(self._d.values())[-limit:]
+            recs = list(self._d.values())[-limit:]
+        return [self._plain(r) for r in recs]
 
     def __len__(self) -> int:
         return len(self._d)

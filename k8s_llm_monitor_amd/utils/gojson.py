@@ -115,7 +115,10 @@ def format_float(f: float) -> str:
         if out[-4] == "e" and out[-3] == "-" and out[-2] == "0":  # Go's e-09 -> e-9 cleanup
             out = out[:-2] + out[-1]
         return out
-    s = format(Decimal(repr(f)), "f")
+    r = repr(f)
+    if "e" not in r:  # repr is already fixed-point here ([1e-4, 1e16)): Go's digits, maybe a ".0"
+        return r.rstrip("0").rstrip(".") if "." in r else r
+    s = format(Decimal(r), "f")
     if "." in s:
         s = s.rstrip("0").rstrip(".")
     return s
@@ -171,6 +174,23 @@ def _empty(v: Any) -> bool:
     return False
 
 
+_FIELDS: dict = {}
+
+
+def _fields(cls) -> list:
+    """Per dataclass type, once: (attribute, encoded '"name":', omitempty, time) of every encoded field."""
+    fs = _FIELDS.get(cls)
+    if fs is None:
+        fs = []
+        for f in dataclasses.fields(cls):
+            md = f.metadata
+            if md.get("skip"):
+                continue
+            fs.append((f.name, quote(md.get("json") or f.name) + ":", bool(md.get("omitempty")), bool(md.get("time"))))
+        _FIELDS[cls] = fs
+    return fs
+
+
 def _enc(o: Any, out: list) -> None:
     if o is None:
         out.append("null")
@@ -191,21 +211,16 @@ def _enc(o: Any, out: list) -> None:
     elif dataclasses.is_dataclass(o) and not isinstance(o, type):
         out.append("{")
         first = True
-        for f in dataclasses.fields(o):
-            md = f.metadata
-            if md.get("skip"):
+        for attr, key, omitempty, is_time in _fields(type(o)):
+            v = getattr(o, attr)
+            if omitempty and _empty(v):
                 continue
-            name = md.get("json") or f.name
-            v = getattr(o, f.name)
-            if md.get("omitempty") and _empty(v):
-                continue
-            if md.get("time") and v is None:
+            if is_time and v is None:
                 v = ZERO_TIME
             if not first:
                 out.append(",")
             first = False
-            out.append(quote(name))
-            out.append(":")
+            out.append(key)
             _enc(v, out)
         out.append("}")
     elif isinstance(o, dict):
