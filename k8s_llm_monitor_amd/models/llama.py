@@ -894,20 +894,26 @@ class CausalLM:
         sync free, so the step stays in the decode hipGraph."""
         c = self.cfg
         xn = self._tp_tail(ws, ns, residual, L["mlp_norm"], packed=False)
+        xp = None  # the normed rows fragment-packed (the expert GEMMs' A operand)
         if xn is None:
             y = self._row_parallel_sum(ws, ns, M, residual)
             if y is None:
-                xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps)
+                # TP=1: one launch writes the router's row-major rows and the packed A operand
+                xp = ops.packed_empty(M, c.d_model, self.dtype, self.device)
+                xn = ops.reduce_add_rms_norm(torch.empty_like(residual), residual, ws, ns, L["mlp_norm"], c.norm_eps,
+                                             packed_out=xp)
             else:
                 xn = ops.fused_add_rms_norm(y, residual, L["mlp_norm"], c.norm_eps)
         _, _, wd = ops.moe_router(xn, L["router"], c.top_k_experts, True)
+        if xp is None:
+            xp = ops.pack_activation(xn)
         if "w13_dg" in L and M <= ops.SKINNY_MAX_M:  # shared-A decode GEMM over the packed expert copies
             E = L["w13_dg"].shape[0]
             act = torch.empty((E, -(-M // 16), L["w13_dg"].shape[1] // 4, 64, 8), dtype=self.dtype, device=self.device)
-            ops.dec_gemm_grouped(ops.pack_activation(xn), L["w13_dg"], 2, M, out=act)
+            ops.dec_gemm_grouped(xp, L["w13_dg"], 2, M, out=act)
             return ops.dec_gemm_grouped(act, L["w2_dg"], 0, M, workspace=ws,
                                         row_w=wd[:, self.e_lo:self.e_hi].contiguous())
-        act = ops.skinny_grouped_swiglu(ops.pack_activation(xn), L["w13_pg"], rows=M)
+        act = ops.skinny_grouped_swiglu(xp, L["w13_pg"], rows=M)
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 
     def _proj_slabs(self, L: dict, key: str, x: Optional[torch.Tensor], rows: int, split: int,

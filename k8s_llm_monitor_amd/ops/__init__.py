@@ -579,18 +579,21 @@ def reduce_slabs(workspace: torch.Tensor, nslabs: int, M: int, N: int, dtype=tor
 
 
 def reduce_add_rms_norm(out: torch.Tensor, residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int,
-                        norm_w: torch.Tensor, eps: float) -> torch.Tensor:
+                        norm_w: torch.Tensor, eps: float, packed_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``residual <- residual + sum of slabs`` (rounded to the residual dtype), ``out <- rms_norm``.
     ``nslabs = 0``: a plain RMSNorm of ``residual``.  A 4-D ``out`` is written fragment-packed
-    ([ceil(M/16), d/32, 64, 8], the next skinny GEMM's A operand)."""
+    ([ceil(M/16), d/32, 64, 8], the next skinny GEMM's A operand); ``packed_out``: a second,
+    packed copy of the same rows (same launch)."""
     if not _gpu(residual):
         M, N = residual.shape
         if nslabs:
             s = workspace[: nslabs * M * N].view(nslabs, M, N).sum(0)
             residual.copy_((residual.float() + s).to(residual.dtype))
         y = ref.rms_norm(residual, norm_w, eps)
+        if packed_out is not None:
+            packed_out.copy_(pack_activation(y))
         return out.copy_(pack_activation(y) if out.dim() == 4 else y)
-    native().reduce_add_rms_norm(out, residual, workspace, nslabs, norm_w, eps)
+    native().reduce_add_rms_norm(out, residual, workspace, nslabs, norm_w, eps, packed_out)
     return out
 
 

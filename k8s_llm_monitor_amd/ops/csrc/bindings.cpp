@@ -68,7 +68,7 @@ int k8sllm_embed_norm_partial(void* out, long out_stride, void* residual, const 
 int k8sllm_gemm_skinny_slabs(int K, int S);
 int k8sllm_reduce_slabs(void* out, const float* partial, int S, long n, hipStream_t s);
 int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M, const void* w, int d,
-                              float eps, long out_stride, hipStream_t s);
+                              float eps, long out_stride, void* out2, hipStream_t s);
 void* k8sllm_car_create(int rank, int world, long max_elems, void* handles, int* err);
 int k8sllm_car_handle_size();
 int k8sllm_car_open(void* state, const void* all_handles);
@@ -865,7 +865,7 @@ void reduce_slabs(torch::Tensor out, torch::Tensor partial, int64_t S) {
 }
 
 void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, c10::optional<torch::Tensor> partial, int64_t S,
-                         torch::Tensor w, double eps) {
+                         torch::Tensor w, double eps, c10::optional<torch::Tensor> out_packed) {
   dev_bf16(out, "out"); dev_bf16(residual, "residual"); dev_bf16(w, "w");
   TORCH_CHECK(residual.is_contiguous() && out.is_contiguous() && w.is_contiguous(), "reduce_add_rms_norm layout");
   const int d = (int)residual.size(-1);
@@ -885,8 +885,16 @@ void reduce_add_rms_norm(torch::Tensor out, torch::Tensor residual, c10::optiona
   } else {
     TORCH_CHECK(out.numel() == (int64_t)M * d, "reduce_add_rms_norm shapes");
   }
+  void* out2 = nullptr;
+  if (out_packed.has_value()) {  // a second, fragment-packed copy of the normed rows
+    const auto& o2 = *out_packed;
+    dev_bf16(o2, "out_packed");
+    TORCH_CHECK(o2.dim() == 4 && o2.is_contiguous() && o2.size(0) == (M + 15) / 16 && o2.size(1) * 32 == d &&
+                    o2.size(2) == 64 && o2.size(3) == 8, "out_packed must be [ceil(M/16), d/32, 64, 8]");
+    out2 = o2.data_ptr();
+  }
   check(k8sllm_reduce_add_rmsnorm(out.data_ptr(), residual.data_ptr(), pp, (int)S, M, w.data_ptr(), d, (float)eps,
-                                  ostride, cur()),
+                                  ostride, out2, cur()),
         "reduce_add_rms_norm");
 }
 

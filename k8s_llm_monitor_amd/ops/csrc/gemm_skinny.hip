@@ -496,13 +496,14 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_skinny_rm_kernel(
 // residual[m] <- bf16(residual[m] + sum_s partial[s][m]); out[m] <- rmsnorm(residual[m]) * w
 // One workgroup per row, 256 threads x 8 columns per chunk (d <= 2048 * NC).  S = 0 is a plain
 // RMSNorm of the residual.  out_stride < 0: out is written fragment-packed (act_index) as the next
-// skinny GEMM's A operand.
+// skinny GEMM's A operand.  out2 (optional): a second, fragment-packed copy (the MoE decode: the
+// router reads the row-major form, the expert GEMMs the packed one - no separate pack pass).
 template <int NC>
 __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restrict__ out,
                                                                  bf16_t* __restrict__ residual,
                                                                  const float* __restrict__ partial, int S, int M,
                                                                  const bf16_t* __restrict__ w, int d, float eps,
-                                                                 long out_stride) {
+                                                                 long out_stride, bf16_t* __restrict__ out2) {
   __shared__ float sred[4];
   const int row = blockIdx.x, tid = threadIdx.x;
   bf16_t* rr = residual + (long)row * d;
@@ -538,7 +539,9 @@ __global__ __launch_bounds__(256) void reduce_add_rmsnorm_kernel(bf16_t* __restr
       unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
-      *reinterpret_cast<uint4*>(out + act_index(row, idx, out_stride)) = pack8(o);
+      const uint4 q = pack8(o);
+      *reinterpret_cast<uint4*>(out + act_index(row, idx, out_stride)) = q;
+      if (out2 != nullptr) *reinterpret_cast<uint4*>(out2 + act_index(row, idx, -(long)(d >> 5))) = q;
     }
   }
 }
@@ -895,13 +898,14 @@ static int skinny_launch(const void* A, long lda, const void* Wp, float* partial
 }
 
 extern "C" int k8sllm_reduce_add_rmsnorm(void* out, void* residual, const float* partial, int S, int M,
-                                         const void* w, int d, float eps, long out_stride, hipStream_t s) {
+                                         const void* w, int d, float eps, long out_stride, void* out2,
+                                         hipStream_t s) {
   if (M <= 0) return 0;
   if (d % 8 != 0 || d > 256 * 8 * 4) return -1;
   const int nc = (d + 2047) / 2048;
 #define K8S_RAR(NC)                                                                                           \
   hipLaunchKernelGGL((reduce_add_rmsnorm_kernel<NC>), dim3(M), dim3(256), 0, s, (bf16_t*)out,                 \
-                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, eps, out_stride)
+                     (bf16_t*)residual, partial, S, M, (const bf16_t*)w, d, eps, out_stride, (bf16_t*)out2)
   if (nc <= 1) K8S_RAR(1);
   else if (nc <= 2) K8S_RAR(2);
   else K8S_RAR(4);
