@@ -21,6 +21,7 @@ int k8sllm_rope_cache(void* qkv, long qkv_stride, const int* positions, const fl
 int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part_ml, const void* q, long q_stride,
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
+void k8sllm_decode_tw_force(int tw);
 int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml, const float* slabs,
                               int nslabs, const int* positions, const float* cos_sin, const int* slot_mapping,
                               void* k_cache, void* v_cache, const int* block_tables, int bt_stride,
@@ -983,6 +984,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);
+  m.def("decode_tw_force", [](int64_t tw) { k8sllm_decode_tw_force((int)tw); });
   m.def("flash_prefill", &flash_prefill);
   m.def("embed_norm_partial", &embed_norm_partial);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),

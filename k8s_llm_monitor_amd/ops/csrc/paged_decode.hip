@@ -472,7 +472,11 @@ extern "C" int k8sllm_paged_decode_fused(void* out, long out_stride, float* part
 // Tokens per wave per chunk: the double-buffered 32-token form once the grid fills the chip
 // (>= 384 workgroups, e.g. batch 64 x 8 kv heads), else the single-buffered 64-token form (small
 // batches, split grids: higher residency).
+static int g_tw_force = 0;  // tools/bench_decode_step.py: 32 / 64 forces one form (0: by grid size)
+extern "C" void k8sllm_decode_tw_force(int tw) { g_tw_force = tw; }
+
 static int decode_tw(int S, int Hkv, int B) {
+  if (g_tw_force == 32 || g_tw_force == 64) return g_tw_force;
   return (long)S * Hkv * B >= 384 ? 32 : 64;
 }
 

@@ -27,7 +27,8 @@ SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=None if on is 
             "seam_auto_rc": lambda m, on: m.set_decode_fusion(seam=bool(on)),
             "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on),
             "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False),
-            "rc_down": lambda m, on: setattr(m, "RC_DOWN", on is not False)}
+            "rc_down": lambda m, on: setattr(m, "RC_DOWN", on is not False),
+            "tw32": lambda m, on: _ops().native().decode_tw_force(32 if on else 0)}
 
 
 def _ops():
