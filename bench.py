@@ -287,8 +287,14 @@ def run_rank(a) -> None:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     res: list[dict] = []
-    for k in range(a.steps):
-        res += step(a.warmup + k)
+    if loadgen and a.path == "http" and a.mode == "wave":
+        # the K closed-loop waves run inside the client process (wave k+1 goes out when wave k is
+        # answered, as step() does per wave) - no parent <-> client pipe round trip between waves
+        res = loadgen.post_waves(port, list(range(a.warmup, a.warmup + a.steps)), a.max_new_tokens,
+                                 allow_errors=a.production, slim=True)
+    else:
+        for k in range(a.steps):
+            res += step(a.warmup + k)
     if on_gpu:
         torch.cuda.synchronize()
     leaders_barrier()

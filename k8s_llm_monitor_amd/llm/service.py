@@ -41,6 +41,9 @@ class GenResult(dict):
 
 class LocalEngineBackend:
     provider = "local-rocm"
+    # generate() never waits past answer_budget_s + 0.75 s (the engine ends the sequence at the
+    # budget): the HTTP layer's write-timeout backstop is already enforced here
+    enforces_deadline = True
 
     def __init__(self, service, max_tokens: int = 2000, temperature: float = 0.1, top_p: float = 1.0,
                  top_k: int = 0, timeout_s: float = 30.0, answer_budget_s: Optional[float] = None):
@@ -83,7 +86,8 @@ class LocalEngineBackend:
                               deadline=time.perf_counter() + budget if budget else None)
         try:
             # the engine stops the sequence at the deadline; the grace covers the last step + detokenize
-            text, seq = fut.result(timeout=budget + 2.0 if budget else None)
+            # (budget + 0.75 s = the server's write timeout - 0.5 s: the HTTP layer's backstop limit)
+            text, seq = fut.result(timeout=budget + 0.75 if budget else None)
         except FutTimeout:
             self.svc.cancel(fut)  # free the KV blocks: nobody waits for this answer any more
             raise TimeoutError("answer not ready within the answer budget") from None

@@ -13,6 +13,7 @@ Protocol: one JSON request per stdin line, one JSON reply per stdout line.
      "slim": bool (optional: only the timing / token-count fields travel back)}
     {"op": "stage", "key": K, "items": [[question, context], ...]}   (kept for later "query"s)
     {"op": "query", "port": P, "staged": K, ...}   (the staged items: only the key crosses the pipe)
+    {"op": "waves", "port": P, "staged": [K, ...], ...}   (closed-loop waves back to back, one reply)
     {"op": "podcomm", "port": P, "pairs": [[pod_a, pod_b], ...], "max_new_tokens": N}
     -> {"ok": true, "results": [...]}   (post_queries / post_pod_communication result dicts)
     -> {"ok": false, "error": "..."}
@@ -51,6 +52,12 @@ def serve(stdin=None, stdout=None) -> None:
                                    offsets_s=req.get("offsets_s"), allow_errors=bool(req.get("allow_errors")))
                 if req.get("slim"):
                     res = [{k: r[k] for k in _SLIM if k in r} for r in res]
+            elif req["op"] == "waves":  # closed-loop waves back to back: wave k+1 goes out when k is answered
+                res = []
+                for key in req["staged"]:
+                    r = post_queries(req["port"], staged[str(key)], req["max_new_tokens"],
+                                     allow_errors=bool(req.get("allow_errors")))
+                    res += [{k: x[k] for k in _SLIM if k in x} for x in r] if req.get("slim") else r
             elif req["op"] == "podcomm":
                 res = post_pod_communication(req["port"], [tuple(x) for x in req["pairs"]], req["max_new_tokens"])
             else:
@@ -96,6 +103,14 @@ class LoadGen:
         else:
             req["items"] = [list(x) for x in items]
         return self._call(req)
+
+    def post_waves(self, port: int, keys: list, max_new_tokens: int, allow_errors: bool = False,
+                   slim: bool = False) -> list:
+        """The staged waves ``keys`` as closed-loop waves inside the client process (each wave
+        posted once the previous one is fully answered, as ``post_queries`` per wave) - one pipe
+        round trip for all of them; returns the concatenated per-request results."""
+        return self._call({"op": "waves", "port": port, "staged": [str(k) for k in keys],
+                           "max_new_tokens": max_new_tokens, "allow_errors": allow_errors, "slim": slim})
 
     def post_pod_communication(self, port: int, pairs: list, max_new_tokens: int) -> list:
         return self._call({"op": "podcomm", "port": port, "pairs": [list(x) for x in pairs],

@@ -345,10 +345,17 @@ class MonitorApp:
         instead of a 504 (LocalEngineBackend.answer_budget_s)."""
         return max(0.5, min(self.llm_timeout_s, self.write_timeout_s) - 1.25)
 
-    def _bounded(self, fn):
+    def _bounded(self, fn, kind: Optional[str] = None):
         """Run fn within the write timeout (leave 0.5 s to write the answer).  One shared pool (no
         thread spawned per request).  The engine itself stops at answer_budget_s (0.75 s earlier),
-        so this limit is a backstop; the backend cancels the engine request if it ever fires."""
+        so this limit is a backstop; the backend cancels the engine request if it ever fires.
+        ``kind``: the analysis type - when the backend that answers it bounds its own wait within
+        the same limit (``enforces_deadline``: the in-process engine), fn runs in the handler
+        thread: no hand-off to a pool thread and back on every request's path."""
+        if kind is not None and self.analysis is not None:
+            b = self.analysis.routes.get(kind, self.analysis.backend)
+            if getattr(b, "enforces_deadline", False):
+                return fn()
         limit = max(0.5, min(self.llm_timeout_s, self.write_timeout_s) - 0.5)
         return _bounded_pool().submit(fn).result(timeout=limit)
 
@@ -391,7 +398,7 @@ class MonitorApp:
         try:
             resp = self._bounded(lambda: self.analysis.query(question, max_tokens=mt,
                                                              ignore_eos=bool(d.get("ignore_eos", False)),
-                                                             context_text=ctx_text))
+                                                             context_text=ctx_text), kind="query")
         except _BUSY as e:
             return self._busy_reply(e)
         except FutTimeout:

@@ -86,7 +86,10 @@ def main() -> None:
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--waves", type=int, default=6)
     ap.add_argument("--answer-tokens", type=int, default=256)
+    ap.add_argument("--switch-ms", type=float, default=0.0, help="sys.setswitchinterval for the server process")
     a = ap.parse_args()
+    if a.switch_ms > 0:
+        sys.setswitchinterval(a.switch_ms * 1e-3)
     from k8s_llm_monitor_amd.monitor.loadgen import LoadGen
 
     lg = LoadGen(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
