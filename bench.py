@@ -423,9 +423,11 @@ def _print_trace(trace: list, t0: float) -> None:
         # wave boundary: the previous wave's last decode step -> this wave's first arrival -> first prefill
         prev = [e[0] for e in dec if e[0] < w[0][0]]
         nxt = [e[0] for e in pre if e[0] >= w[0][0]]
+        pls = [e for e in ev if e[1] == "plaunch" and e[0] >= w[0][0]]
         if prev and nxt:
+            lt = f", first prefill launched +{(pls[0][0] - w[0][0]) * 1e3:.1f} ms ({pls[0][3]:.1f} ms host)" if pls else ""
             print(f"[trace] boundary: last decode -> first add {(w[0][0] - prev[-1]) * 1e3:.1f} ms, "
-                  f"first add -> first prefill {(nxt[0] - w[0][0]) * 1e3:.1f} ms", file=sys.stderr)
+                  f"first add -> first prefill {(nxt[0] - w[0][0]) * 1e3:.1f} ms{lt}", file=sys.stderr)
             # where the boundary goes: answers resolved (detokenized) on the engine thread ->
             # first new request submitted by an HTTP handler -> added by the engine thread
             res = [e[0] for e in ev if e[1] == "resolved" and prev[-1] <= e[0] < w[0][0]]
@@ -453,6 +455,10 @@ def _print_trace(trace: list, t0: float) -> None:
             return v[min(len(v) - 1, int(f * len(v)))] if v else float("nan")
         print(f"[trace] decode interval p50 {q(iv, .5):.3f} p90 {q(iv, .9):.3f} ms; launch p50 {q(la, .5):.3f} "
               f"p90 {q(la, .9):.3f} ms; wait p10 {q(wt, .1):.3f} p50 {q(wt, .5):.3f} ms", file=sys.stderr)
+    pl = sorted(e[3] for e in ev if e[1] == "plaunch")
+    if pl:
+        print(f"[trace] prefill launch host ms p50 {pl[len(pl) // 2]:.2f} max {pl[-1]:.2f} ({len(pl)} steps)",
+              file=sys.stderr)
 
 
 def main(argv=None) -> None:

@@ -272,7 +272,10 @@ class LLMEngine:
         if self.bus is not None:
             self.bus.send_obj(self._pack(plan))
         plan.chunks = [q.chunk for q in plan.seqs]  # for the trace (chunk_done clears them)
+        t_l = time.perf_counter() if self.trace is not None else 0.0
         h = self.runner.prefill_launch(plan.seqs)
+        if self.trace is not None:  # host ms to stage and enqueue the step (exposed on a wave's first step)
+            self.trace.append((time.perf_counter(), "plaunch", len(plan.seqs), (time.perf_counter() - t_l) * 1e3))
         self._pf_step_id += 1
         sid = self._pf_step_id
         for seq in plan.seqs:
