@@ -995,7 +995,9 @@ class EngineService:
             except Exception as e:  # noqa: BLE001 - reject this request only
                 fut.set_exception(e)
             if coalesce and self._waiting_tokens() >= cfg.max_prefill_tokens:
-                coalesce = False  # a full prefill step is already queued: start it now
+                # a full prefill step is queued: start it now - the rest of the burst is drained
+                # while that step runs (draining it first held the launch until the burst ended)
+                break
             try:
                 item = self._q.get_nowait()
             except queue.Empty:
