@@ -436,6 +436,14 @@ def _print_trace(trace: list, t0: float) -> None:
                 print(f"[trace]   last decode -> answers resolved {(res[-1] - prev[-1]) * 1e3:.1f} ms, "
                       f"-> first submit {(sub[0] - res[-1]) * 1e3:.1f} ms, -> first add {(w[0][0] - sub[0]) * 1e3:.1f} ms",
                       file=sys.stderr)
+        # arrival timeline of the wave: k-th request submitted (server side) and added (engine)
+        sub_w = [e[0] for e in ev if e[1] == "submit" and w[0][0] - 0.5 <= e[0] <= w[-1][0]]
+        if sub_w:
+            t_s = sub_w[0]
+            ks = [k for k in (1, 4, 8, 12, 16, 32, 64) if k <= len(w)]
+            print("[trace]   k-th submit / add (ms after the first submit): " + " ".join(
+                f"{k}:{(sub_w[min(k, len(sub_w)) - 1] - t_s) * 1e3:.1f}/{(w[k - 1][0] - t_s) * 1e3:.1f}" for k in ks),
+                file=sys.stderr)
         gaps = sorted(b[0] - a_[0] for a_, b in zip(w, w[1:]))
         print(f"[trace] adds {len(w)} first +{(w[0][0] - t0) * 1e3:.1f} ms last +{(w[-1][0] - t0) * 1e3:.1f} ms"
               + (f" median gap {gaps[len(gaps) // 2] * 1e3:.2f} ms max gap {gaps[-1] * 1e3:.2f} ms" if gaps else ""),
