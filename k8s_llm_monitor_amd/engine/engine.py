@@ -698,11 +698,6 @@ class EngineService:
         # prefill throughput estimate (tokens/s, EWMA over prefill steps) for deadline admission
         self._prefill_tps: Optional[float] = None
         self._waiting_est = 0  # prompt tokens waiting in the scheduler (engine thread writes)
-        # prompt tokens submitted but not yet taken by the engine thread, and the event a submitter
-        # sets when those plus the scheduler's waiting tokens fill a prefill step (_drain)
-        self._qtok = 0
-        self._qtok_lock = threading.Lock()
-        self._step_full = threading.Event()
         self.tpot = TpotModel()
         self.answer_lens = AnswerLengths()
         self._step_cache: dict = {}  # per-step memo of the running set's deadline slack
@@ -810,10 +805,6 @@ class EngineService:
         if tr is not None:
             tr.append((time.perf_counter(), "submit", 1, 0))
         self._q.put((prompt, params, request_id, fut, on_tokens, deadline))
-        with self._qtok_lock:
-            self._qtok += len(prompt)
-            if self._qtok + self._waiting_est >= self.engine.cfg.max_prefill_tokens:
-                self._step_full.set()
         return fut
 
     def cancel(self, fut: Future) -> bool:
@@ -993,8 +984,6 @@ class EngineService:
         t_end = time.perf_counter() + cfg.admit_window_ms * 1e-3
         while item is not None:
             prompt, params, rid, fut, on_tokens, deadline = item
-            with self._qtok_lock:
-                self._qtok -= len(prompt)
             try:
                 if fut.cancelled():  # cancelled while queued
                     raise _Skip()
@@ -1005,8 +994,7 @@ class EngineService:
                 pass
             except Exception as e:  # noqa: BLE001 - reject this request only
                 fut.set_exception(e)
-            self._waiting_est = self._waiting_tokens()
-            if coalesce and self._waiting_est >= cfg.max_prefill_tokens:
+            if coalesce and self._waiting_tokens() >= cfg.max_prefill_tokens:
                 # a full prefill step is queued: start it now - the rest of the burst is drained
                 # while that step runs (draining it first held the launch until the burst ended)
                 break
@@ -1016,15 +1004,8 @@ class EngineService:
                 item = None
                 wait = min(cfg.admit_gap_ms * 1e-3, t_end - time.perf_counter()) if coalesce else 0.0
                 if wait > 0:
-                    # wait for the gap or for a full step's worth of submitted tokens, then take what
-                    # arrived in bulk: one wake-up per gap instead of one per request - every wake-up
-                    # re-takes the interpreter lock, which a burst's HTTP handler threads hold
-                    with self._qtok_lock:
-                        if self._qtok + self._waiting_est < cfg.max_prefill_tokens:
-                            self._step_full.clear()
-                    self._step_full.wait(wait)
                     try:
-                        item = self._q.get_nowait()
+                        item = self._q.get(timeout=wait)
                     except queue.Empty:
                         item = None
 
