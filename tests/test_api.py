@@ -260,3 +260,47 @@ def test_context_fits_a_short_model_window():
         assert r.result["prompt_tokens"] + 32 <= 512
     finally:
         svc.close()
+
+
+def test_record_store_keeps_answers_and_reads_back_plain(tmp_path):
+    """RecordStore keeps a finished AnalysisResponse as is (no Go-JSON round trip on the answer's
+    path) and converts on read: get / list return the same plain dicts the round trip produced, and
+    the file store writes one Go-JSON line per record."""
+    from k8s_llm_monitor_amd.llm.service import RecordStore
+    from k8s_llm_monitor_amd.monitor.types import AnalysisResponse
+    from k8s_llm_monitor_amd.utils import gojson
+    from k8s_llm_monitor_amd.utils.gojson import utcnow
+
+    for kind in ("memory", "file"):
+        st = RecordStore(kind, path=str(tmp_path / kind), capacity=2)
+        rs = [AnalysisResponse(request_id=f"r{i}", status="success",
+                               result={"type": "query", "answer": f"a<{i}>", "latency_ms": 12.5 + i},
+                               timestamp=utcnow()) for i in range(3)]
+        for r in rs:
+            st.put(r)
+        assert st.get("r0") is None  # capacity 2: the oldest was evicted
+        assert st.get("r2") == gojson.to_plain(rs[2])
+        assert st.list(10) == [gojson.to_plain(rs[1]), gojson.to_plain(rs[2])]
+        if kind == "file":
+            lines = (tmp_path / kind / "analysis_records.jsonl").read_text().splitlines()
+            assert [json.loads(x)["request_id"] for x in lines] == ["r0", "r1", "r2"]
+
+
+def test_gojson_float_fast_path_matches_decimal_form():
+    """format_float's fixed-point fast path (repr already in Go's digits) equals the Decimal form
+    it replaced, over random values across the fixed-point range and integral floats."""
+    import random
+    from decimal import Decimal
+
+    from k8s_llm_monitor_amd.utils.gojson import format_float
+
+    def slow(f):
+        s = format(Decimal(repr(f)), "f")
+        return s.rstrip("0").rstrip(".") if "." in s else s
+
+    r = random.Random(0)
+    for _ in range(20000):
+        f = r.choice([r.uniform(-1e3, 1e3), 10 ** r.uniform(-6, 20.9) * r.choice([1, -1]),
+                      float(r.randint(-10 ** 6, 10 ** 6)), round(r.uniform(0, 100), 2)])
+        if f != 0:
+            assert format_float(f) == slow(f), f
