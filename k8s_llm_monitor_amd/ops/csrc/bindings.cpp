@@ -22,6 +22,7 @@ int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
 void k8sllm_decode_tw_force(int tw);
+void k8sllm_tile_resid_nt(int v);
 int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml, const float* slabs,
                               int nslabs, const int* positions, const float* cos_sin, const int* slot_mapping,
                               void* k_cache, void* v_cache, const int* block_tables, int bt_stride,
@@ -985,6 +986,7 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);
   m.def("decode_tw_force", [](int64_t tw) { k8sllm_decode_tw_force((int)tw); });
+  m.def("tile_resid_nt", [](int64_t v) { k8sllm_tile_resid_nt((int)v); });
   m.def("flash_prefill", &flash_prefill);
   m.def("embed_norm_partial", &embed_norm_partial);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),

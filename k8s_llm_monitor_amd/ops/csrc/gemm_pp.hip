@@ -441,7 +441,7 @@ extern "C" int k8sllm_gemm_pp(const void* X, const void* W, void* Y, int M, int 
   if (rs && (grouped || rs_np < 4 || rs_np > 64 || rs_np % 4 != 0 || (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
     return -1;
   const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,
-                   (const bf16_t*)norm_w, ss_out};
+                   (const bf16_t*)norm_w, ss_out, 0};
   if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
   if (epi == TILE_EPI_RESID && 256L * N * 2 >= (1L << 31)) return -3;
   const int n_mt = (M + 255) / 256 + (grouped ? E : 0), n_nt = (N + 255) / 256;

@@ -429,8 +429,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       }
       const uint4 hq = pack8(h), wq = pack8(hw);
       const uint32_t off = ro + (uint32_t)(4 * b * N * 2);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 0);
+      if (ep.st_nt) {
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 2);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 0);
+      }
       ss = row16_sum(ss);
       const int grow = wm * 128 + r;
       if (cc == 0 && grow < mrows) ep.ss_out[(long)(row0 + grow) * ss_np + ssc] = ss;
@@ -505,6 +510,9 @@ extern "C" int k8sllm_gemm_pp(const void* X, const void* W, void* Y, int M, int 
                               float* ss_out, hipStream_t s);
 
 // algo 2: the 8-wave ping-pong schedule (gemm_pp.hip), same contract.
+static int g_resid_nt = 0;  // tools/bench_tile_epilogues.py: 1 = non-temporal residual-epilogue stores
+extern "C" void k8sllm_tile_resid_nt(int v) { g_resid_nt = v; }
+
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
                                 long w_es, int epi, int algo, const int* rope_pos, const float* rope_cs,
                                 int rope_heads, const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw,
@@ -534,7 +542,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
              (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
     return -1;
   const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,
-                   (const bf16_t*)norm_w, ss_out};
+                   (const bf16_t*)norm_w, ss_out, g_resid_nt};
   // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert / n-tile)
   if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
   if (epi == TILE_EPI_RESID && 256L * N * 2 >= (1L << 31)) return -3;

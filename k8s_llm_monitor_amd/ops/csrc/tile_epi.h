@@ -33,6 +33,7 @@ struct TileEpi {
   bf16_t* hw;            // RESID: [M][N] resid * norm_w
   const bf16_t* norm_w;  // RESID: [N] the next RMSNorm's weight
   float* ss_out;         // RESID: [M][N / 128]
+  int st_nt;             // RESID: non-temporal resid / hw stores (tools A/B: k8sllm_tile_resid_nt)
 };
 
 // sum over the 16 lanes of a DPP row (lanes 16r .. 16r + 15), the total in every lane
