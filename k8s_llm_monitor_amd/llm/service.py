@@ -90,7 +90,8 @@ class LocalEngineBackend:
             text, seq = fut.result(timeout=budget + 0.75 if budget else None)
         except FutTimeout:
             self.svc.cancel(fut)  # free the KV blocks: nobody waits for this answer any more
-            raise TimeoutError("answer not ready within the answer budget") from None
+            # a futures TimeoutError: the HTTP layer answers it 504, as its own write-timeout backstop
+            raise FutTimeout("answer not ready within the answer budget") from None
         t = seq.timings()
         return GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason, **t)
 
@@ -346,6 +347,8 @@ class AnalysisService:
             resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
         except (EngineOverloaded, EngineUnavailable):
             raise  # admission refused: the HTTP layer answers 503 (nothing to record)
+        except FutTimeout:
+            raise  # the answer budget ran out: the HTTP layer answers 504
         except Exception as e:  # noqa: BLE001 - an engine failure becomes an error record, not a 500
             log.error("analysis %s failed: %s", rid, e)
             resp = AnalysisResponse(request_id=rid, status="error", result={"type": kind, **extra},

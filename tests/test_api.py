@@ -304,3 +304,26 @@ def test_gojson_float_fast_path_matches_decimal_form():
                       float(r.randint(-10 ** 6, 10 ** 6)), round(r.uniform(0, 100), 2)])
         if f != 0:
             assert format_float(f) == slow(f), f
+
+
+@pytest.mark.parametrize("inline", [True, False])
+def test_query_answer_budget_timeout_is_504(mon, inline):
+    """A backend whose answer budget runs out answers /api/v1/query with 504, both when the query
+    runs in the handler thread (the backend bounds its own wait: ``enforces_deadline``) and on the
+    bounded pool."""
+    from concurrent.futures import TimeoutError as FutTimeout
+
+    class SlowBackend:
+        provider, model = "stub", "stub"
+        enforces_deadline = inline
+
+        def count_tokens(self, text):
+            return len(text) // 4
+
+        def generate(self, prompt, **kw):
+            raise FutTimeout("answer not ready within the answer budget")
+
+    a = mon.app
+    a.analysis.backend = SlowBackend()
+    r = a.handle("POST", "/api/v1/query", json.dumps({"question": "why is node-1 NotReady?"}).encode())
+    assert r.code == 504, (r.code, r.body[:200])
