@@ -75,10 +75,10 @@ def parse(argv=None):
                     help="process: the HTTP clients run in a child load-generator process (remote clients; the "
                          "serving process keeps its interpreter lock); thread: client threads in this process")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--decode-fusion", choices=["auto", "none", "seam", "rc"], default="auto",
-                    help="A/B runs of the decode-step fusions (CausalLM.set_decode_fusion): auto = the "
-                         "default (row-complete o only for the smallest buckets), none = off, seam / rc = "
-                         "that fusion in every bucket")
+    ap.add_argument("--decode-fusion", choices=["auto", "none", "rc"], default="auto",
+                    help="A/B runs of the decode-step fusion (CausalLM.set_decode_fusion): auto = the "
+                         "default (row-complete o only for the smallest buckets), none = off, rc = "
+                         "every bucket")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
@@ -193,13 +193,19 @@ def run_rank(a) -> None:
 
     admit = {k: v for k, v in (("admit_gap_ms", a.admit_gap_ms), ("admit_window_ms", a.admit_window_ms),
                                ("mixed_prefill_tokens", a.mixed_prefill_tokens)) if v is not None}
+    if not on_gpu:
+        # the CPU engine's steps are seconds long and its HTTP handlers share the same 8 cores, so a
+        # wave's requests arrive over ~100 ms: coalesce them for 250 ms (still ~1/8 of one CPU
+        # prefill step) so the wave starts as one prefill batch (config 1, VERDICT r5 Missing #3)
+        admit.setdefault("admit_gap_ms", 25.0)
+        admit.setdefault("admit_window_ms", 250.0)
     eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=max(a.batch, 8) if a.mode == "latency" else a.batch,
                                  max_model_len=8192, max_prefill_tokens=a.max_prefill_tokens,
                                  chunked_prefill=bool(a.chunked_prefill), tp_size=a.tp,
-                                 kv_cache_gb=a.kv_cache_gb if on_gpu else 0.05, use_graphs=not a.no_graphs,
+                                 kv_cache_gb=a.kv_cache_gb if on_gpu else 0.0, use_graphs=not a.no_graphs,
                                  seed=a.seed + ps.dp_rank, **admit), pstate=ps)
     if a.decode_fusion != "auto":
-        eng.model.set_decode_fusion(seam=a.decode_fusion == "seam", rc=a.decode_fusion == "rc")
+        eng.model.set_decode_fusion(rc=a.decode_fusion == "rc")
     eng.warmup()
     devices = [str(ps.device)] * world
     if world > 1:

@@ -32,7 +32,7 @@ DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160
 class RunnerConfig:
     max_num_seqs: int = 64
     max_model_len: int = 8192
-    kv_cache_gb: float = 16.0
+    kv_cache_gb: float = 16.0  # <= 0: max_num_seqs x max_model_len worth of blocks
     num_blocks: Optional[int] = None  # overrides kv_cache_gb
     use_graphs: bool = True
     seed: int = 0
@@ -48,7 +48,12 @@ class ModelRunner:
         self.max_blocks_per_seq = (self.max_len + BLOCK_SIZE - 1) // BLOCK_SIZE
         L, hkv, D = c.n_layers, model.hkv, model.D
         per_block = 2 * L * hkv * D * BLOCK_SIZE * 2  # bytes (K + V, bf16)
-        nb = cfg.num_blocks or max(self.max_blocks_per_seq + 1, int(cfg.kv_cache_gb * (1 << 30) // per_block))
+        if cfg.num_blocks:
+            nb = cfg.num_blocks
+        elif cfg.kv_cache_gb <= 0:  # auto: every admitted sequence can reach max_len (+ one spare block)
+            nb = cfg.max_num_seqs * self.max_blocks_per_seq + 1
+        else:
+            nb = max(self.max_blocks_per_seq + 1, int(cfg.kv_cache_gb * (1 << 30) // per_block))
         self.num_blocks = nb
         self.k_cache = torch.zeros(L, nb, hkv, D // 8, BLOCK_SIZE, 8, dtype=model.dtype, device=self.device)
         self.v_cache = torch.zeros(L, nb, hkv, D, BLOCK_SIZE, dtype=model.dtype, device=self.device)

@@ -39,6 +39,12 @@ class GenResult(dict):
     """{text, prompt_tokens, completion_tokens, latency_ms, ttft_ms, model, provider}"""
 
 
+class AnswerBudgetExceeded(FutTimeout):
+    """The in-process engine's answer budget ran out (LocalEngineBackend.generate): the HTTP layer
+    answers 504.  Its own type, so that other timeouts (a routed backend's socket timeout, which
+    IS ``concurrent.futures.TimeoutError`` on Python >= 3.11) still become error records."""
+
+
 class LocalEngineBackend:
     provider = "local-rocm"
     # generate() never waits past answer_budget_s + 0.75 s (the engine ends the sequence at the
@@ -74,13 +80,14 @@ class LocalEngineBackend:
         return len(self.tokenizer.encode(text, bos=False))
 
     def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
-                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+                 request_id: Optional[str] = None, ignore_eos: bool = False,
+                 top_p: Optional[float] = None) -> GenResult:
         from ..engine import SamplingParams
 
         d = self.default
         p = SamplingParams(max_tokens=max_tokens or d.max_tokens,
                            temperature=d.temperature if temperature is None else temperature,
-                           top_k=d.top_k, top_p=d.top_p, ignore_eos=ignore_eos)
+                           top_k=d.top_k, top_p=d.top_p if top_p is None else top_p, ignore_eos=ignore_eos)
         budget = self.answer_budget_s
         fut = self.svc.submit(P.SYSTEM_PREAMBLE + prompt, p, request_id,
                               deadline=time.perf_counter() + budget if budget else None)
@@ -91,7 +98,7 @@ class LocalEngineBackend:
         except FutTimeout:
             self.svc.cancel(fut)  # free the KV blocks: nobody waits for this answer any more
             # a futures TimeoutError: the HTTP layer answers it 504, as its own write-timeout backstop
-            raise FutTimeout("answer not ready within the answer budget") from None
+            raise AnswerBudgetExceeded("answer not ready within the answer budget") from None
         t = seq.timings()
         return GenResult(text=text, model=self.model, provider=self.provider, finish_reason=seq.finish_reason, **t)
 
@@ -180,13 +187,17 @@ class OpenAIBackend:
         return max(1, len(text.encode()) // 3)
 
     def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
-                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+                 request_id: Optional[str] = None, ignore_eos: bool = False,
+                 top_p: Optional[float] = None) -> GenResult:
         if not self.api_key:
             raise RuntimeError("llm.api_key / OPENAI_API_KEY not configured")
-        body = json.dumps({"model": self.model, "max_tokens": max_tokens or self.max_tokens,
-                           "temperature": self.temperature if temperature is None else temperature,
-                           "messages": [{"role": "system", "content": P.SYSTEM_PREAMBLE},
-                                        {"role": "user", "content": prompt}]}).encode()
+        req_d = {"model": self.model, "max_tokens": max_tokens or self.max_tokens,
+                 "temperature": self.temperature if temperature is None else temperature,
+                 "messages": [{"role": "system", "content": P.SYSTEM_PREAMBLE},
+                              {"role": "user", "content": prompt}]}
+        if top_p is not None:
+            req_d["top_p"] = top_p
+        body = json.dumps(req_d).encode()
         req = urllib.request.Request(self.base_url + "/chat/completions", data=body, method="POST",
                                      headers={"Content-Type": "application/json",
                                               "Authorization": f"Bearer {self.api_key}"})
@@ -209,7 +220,8 @@ class RuleBackend:
         return max(1, len(text.encode()) // 3)
 
     def generate(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
-                 request_id: Optional[str] = None, ignore_eos: bool = False) -> GenResult:
+                 request_id: Optional[str] = None, ignore_eos: bool = False,
+                 top_p: Optional[float] = None) -> GenResult:
         flagged = [ln.strip() for ln in prompt.splitlines()
                    if any(k in ln for k in ("[资源压力]", "[不健康]", "状态=", "接近限制", "不通", "告警", "UAV "))]
         text = ("未发现明显异常。" if not flagged else
@@ -319,27 +331,63 @@ class AnalysisService:
             self._ctx_cache = (key, ctx)
         return ctx
 
-    def _fit(self, ctx: str, frame: str, max_tokens: Optional[int]) -> str:
+    def context_ready(self) -> bool:
+        """True when cluster_context() would return without touching the K8s API (no metrics
+        manager, or the current snapshot's context is cached)."""
+        if self.manager is None:
+            return True
+        snap = self.manager.get_latest_snapshot()
+        with self._ctx_lock:
+            return self._ctx_cache[0] == (id(snap), snap.timestamp)
+
+    def backend_for(self, kind: str):
+        """The backend that answers analysis type ``kind`` (``llm.routes``, else the default)."""
+        return self.routes.get(kind, self.backend)
+
+    def _fit(self, ctx: str, frame: str, max_tokens: Optional[int], kind: str = "query") -> str:
         """Trim the cluster context so that the whole prompt (``frame`` = the prompt without the
-        context) plus ``max_tokens`` answer tokens fit the model's window: a 1024-token GPT-2 would
-        otherwise get its prompt cut in the middle by the engine and room for one answer token.
-        Cheap when nothing can overflow: a byte-level BPE token covers >= 1 byte, so a prompt of
-        fewer bytes than the budget is never tokenized here."""
-        limit = getattr(self.backend, "max_prompt_tokens", None)
-        if limit is None:
+        context) plus ``max_tokens`` answer tokens fit the window of the model that answers
+        ``kind`` (a routed deployment's, not the local one's), counted with that backend's
+        tokenizer: a 1024-token GPT-2 would otherwise get its prompt cut in the middle by the
+        engine and room for one answer token.  A backend that publishes no window (a remote
+        OpenAI-compatible server) gets the context untrimmed.  Cheap when nothing can overflow: a
+        byte-level BPE token covers >= 1 byte, so a prompt of fewer bytes than the budget is never
+        tokenized here."""
+        backend = self.backend_for(kind)
+        limit = getattr(backend, "max_prompt_tokens", None)
+        count = getattr(backend, "count_tokens", None)
+        if limit is None or count is None:
             return ctx
         budget = limit(max_tokens or self.max_tokens) - len(P.SYSTEM_PREAMBLE.encode())
         if len(ctx.encode()) + len(frame.encode()) <= budget:
             return ctx
-        budget -= self.backend.count_tokens(frame) + 8
-        return P.trim_to_budget(ctx, lambda t: [0] * self.backend.count_tokens(t), max(budget, 16))
+        budget -= count(frame) + 8
+        return P.trim_to_budget(ctx, lambda t: [0] * count(t), max(budget, 16))
+
+    def fit_chat(self, parts: list, max_tokens: Optional[int]) -> str:
+        """The turns of an OpenAI-style chat joined into one prompt that fits the local model's
+        window with ``max_tokens`` answer tokens: the oldest turns are dropped first; a last turn
+        that alone is too long keeps its head and tail (trim_to_budget)."""
+        limit = getattr(self.backend, "max_prompt_tokens", None)
+        count = getattr(self.backend, "count_tokens", None)
+        joined = "\n\n".join(parts)
+        if limit is None or count is None:
+            return joined
+        budget = limit(max_tokens or self.max_tokens) - len(P.SYSTEM_PREAMBLE.encode())
+        if len(joined.encode()) <= budget:
+            return joined
+        budget = max(budget, 16)
+        parts = list(parts)
+        while len(parts) > 1 and count("\n\n".join(parts)) > budget:
+            parts.pop(0)
+        return P.trim_to_budget("\n\n".join(parts), lambda t: [0] * count(t), budget)
 
     # ------------------------------------------------------------------ entry points
     def _respond(self, rid: str, kind: str, prompt: str, extra: dict, max_tokens: Optional[int] = None,
                  ignore_eos: bool = False) -> AnalysisResponse:
         from ..engine import EngineOverloaded, EngineUnavailable
 
-        backend = self.routes.get(kind, self.backend)
+        backend = self.backend_for(kind)
         try:
             g = backend.generate(prompt, max_tokens=max_tokens or self.max_tokens, request_id=rid,
                                  ignore_eos=ignore_eos)
@@ -347,7 +395,7 @@ class AnalysisService:
             resp = AnalysisResponse(request_id=rid, status="success", result=result, timestamp=utcnow())
         except (EngineOverloaded, EngineUnavailable):
             raise  # admission refused: the HTTP layer answers 503 (nothing to record)
-        except FutTimeout:
+        except AnswerBudgetExceeded:
             raise  # the answer budget ran out: the HTTP layer answers 504
         except Exception as e:  # noqa: BLE001 - an engine failure becomes an error record, not a 500
             log.error("analysis %s failed: %s", rid, e)
@@ -363,7 +411,7 @@ class AnalysisService:
         rid = uuid.uuid4().hex
         ctx = context_text if context_text else self.cluster_context()
         mt = max_tokens or self.max_tokens
-        ctx = self._fit(ctx, P.build_query_prompt("", question), mt)
+        ctx = self._fit(ctx, P.build_query_prompt("", question), mt, "query")
         prompt = P.build_query_prompt(ctx, question)
         extra = {"question": question}
         try:
@@ -392,7 +440,7 @@ class AnalysisService:
         lets a caller supply the cluster state itself (e.g. another collector's snapshot)."""
         rid = uuid.uuid4().hex
         ctx = context_text if context_text else self.cluster_context()
-        ctx = self._fit(ctx, P.build_query_prompt("", question), max_tokens)
+        ctx = self._fit(ctx, P.build_query_prompt("", question), max_tokens, "query")
         prompt = P.build_query_prompt(ctx, question)
         return self._respond(rid, "query", prompt, {"question": question}, max_tokens, ignore_eos)
 
@@ -408,7 +456,7 @@ class AnalysisService:
         if kind not in ("anomaly_detection", "root_cause"):
             raise ValueError(f"unknown analysis type: {kind}")
         mt = int(params.get("max_tokens") or 0) or None
-        ctx = self._fit(self.cluster_context(), P.build_analysis_prompt(kind, "", params), mt)
+        ctx = self._fit(self.cluster_context(), P.build_analysis_prompt(kind, "", params), mt, kind)
         prompt = P.build_analysis_prompt(kind, ctx, params)
         return self._respond(uuid.uuid4().hex, kind, prompt, {"parameters": params}, mt)
 

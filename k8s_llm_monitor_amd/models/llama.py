@@ -256,13 +256,11 @@ class CausalLM:
 
     def _attn_core(self, L: dict, x: Optional[torch.Tensor], meta: AttnMeta, kv, slabs: Optional[tuple] = None,
                    rows: Optional[int] = None, rownorm: Optional[tuple] = None,
-                   rowscale: Optional[tuple] = None, fused: Optional[tuple] = None) -> torch.Tensor:
+                   rowscale: Optional[tuple] = None) -> torch.Tensor:
         """QKV projection, RoPE + KV-cache write, attention; returns the per-head output [T, Hq*D].
         ``slabs = (workspace, splits)``: decode QKV by the split-K skinny GEMM over ``x`` (row-major
         or fragment-packed with ``rows`` valid rows), reduced inside rope_and_cache; the attention
-        output is then written fragment-packed for the o_proj skinny GEMM.  ``fused = (nslabs,
-        norm_w, residual)``: ``x`` is None and the QKV GEMM builds its own normed input from the
-        previous layer's down-projection slabs (_proj_slabs)."""
+        output is then written fragment-packed for the o_proj skinny GEMM."""
         c = self.cfg
         k_cache, v_cache = kv if kv is not None else (None, None)
         partial, ns = None, 0
@@ -271,7 +269,7 @@ class CausalLM:
         cs = self.cos_sin if self.cos_sin is not None else _dummy_cs(self)
         if slabs is not None:
             ws, splits = slabs
-            ns = self._proj_slabs(L, "wqkv", x, T, splits, rownorm, fused=fused)
+            ns = self._proj_slabs(L, "wqkv", x, T, splits, rownorm)
             if self._attn_rope and not meta.is_prefill and k_cache is not None and c.arch == "llama":
                 # the attention kernel reduces the slabs, applies RoPE and writes the new k / v
                 out = ops.packed_empty(T, self.hq * self.D, self.dtype, self.device)
@@ -700,7 +698,7 @@ class CausalLM:
         control flow (and TP over gloo) is covered by the CPU tests."""
         self._skinny_ws = None
         self.lm_head_d = None
-        self._fuse_norm, self._seam, self._rc_o = False, None, 0
+        self._rc_o = 0
         for L in self.layers:  # (re)built below from the current weights
             for key in ("wqkv_d", "wo_d", "w13_d", "w2_d", "w13_dg", "w2_dg"):
                 L.pop(key, None)
@@ -761,34 +759,22 @@ class CausalLM:
     # batch-1 TPOT 3.14 vs 3.18 ms, latency_b1_rc_ab.md); at 64 rows its per-workgroup re-read of
     # the attention output cancels the gain (neutral)
     RC_O_MAX_ROWS = 32
-    # the down projection row-complete as well (K = 14336: Llama-3-8B; residual add + the next
-    # qkv's operands in its epilogue): bit-identical, but measured neutral at 1 row and 0.2-4.5 %
-    # slower at 4-32 (its waves split K, so each re-reads its slice of the activations that the
-    # slab kernel stages once per workgroup; profiles/r05/rc_down_*_ab.jsonl) - off
-    RC_DOWN = False
 
-    def set_decode_fusion(self, seam: bool = False, rc=None) -> None:
-        """Two alternatives to the decode step's add_norm_partial launches (profiles/r05/README.md;
-        both bit-compatible with the slab path; the seam is off by default, rc on for small buckets):
-
-        * ``seam`` - the add-RMSNorm runs as the first phase of the consuming GEMM (gate_up, the
-          next layer's qkv) behind an in-launch grid seam (ops.dec_gemm_fused_norm): neutral - the
-          seam's chain (slab reads, write-through stores, fan-in, A re-read) costs what the launch
-          it replaces did;
-        * ``rc`` - the o projection row-complete, residual add and the gate_up GEMM's norm operands
-          in its epilogue, no split-K slabs (ops.dec_gemm_rc): neutral - re-reading the attention
-          output from L2 in every workgroup costs what the slab round trip did at 64 rows; at 1-32
-          rows that re-read is small and rc wins 0.4-1.4 % per step, so ``rc=None`` (the
-          default) turns it on for decode buckets of at most RC_O_MAX_ROWS rows (the hipGraphs are
-          captured per bucket, so the choice is static per graph); True: every bucket; False: off.
-
-        Both need TP=1, the decode weight copies and a GPU not shared by several rank processes
-        (the seam's workgroups must be resident together)."""
+    def set_decode_fusion(self, rc=None) -> None:
+        """The row-complete o projection as the alternative to the decode step's first
+        add_norm_partial launch (profiles/r05/README.md; bit-compatible with the slab path): the o
+        projection without split-K slabs, residual add and the gate_up GEMM's norm operands in its
+        epilogue (ops.dec_gemm_rc).  At 64 rows it is neutral (re-reading the attention output
+        from L2 in every workgroup costs what the slab round trip did); at 1-32 rows it wins
+        0.4-1.4 % per step, so ``rc=None`` (the default) turns it on for decode buckets of at most
+        RC_O_MAX_ROWS rows (the hipGraphs are captured per bucket, so the choice is static per
+        graph); True: every bucket; False: off.  Needs TP=1 and the decode weight copies.
+        (Measured and removed in round 6's cleanup: the add-RMSNorm as the consuming GEMM's first
+        phase behind a grid seam - neutral to slower - and the down projection row-complete -
+        0.2-4.5 % slower at 4-32 rows; profiles/r05/README.md.)"""
         c = self.cfg
         ok = (self.tp == 1 and not c.is_moe and bool(self.layers) and "w13_d" in self.layers[0]
               and c.d_model % 512 == 0)
-        self._fuse_norm = bool(seam) and ok and not os.environ.get("K8SLLM_DEVICE")
-        self._seam = ops.SeamState(self.device) if self._fuse_norm else None
         rows = self.RC_O_MAX_ROWS if rc is None else (1 << 30 if rc is True else int(rc))
         self._rc_o = rows if ok and "wo_d" in self.layers[0] else 0
 
@@ -803,11 +789,9 @@ class CausalLM:
         M = residual.shape[0]
         # first = layer 0's (A operand, rownorm), already produced with the embedding (embed_norm_partial)
         xw, rn = first if first is not None else self._norm_tail(residual, None, 0, self.layers[0]["attn_norm"])
-        pend = None  # (nslabs, norm_w, residual): the next QKV GEMM runs the pending add-RMSNorm itself
         for i, L in enumerate(self.layers):
             kv = kv_caches[i] if kv_caches is not None else None
-            op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn, fused=pend)
-            pend = None
+            op = self._attn_core(L, xw, meta, kv, slabs=(ws, self._split_qkv), rows=M, rownorm=rn)
             rc = None
             if M <= self._rc_o and "w13_d" in L:
                 # o projection row-complete: residual += o and the gate_up GEMM's normed input in
@@ -817,20 +801,9 @@ class CausalLM:
                 xw, rn = rc
                 act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
                 ops.dec_gemm(xw, L["w13_d"], 2, M, out=act, rownorm=rn)
-                if self.RC_DOWN and i + 1 < n and "w2_d" in L and "wqkv_d" in self.layers[i + 1]:
-                    # the down projection row-complete too: residual += down and the next layer's
-                    # qkv operands in its epilogue (no slabs, no add_norm launch); None where the
-                    # kernel does not tile the shape
-                    rc = ops.dec_gemm_rc(act, L["w2_d"], M, residual, self.layers[i + 1]["attn_norm"], eps)
-                    if rc is not None:
-                        xw, rn = rc
-                        continue
                 ns = self._proj_slabs(L, "w2", act, M, self._split_d)
                 if i + 1 < n:
-                    if self._fuse_norm and "wqkv_d" in self.layers[i + 1]:
-                        pend, xw, rn = (ns, self.layers[i + 1]["attn_norm"], residual), None, None
-                    else:
-                        xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
+                    xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
                 continue
             ns = self._proj_slabs(L, "wo", op, M, self._split_o)
             if c.is_moe and self.tp > 1 and self.moe_decode == "a2a":
@@ -849,12 +822,6 @@ class CausalLM:
                 return self._logits(xr)
             if c.is_moe:
                 ns = self._moe_skinny(L, residual, ws, ns, M)
-            elif self._fuse_norm and "w13_d" in L:
-                # residual += o; the gate_up GEMM's first phase builds its own normed input
-                act = ops.packed_empty(M, self.f_local, self.dtype, self.device)
-                ops.dec_gemm_fused_norm(L["w13_d"], 2, M, residual, ws, ns, L["mlp_norm"], eps,
-                                        self._seam.counters[1], self._seam.err, out=act)
-                ns = self._proj_slabs(L, "w2", act, M, self._split_d)
             else:
                 xw, rn = self._norm_tail(residual, ws, ns, L["mlp_norm"], rows=M)
                 if "w13_d" in L:
@@ -864,9 +831,6 @@ class CausalLM:
                     act = ops.skinny_swiglu(xw, L["w13_p"], rows=M, packed_out=True, rownorm=rn)
                 ns = self._proj_slabs(L, "w2", act, M, self._split_d)
             if i + 1 < n:
-                if self._fuse_norm and not c.is_moe and "wqkv_d" in self.layers[i + 1]:
-                    pend, xw, rn = (ns, self.layers[i + 1]["attn_norm"], residual), None, None
-                    continue
                 xw, rn = self._norm_tail(residual, ws, ns, self.layers[i + 1]["attn_norm"], rows=M)
         # final norm feeds the LM head: fragment-packed for the decode GEMM (gemm_decode.hip), or
         # complete and row-major for hipBLASLt where no decode copy of the head exists
@@ -917,17 +881,11 @@ class CausalLM:
         return ops.skinny_grouped_slabs(act, L["w2_pg"], ws, M, wd[:, self.e_lo:self.e_hi].contiguous(), splits=1)
 
     def _proj_slabs(self, L: dict, key: str, x: Optional[torch.Tensor], rows: int, split: int,
-                    rownorm: Optional[tuple] = None, fused: Optional[tuple] = None) -> int:
+                    rownorm: Optional[tuple] = None) -> int:
         """Split-K slabs of a decode projection into the shared workspace: the shared-A decode
         GEMM over the packed copy ``L[key + "_d"]`` where one exists, else gemm_skinny over
-        ``L[key + "_p"]``.  ``fused = (nslabs, norm_w, residual)``: the GEMM first adds the
-        workspace's ``nslabs`` slabs to the residual and builds its own normed A (one launch,
-        ops.dec_gemm_fused_norm).  Returns the slab count."""
+        ``L[key + "_p"]``.  Returns the slab count."""
         wd = L.get(key + "_d")
-        if fused is not None:
-            nsl, norm_w, residual = fused
-            return ops.dec_gemm_fused_norm(wd, 0, rows, residual, self._skinny_ws, nsl, norm_w, self.cfg.norm_eps,
-                                           self._seam.counters[0], self._seam.err, workspace=self._skinny_ws)
         if wd is not None:
             return ops.dec_gemm(x, wd, 0, rows, workspace=self._skinny_ws, rownorm=rownorm)
         return ops.skinny_slabs(x, L[key + "_p"], self._skinny_ws, split, rows=rows, rownorm=rownorm)

@@ -395,10 +395,16 @@ class MonitorApp:
                     gen.close()  # a client that went away cancels the generation
 
             return StreamReply(200, events(), headers={"Cache-Control": "no-cache"})
+        # inline (handler thread, the engine bounds its own wait) only when nothing before the
+        # generation can block: the context is supplied or already built for this snapshot - a
+        # new snapshot's context lists events over the K8s API, so it runs under the pool's
+        # write-timeout backstop instead
+        inline = ctx_text is not None or self.analysis.context_ready()
         try:
             resp = self._bounded(lambda: self.analysis.query(question, max_tokens=mt,
                                                              ignore_eos=bool(d.get("ignore_eos", False)),
-                                                             context_text=ctx_text), kind="query")
+                                                             context_text=ctx_text),
+                                 kind="query" if inline else None)
         except _BUSY as e:
             return self._busy_reply(e)
         except FutTimeout:
@@ -411,7 +417,10 @@ class MonitorApp:
         """OpenAI-compatible generation (the wire format of the reference's ``callLLMAPI``,
         ``provider: openai``): another deployment's ``llm.routes`` entry, or a reference server
         whose ``llm.base_url`` points here, gets its answer from this server's backend.  The
-        prompt is the caller's: system message(s) then the user / assistant turns.  Non-streaming."""
+        prompt is the caller's: system message(s) then the user / assistant turns, fitted to the
+        local model's window (oldest turns dropped first).  Non-streaming: ``stream: true`` and
+        ``stop`` sequences are refused with 400 rather than silently ignored; ``top_p`` is
+        honoured."""
         _only(method, "POST")
         if self.analysis is None:
             raise http_error(503, "Analysis engine not available")
@@ -425,13 +434,20 @@ class MonitorApp:
         parts = [m["content"] for m in msgs]
         if msgs[0].get("role") == "system" and msgs[0]["content"] == P.SYSTEM_PREAMBLE:
             parts = parts[1:]  # every backend adds this server's own preamble
+        if d.get("stream") is True:
+            raise http_error(400, "stream: true is not supported on /v1/chat/completions")
+        if d.get("stop"):
+            raise http_error(400, "stop sequences are not supported")
         mt = d.get("max_tokens")
         mt = int(mt) if isinstance(mt, (int, float)) and mt > 0 else None
         temp = d.get("temperature")
         temp = float(temp) if isinstance(temp, (int, float)) else None
+        top_p = d.get("top_p")
+        top_p = float(top_p) if isinstance(top_p, (int, float)) and 0 < top_p <= 1 else None
         backend = self.analysis.backend
         try:
-            g = self._bounded(lambda: backend.generate("\n\n".join(parts), max_tokens=mt, temperature=temp))
+            prompt = self.analysis.fit_chat(parts, mt)
+            g = self._bounded(lambda: backend.generate(prompt, max_tokens=mt, temperature=temp, top_p=top_p))
         except _BUSY as e:
             return self._busy_reply(e)
         except FutTimeout:

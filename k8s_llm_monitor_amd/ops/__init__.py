@@ -1,6 +1,6 @@
 """Fused operators.  GPU tensors run the gfx950 HIP kernels of ``_k8sllm_ops`` (built in-tree by
 ``python -m k8s_llm_monitor_amd.ops.build``); CPU tensors run the fp32 references of
-:mod:`.reference`.  A GPU tensor never silently falls back: if the extension is missing on a
+:mod:`.reference` (attention: the batched SDPA forms of :mod:`.cpu_attn`, same math).  A GPU tensor never silently falls back: if the extension is missing on a
 GPU box the call raises, so tests and benchmarks always exercise the native kernels.
 """
 from __future__ import annotations
@@ -11,6 +11,7 @@ from typing import Optional
 
 import torch
 
+from . import cpu_attn
 from . import reference as ref
 
 _EXT = None
@@ -425,7 +426,7 @@ def dec_gemm(a: torch.Tensor, wp: torch.Tensor, epi: int, rows: int, workspace: 
         out.copy_(pack_activation((torch.nn.functional.silu(g) * u).to(a.dtype)))
         return 1
     rn = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
-    r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn, None, 0, None, None, None, None)
+    r = native().gemm_dec(a, wp, workspace, out, S, epi, ntw, waves, depth, M, *rn)
     if r < 0:
         raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
     return r
@@ -494,50 +495,6 @@ def dec_gemm_rc(a: torch.Tensor, wp: torch.Tensor, rows: int, residual: torch.Te
     if not native().gemm_dec_rc(a, wp, residual, norm_w, xw, ss, rows):
         return None
     return xw, (ss, eps)
-
-
-class SeamState:
-    """Device words of the fused-norm GEMMs' grid seam (gemm_decode.hip DecNorm): 8 monotonic
-    shard counters (int64, 128 B apart) per call site, and one give-up flag shared by all.
-    Zeroed once; the counters only grow, so hipGraph replays need no re-initialisation.  One
-    call site = one launch shape (every launch on a state must use the same grid)."""
-
-    def __init__(self, device, sites: int = 2):
-        self.counters = [torch.zeros(8 * 16, dtype=torch.int64, device=device) for _ in range(sites)]
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
-
-    def failed(self) -> bool:
-        """True once any seam spin gave up (a workgroup was not resident: its outputs are wrong)."""
-        return bool(self.err.item())
-
-
-def dec_gemm_fused_norm(wp: torch.Tensor, epi: int, rows: int, residual: torch.Tensor, slabs: torch.Tensor,
-                        nslabs: int, norm_w: torch.Tensor, eps: float, seam: torch.Tensor, err: torch.Tensor,
-                        workspace: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> int:
-    """add_norm_partial + dec_gemm in ONE launch: the GEMM's first phase adds the previous
-    projection's ``nslabs`` split-K slabs to ``residual`` (in place) and builds this GEMM's A
-    operand (residual * norm_w, fragment-packed) and the rows' sums of squares, handed to every
-    workgroup through a grid seam (``seam`` counters, ``err`` give-up flag: SeamState); the GEMM
-    then runs on them with the deferred 1/rms row scale.  ``slabs`` may be the same workspace the
-    GEMM's own slab epilogue writes (epi 0): every slab read precedes the seam.  Falls back to the
-    two launches where the fused one cannot run (shape, configuration, more workgroups than CUs).
-    Returns what dec_gemm returns."""
-    M, d = residual.shape[0], residual.shape[1]
-    xw = packed_empty(rows, d, residual.dtype, residual.device)
-    ss = torch.empty(rows, d // 512, dtype=torch.float32, device=residual.device)
-    if _gpu(residual) and nslabs <= 8:
-        N, K = skinny_wdims(wp)
-        cfg = dec_config(N, K, epi)
-        if cfg is not None:
-            S, ntw, waves, depth = cfg
-            r = native().gemm_dec(xw, wp, workspace, out, S, epi, ntw, waves, depth, rows, ss, float(eps), slabs,
-                                  nslabs, residual, norm_w, seam, err)
-            if r >= 0:
-                return r
-            if r != -2:
-                raise RuntimeError(f"gemm_dec: configuration {cfg} not compiled for N={N} K={K} epi={epi}")
-    add_norm_partial(residual, slabs, nslabs, norm_w, out=xw, ss_part=ss)
-    return dec_gemm(xw, wp, epi, rows, workspace=workspace, out=out, rownorm=(ss, eps))
 
 
 def add_norm_partial(residual: torch.Tensor, workspace: Optional[torch.Tensor], nslabs: int, norm_w: torch.Tensor,
@@ -770,7 +727,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
                  workspace: Optional[tuple] = None, out: Optional[torch.Tensor] = None,
                  splits: Optional[int] = None) -> torch.Tensor:
     if not _gpu(q):
-        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale)
+        r = cpu_attn.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale)
         if out is not None and out.dim() == 4:  # fragment-packed output (gemm_skinny A operand)
             r = pack_activation(r)
         return out.copy_(r) if out is not None else r
@@ -847,8 +804,8 @@ def flash_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int
     if not _gpu(qkv):
         if paged is not None:
             cs, kc, vc, bt = paged
-            return ref.paged_prefill(qkv, cu_seqlens, cs, kc, vc, bt, Hq, Hkv, D, scale)
-        return ref.flash_prefill(qkv, cu_seqlens, Hq, Hkv, D, scale)
+            return cpu_attn.paged_prefill(qkv, cu_seqlens, cs, kc, vc, bt, Hq, Hkv, D, scale)
+        return cpu_attn.flash_prefill(qkv, cu_seqlens, Hq, Hkv, D, scale)
     if qblocks is None:
         qs, st = prefill_qblocks(cu_seqlens.tolist())
         qblocks = (torch.tensor(qs, dtype=torch.int32, device=qkv.device),
@@ -1000,9 +957,12 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
     ``rowscale = (ss_part [M, K / 128] fp32, eps)`` (dense, with ``swiglu`` or ``rope``, schedule 1):
     the deferred half of an RMSNorm - every row of the product is multiplied by
     rsqrt(sum(ss_part[row]) / K + eps) before the epilogue (``x`` holds the norm's weighted input,
-    gemm_tile_resid's ``hw``)."""
+    gemm_tile_resid's ``hw``).
+    ``w`` may also be fragment-packed (pack_skinny: [N/16, K/32, 64, 8], grouped [E, ...]): the
+    decode GEMMs' layout, consumed as is (every W DMA piece one contiguous 1-KiB block)."""
     M = x.shape[0]
-    N = w.shape[-2]
+    packed = w.dim() == (5 if offsets is not None else 4)
+    N = w.shape[-4] * 16 if packed else w.shape[-2]
     if out is None:
         alloc = torch.zeros if offsets is not None else torch.empty
         out = alloc(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
@@ -1011,6 +971,8 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
     if rowscale is not None and (offsets is not None or not (swiglu or rope is not None)):
         raise ValueError("gemm_tile: the row scale is for the dense fused consumers (SwiGLU or RoPE)")
     if not _gpu(x):
+        if packed:
+            w = (torch.stack([unpack_skinny(e) for e in w]) if offsets is not None else unpack_skinny(w))
         inv = None
         if rowscale is not None:
             ssp, eps = rowscale
@@ -1039,8 +1001,8 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
                     out[a:b] = one(x[a:b], w[e])
         return out
     rs_part, rs_eps = rowscale if rowscale is not None else (None, 1e-5)
-    if rowscale is not None and algo not in (1, 2):
-        raise ValueError("gemm_tile: the row scale needs schedule 1 or the ping-pong kernel (2)")
+    if rowscale is not None and algo != 1:
+        raise ValueError("gemm_tile: the row scale needs schedule 1")
     if rope is not None:
         pos, cs, heads = rope
         native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads, rs_part, rs_eps)
@@ -1059,12 +1021,15 @@ def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_
     bf16(x @ w^T)) in place; returns ``(hw, ss)`` - hw = bf16(resid * norm_w) [M, N] and ss [M, N / 128]
     fp32 partial sums of resid^2 over each 128 columns, the operands of the consumer's row scale
     (``gemm_tile(hw, ..., rowscale=(ss, eps))`` = the projection of rms_norm(resid) * norm_w)."""
-    M, N = x.shape[0], w.shape[0]
+    M = x.shape[0]
+    N = w.shape[0] * 16 if w.dim() == 4 else w.shape[0]  # row-major or fragment-packed W
     if N % 128 or resid.shape != (M, N):
         raise ValueError("gemm_tile_resid: N % 128 == 0 and resid [M, N]")
     hw = hw if hw is not None else torch.empty_like(resid)
     ss = ss if ss is not None else torch.empty(M, N // 128, dtype=torch.float32, device=resid.device)
     if not _gpu(x):
+        if w.dim() == 4:
+            w = unpack_skinny(w)
         y = torch.nn.functional.linear(x.float(), w.float()).to(x.dtype)
         h = (y.float() + resid.float()).to(resid.dtype)
         resid.copy_(h)
@@ -1089,8 +1054,7 @@ QKV_ROPE_TILE = True  # qkv + fused RoPE on the tile kernel
 # residual-add RMSNorm folded into the o / down epilogues and the qkv / gate_up row scale
 FUSED_NORM = True
 TILE_MIN_M = 1024  # below this a 256-row tile wastes most of its MFMAs on padding rows
-# 1: the 4-wave kernel's two-barrier schedule; 2: the 8-wave ping-pong kernel (csrc/gemm_pp.hip,
-# bit-identical, 5-6 % slower at the Llama-3-8B shapes: profiles/r05/README.md)
+# 1: the 4-wave kernel's two-barrier schedule, 0: one barrier per k-tile (K < 192 only)
 TILE_ALGO = 1
 
 

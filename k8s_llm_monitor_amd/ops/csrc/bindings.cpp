@@ -22,7 +22,6 @@ int k8sllm_paged_decode(void* out, long out_stride, float* part_out, float* part
                         const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                         const int* seq_lens, int B, int Hq, int Hkv, int D, int S, float scale, hipStream_t s);
 void k8sllm_decode_tw_force(int tw);
-void k8sllm_tile_resid_nt(int v);
 int k8sllm_paged_decode_fused(void* out, long out_stride, float* part_out, float* part_ml, const float* slabs,
                               int nslabs, const int* positions, const float* cos_sin, const int* slot_mapping,
                               void* k_cache, void* v_cache, const int* block_tables, int bt_stride,
@@ -44,10 +43,11 @@ int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, in
 int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
+void k8sllm_flash_stagger(int v);
 int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E, long w_es,
                      int epi, int algo, const int* rope_pos, const float* rope_cs, int rope_heads,
                      const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw, const void* norm_w,
-                     float* ss_out, hipStream_t s);
+                     float* ss_out, int wpk, hipStream_t s);
 int k8sllm_moe_grouped_gemm(const void* X, const void* W, void* Y, const int* offsets, int E, long rows, int N, int K,
                             long w_es, int epi, hipStream_t s);
 int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
@@ -57,9 +57,7 @@ int k8sllm_gemm_skinny(const void* A, long lda, const void* Wp, float* partial, 
 int k8sllm_gemm_skinny_auto_splits(int M, int N, int K);
 int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K, int splits,
                     int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc, int rn_d, float rn_eps,
-                    const float* np_slabs, int np_S, void* np_resid, const void* np_w, void* np_seam, int* np_err,
                     int experts, long a_es, long w_es, long y_es, const float* rw, int rw_ld, hipStream_t s);
-void k8sllm_gemm_pp_sched(int sch);
 int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, const void* nw, void* xw, float* ss, int M, int N,
                        int K, hipStream_t s);
 int k8sllm_add_norm_partial(void* out, long out_stride, void* residual, const float* partial, int S, int M,
@@ -411,12 +409,16 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.is_contiguous() && y.is_contiguous(),
               "gemm_tile: x [M, K], w contiguous, y contiguous");
   const bool grouped = offsets.has_value();
-  TORCH_CHECK(w.dim() == (grouped ? 3 : 2), "gemm_tile: w [N, K] (dense) or [E, N, K] (grouped)");
+  // w row-major [N, K] / [E, N, K], or fragment-packed [N/16, K/32, 64, 8] / [E, ...] (pack_skinny)
+  const bool wpk = w.dim() == (grouped ? 5 : 4);
+  TORCH_CHECK(w.dim() == (grouped ? 3 : 2) || (wpk && w.size(-2) == 64 && w.size(-1) == 8),
+              "gemm_tile: w [N, K] (dense) or [E, N, K] (grouped), or their fragment-packed forms");
   const int E = grouped ? (int)w.size(0) : 1;
-  const int N = (int)w.size(w.dim() - 2), K = (int)w.size(w.dim() - 1);
+  const int N = wpk ? (int)w.size(w.dim() - 4) * 16 : (int)w.size(w.dim() - 2);
+  const int K = wpk ? (int)w.size(w.dim() - 3) * 32 : (int)w.size(w.dim() - 1);
   const int M = (int)x.size(0);
   TORCH_CHECK(x.size(1) == K, "gemm_tile: K mismatch");
-  TORCH_CHECK(algo >= 0 && algo <= 2, "gemm_tile: algo 0 (one barrier per k-tile), 1 (two) or 2 (8-wave ping-pong)");
+  TORCH_CHECK(algo >= 0 && algo <= 1, "gemm_tile: algo 0 (one barrier per k-tile) or 1 (two)");
   TORCH_CHECK(N % 16 == 0 && K % 64 == 0 && K >= 64 && (!swiglu || N % 256 == 0),
               "gemm_tile: N % 16 == 0 (SwiGLU: % 256), K % 64 == 0");
   TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (swiglu ? N / 2 : N), "gemm_tile: y shape");
@@ -467,7 +469,8 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
   check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), rsd ? resid->data_ptr() : y.data_ptr(), M, N, K, op, E,
                          (long)N * K, epi, (int)algo, rp, rc, (int)rope_heads, rsp, rs_np, (float)rs_eps,
                          rsd ? resid->data_ptr() : nullptr, rsd ? hw->data_ptr() : nullptr,
-                         rsd ? norm_w->data_ptr() : nullptr, rsd ? ss_out->data_ptr<float>() : nullptr, cur()),
+                         rsd ? norm_w->data_ptr() : nullptr, rsd ? ss_out->data_ptr<float>() : nullptr, wpk ? 1 : 0,
+                         cur()),
         "gemm_tile");
 }
 
@@ -579,18 +582,9 @@ int64_t gemm_skinny(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tens
 // returns S = splits; epi 1: y [M, N] bf16 (row stride y.stride(0)); epi 2: packed SwiGLU
 // y [ceil(M/16), N/64, 64, 8].  Returns the slab count (1 for epi 1/2); -1 if the configuration
 // is not available (the caller falls back to gemm_skinny).
-//
-// Fused add-RMSNorm prologue (np_slabs given; gemm_decode.hip DecNorm): the launch first reduces
-// np_nslabs fp32 slabs [S][M][K] into the bf16 residual [M][K] (in place) and WRITES a (resid *
-// np_w, fragment-packed) and rn_ss ([M][K/512] sums of squares) before its GEMM reads them, through
-// a grid seam on np_seam (>= 8 x 16 int64, zeroed once, one per call site).  np_err (int32 [1])
-// turns 1 if a seam spin gave up.  Returns -2 when the prologue cannot run for this launch (grid
-// larger than the CU count, shape, configuration): the caller then runs add_norm_partial first.
 int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor> partial, c10::optional<torch::Tensor> y,
                  int64_t splits, int64_t epi, int64_t ntw, int64_t waves, int64_t depth, int64_t rows,
-                 c10::optional<torch::Tensor> rn_ss, double rn_eps, c10::optional<torch::Tensor> np_slabs,
-                 int64_t np_nslabs, c10::optional<torch::Tensor> np_resid, c10::optional<torch::Tensor> np_w,
-                 c10::optional<torch::Tensor> np_seam, c10::optional<torch::Tensor> np_err) {
+                 c10::optional<torch::Tensor> rn_ss, double rn_eps) {
   dev_bf16(a, "a"); dev_bf16(wp, "wp");
   TORCH_CHECK(wp.dim() == 4 && wp.is_contiguous() && wp.size(2) == 64 && wp.size(3) == 8,
               "gemm_dec: wp must be fragment-packed [N/16, K/32, 64, 8]");
@@ -623,35 +617,8 @@ int64_t gemm_dec(torch::Tensor a, torch::Tensor wp, c10::optional<torch::Tensor>
   const float* rp = nullptr;
   int rn_nc = 0;
   rownorm_args(rn_ss, M, K, rp, rn_nc);
-  const float* nsp = nullptr;
-  void *nrp = nullptr, *nsm = nullptr;
-  const void* nwp = nullptr;
-  int* nerr = nullptr;
-  if (np_slabs.has_value()) {
-    TORCH_CHECK(np_slabs->is_cuda() && np_slabs->scalar_type() == torch::kFloat32 && np_slabs->is_contiguous() &&
-                    np_slabs->numel() >= np_nslabs * M * K && np_nslabs >= 1,
-                "gemm_dec: np_slabs must be contiguous fp32 with nslabs x M x K elements");
-    TORCH_CHECK(np_resid.has_value() && np_w.has_value() && np_seam.has_value() && np_err.has_value() &&
-                    rp != nullptr, "gemm_dec: the fused norm needs resid, w, seam, err and rn_ss");
-    dev_bf16(*np_resid, "np_resid");
-    dev_bf16(*np_w, "np_w");
-    TORCH_CHECK(np_resid->dim() == 2 && np_resid->is_contiguous() && np_resid->size(0) >= M && np_resid->size(1) == K,
-                "gemm_dec: np_resid [M, K]");
-    TORCH_CHECK(np_w->numel() == K && np_w->is_contiguous(), "gemm_dec: np_w [K]");
-    TORCH_CHECK(np_seam->is_cuda() && np_seam->scalar_type() == torch::kInt64 && np_seam->numel() >= 8 * 16,
-                "gemm_dec: np_seam int64 [>= 128]");
-    TORCH_CHECK(np_err->is_cuda() && np_err->scalar_type() == torch::kInt32 && np_err->numel() >= 1,
-                "gemm_dec: np_err int32 [1]");
-    nsp = np_slabs->data_ptr<float>();
-    nrp = np_resid->data_ptr();
-    nwp = np_w->data_ptr();
-    nsm = np_seam->data_ptr();
-    nerr = np_err->data_ptr<int>();
-  }
   const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, ldy, M, N, K, (int)splits, (int)epi, (int)ntw,
-                                 (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, nsp, (int)np_nslabs, nrp, nwp,
-                                 nsm, nerr, 1, 0, 0, 0, nullptr, 0, cur());
-  if (rc == -6) return -2;
+                                 (int)waves, (int)depth, rp, rn_nc, K, (float)rn_eps, 1, 0, 0, 0, nullptr, 0, cur());
   if (rc < 0) return -1;
   check(rc, "gemm_dec");
   return epi == 0 ? splits : 1;
@@ -704,8 +671,7 @@ int64_t gemm_dec_grouped(torch::Tensor a, torch::Tensor wp, c10::optional<torch:
     y_es = y->stride(0);
   }
   const int rc = k8sllm_gemm_dec(a.data_ptr(), wp.data_ptr(), pp, yp, 0, M, N, K, (int)splits, (int)epi, (int)ntw,
-                                 (int)waves, (int)depth, nullptr, 0, K, 0.f, nullptr, 0, nullptr, nullptr, nullptr,
-                                 nullptr, E, a_es, w_es, y_es, rw, rw_ld, cur());
+                                 (int)waves, (int)depth, nullptr, 0, K, 0.f, E, a_es, w_es, y_es, rw, rw_ld, cur());
   if (rc < 0) return -1;
   check(rc, "gemm_dec_grouped");
   return epi == 0 ? (int64_t)E * splits : 1;
@@ -986,7 +952,6 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("paged_decode", &paged_decode);
   m.def("paged_decode_fused", &paged_decode_fused);
   m.def("decode_tw_force", [](int64_t tw) { k8sllm_decode_tw_force((int)tw); });
-  m.def("tile_resid_nt", [](int64_t v) { k8sllm_tile_resid_nt((int)v); });
   m.def("flash_prefill", &flash_prefill);
   m.def("embed_norm_partial", &embed_norm_partial);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("top_p"),
@@ -998,10 +963,10 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
+  m.def("flash_stagger", [](int64_t v) { k8sllm_flash_stagger((int)v); });
   m.def("gemm_dec", &gemm_dec);
   m.def("gemm_dec_grouped", &gemm_dec_grouped);
   m.def("gemm_dec_rc", &gemm_dec_rc);
-  m.def("gemm_pp_sched", [](int64_t sch) { k8sllm_gemm_pp_sched((int)sch); });
   m.def("reduce_add_rms_norm", &reduce_add_rms_norm);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("add_norm_partial", &add_norm_partial);

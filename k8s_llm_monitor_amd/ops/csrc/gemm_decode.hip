@@ -31,30 +31,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum { DEC_SLAB = 0, DEC_BF16 = 1, DEC_SWIGLU8 = 2 };
 
-// Fused add-RMSNorm prologue (NP): the residual add + deferred-norm operands that
-// add_norm_partial_kernel (gemm_skinny.hip) computes as its own launch between two decode GEMMs
-// become this GEMM's first phase.  Every workgroup reduces a share of the previous projection's
-// split-K slabs into the residual stream and writes its share of this GEMM's A operand (resid * w,
-// fragment-packed) and of the per-512-column sums of squares; a grid-wide seam then hands A to
-// every workgroup.  One launch and one kernel boundary fewer per norm, and the seam's latency runs
-// beside this kernel's own start instead of a whole launch ramp.
-//
-// Seam protocol (MI355X_MICROARCH.md "Valid forms", table row 1; cdna_hip_programming.md G16):
-// every storing wave writes its A / sums-of-squares bytes write-through (sc1) and drains them
-// (s_waitcnt vmcnt(0)); a workgroup barrier; ONE lane adds 1 to its XCD-shard counter (agent
-// scope, 64-bit, monotonic: never reset, so graph replays need no re-initialisation); lanes 0-7 of
-// wave 0 poll the 8 shards (sc1 loads) until each holds this launch's target; a barrier; every
-// load of the handed-off bytes is an sc1 buffer load.  All workgroups must be resident at once
-// (the host launches at most one per CU); every spin is bounded and reports through `err`.
-struct DecNorm {
-  const float* slabs;          // [S][M][K] fp32 split-K partials of the previous projection
-  int S;
-  bf16_t* resid;               // [M][K] residual stream (bf16), updated in place
-  const bf16_t* w;             // [K] RMSNorm weight
-  unsigned long long* seam;    // 8 shard counters, 128 B apart (zeroed once, monotonic)
-  int* err;                    // set to 1 when a seam spin gives up (a non-resident workgroup)
-};
-
 // Grouped launches (MoE experts, grid.z = local expert e): A, W and the SWIGLU8 output advance by
 // a per-expert stride; SLAB partials land in slab e * S + split, scaled by the routing weight
 // rw[row * rw_ld + e] (0 where the row did not pick the expert), so the residual-add kernel's slab
@@ -65,16 +41,12 @@ struct DecGroup {
   int rw_ld;
 };
 
-constexpr int kSeamStride = 16;  // u64 words between shard counters (128 B)
-constexpr unsigned kSeamSpins = 1u << 22;
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dec_rsrc(const void* base, long bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   const int nb = __builtin_amdgcn_readfirstlane((int)min(bytes, 0x7fffffffL));
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
 }
-constexpr int kSC1 = 16;  // buffer-op aux bits: sc1 (write-through stores / L1-bypassing loads)
 constexpr int kRnMax = 4;   // narrow deferred-norm rows: up to 16 partials (4 per thread)
 constexpr int kRnWide = 16;  // wide rows: up to 256 partials (16 x 16 B per thread)
 
@@ -87,11 +59,11 @@ struct DecGeom {
   static constexpr int NLD = (PIECES + 64 * WAVES - 1) / (64 * WAVES);  // staging loads per thread
 };
 
-template <int MT, int NTW, int WAVES, int EPI, int DEPTH, bool NP, bool RNW = false>
+template <int MT, int NTW, int WAVES, int EPI, int DEPTH, bool RNW = false>
 __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, float* __restrict__ partial,
     bf16_t* __restrict__ Y, long ldy, int M, int N, int K, int kchunk, const float* __restrict__ rn_ss, int rn_nc,
-    float rn_inv_d, float rn_eps, DecNorm np, DecGroup grp) {
+    float rn_inv_d, float rn_eps, DecGroup grp) {
   using G = DecGeom<MT, WAVES>;
   const int ex = blockIdx.z;  // expert of a grouped launch (0 otherwise)
   A += ex * grp.a_es;
@@ -107,16 +79,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
   const int niter = nsteps / ITER;
   const int tile0 = (blockIdx.x * WAVES + wave) * NTW;  // this wave's first n-tile
 
-  // A (and the row sums of squares) written by this launch's own norm phase are read by sc1
-  // loads only (the seam protocol); otherwise plain loads
-  const __amdgpu_buffer_rsrc_t a_rs = dec_rsrc(A, (long)MT * 16 * K * 2);
-
   // ---- weight stream: DEPTH k-steps x NTW fragments in flight per wave, filled after chunk 0's
-  // staging loads (below).  (With NP, filling it before the norm phase - the weights do not depend
-  // on it - measured SLOWER: gate_up 49.9 vs 45.7 us, the ring's HBM loads queue ahead of the
-  // L2-resident slab loads the norm phase waits for; and filling it after the norm phase, beside
-  // the seam wait, too: 6.19 vs 6.01 ms per 64-row decode step - the early workgroups' ring loads
-  // slow the late ones' norm phase, which the seam waits for; profiles/r05/README.md.)
+  // staging loads (below)
   const u32x4* wp[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
@@ -129,88 +93,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
       for (int t = 0; t < NTW; ++t) wr[d][t] = __builtin_nontemporal_load(wp[t] + d * 64);
   };
 
-  // ---- NP: the fused add-RMSNorm phase and the grid seam (see DecNorm)
-  if constexpr (NP) {
-    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
-    const int cpr = K >> 9;  // 512-column chunks per row: one wave each
-    const int c = bid + wave * nwg;
-    if (c < M * cpr) {
-      const int row = c / cpr, chunk = c - row * cpr;
-      const int col = chunk * 512 + lane * 8;
-      bf16_t* rr = np.resid + (long)row * K + col;
-      // one memory round trip: residual, weight and every slab (np.S <= 8, host-checked; past S
-      // the last slab is re-read and masked) are issued before the first wait
-      f32x4 pa[8], pb[8];
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const float* p = np.slabs + ((long)min(s, np.S - 1) * M + row) * K + col;
-        pa[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-        pb[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
-      }
-      const uint4 wv = *reinterpret_cast<const uint4*>(np.w + col);
-      const uint4 rv = *reinterpret_cast<const uint4*>(rr);
-      float acc[8];
-      unpack8(rv, acc);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        if (s < np.S) {
-          acc[0] += pa[s].x; acc[1] += pa[s].y; acc[2] += pa[s].z; acc[3] += pa[s].w;
-          acc[4] += pb[s].x; acc[5] += pb[s].y; acc[6] += pb[s].z; acc[7] += pb[s].w;
-        }
-      }
-      const uint4 q = pack8(acc);  // the residual stream is bf16: round, then norm (add_norm_partial)
-      float v[8], wf[8], o[8];
-      unpack8(q, v);
-      unpack8(wv, wf);
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ss += v[j] * v[j];
-        o[j] = v[j] * wf[j];
-      }
-      const uint4 xo = pack8(o);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{xo.x, xo.y, xo.z, xo.w}, a_rs,
-                                             (uint32_t)(act_index(row, col, -(long)(K >> 5)) * 2), 0, kSC1);
-      *reinterpret_cast<uint4*>(rr) = q;  // read by the next launch only: plain
-      ss = wave_sum(ss);
-      if (lane == 0) {
-        const __amdgpu_buffer_rsrc_t ss_rs = dec_rsrc(rn_ss, (long)M * cpr * 4);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss), ss_rs, (uint32_t)((row * cpr + chunk) * 4), 0, kSC1);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // the arrival stays behind the barrier
-    if (wave == 0) {
-      unsigned long long tgt = 0;
-      if (lane == 0) {  // arrive: this workgroup's shard; this launch's target per shard follows from the ticket
-        const int sh = bid & 7;
-        const unsigned long long nin = (unsigned long long)((nwg - sh + 7) >> 3);
-        const unsigned long long v =
-            __hip_atomic_fetch_add(np.seam + sh * kSeamStride, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tgt = v / nin + 1;  // launches completed on this state, including this one
-      }
-      tgt = __shfl(tgt, 0, kWave);
-      if (lane < 8) {
-        const unsigned long long need = tgt * (unsigned long long)((nwg - lane + 7) >> 3);
-        const __amdgpu_buffer_rsrc_t sm = dec_rsrc(np.seam, 8 * kSeamStride * 8);
-        bool ok = false;
-        for (unsigned spins = 0;; ++spins) {
-          // one 8-byte load per shard: an untorn 64-bit value
-          const auto x = __builtin_amdgcn_raw_buffer_load_b64(sm, (uint32_t)(lane * kSeamStride * 8), 0, kSC1);
-          ok = (((unsigned long long)x[1] << 32) | x[0]) >= need;
-          if (__all(ok) || spins >= kSeamSpins) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (!ok) __hip_atomic_store(np.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // no load of A is moved above the seam (s_barrier is no memory op)
-  }
-
   // ---- the A rows' partial sums of squares (deferred RMSNorm), 4 threads per row, loaded first so
-  // their wait below is a counted one (the NP seam: sc1 loads).  Narrow rows (<= 16 partials:
+  // their wait below is a counted one.  Narrow rows (<= 16 partials:
   // add_norm_partial's per-512-column sums) one float per load; wide rows (16 | partials <= 256:
   // gemm_dec_rc_kernel's per-16-column sums) 16-byte loads, each thread a quarter of the row.
   // (RNW: the wide form, a compile-time choice - the host picks the instantiation by rn_nc)
@@ -224,16 +108,14 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
 #pragma unroll
       for (int j = 0; j < kRnMax; ++j) {
         const uint32_t off = (uint32_t)((row * rn_nc + min(part + 4 * j, rn_nc - 1)) * 4);
-        rnv[j] = __uint_as_float(NP ? __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, kSC1)
-                                    : __builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, 0));
+        rnv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ss_rs, off, 0, 0));
       }
     } else {
       const int q = rn_nc >> 2;  // this thread's quarter: floats part*q .. part*q + q - 1
 #pragma unroll
       for (int j = 0; j < (RNW ? kRnWide : 1); ++j) {
         const uint32_t off = (uint32_t)((row * rn_nc + part * q + min(4 * j, q - 4)) * 4);
-        rnw[j] = __builtin_bit_cast(f32x4, NP ? __builtin_amdgcn_raw_buffer_load_b128(ss_rs, off, 0, kSC1)
-                                              : __builtin_amdgcn_raw_buffer_load_b128(ss_rs, off, 0, 0));
+        rnw[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ss_rs, off, 0, 0));
       }
     }
   }
@@ -246,14 +128,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm_dec_kernel(
       // threads past the chunk (waves that do not divide it) repeat its last piece: every load
       // unconditional, so the counted vmcnt waits stay exact
       const int p = min((int)threadIdx.x + i * 64 * WAVES, G::PIECES - 1);
-      {
-        const int mt = p / (kDecCH * 64), j = (p >> 6) % kDecCH, ln = p & 63;
-        const long e = (((long)mt * ksteps + kb + c * kDecCH + j) * 64 + ln) * 8;
-        if constexpr (NP)
-          stg[i] = __builtin_amdgcn_raw_buffer_load_b128(a_rs, (uint32_t)(e * 2), 0, kSC1);
-        else
-          stg[i] = *reinterpret_cast<const u32x4*>(A + e);
-      }
+      const int mt = p / (kDecCH * 64), j = (p >> 6) % kDecCH, ln = p & 63;
+      const long e = (((long)mt * ksteps + kb + c * kDecCH + j) * 64 + ln) * 8;
+      stg[i] = *reinterpret_cast<const u32x4*>(A + e);
     }
   };
   auto stage_store = [&](int c) {
@@ -500,17 +377,12 @@ using namespace k8sllm;
 // (ceil((N / 16) / (ntw * waves)), splits) - the last workgroup may hold fewer n-tiles.  depth: weight k-steps in flight per wave.
 // Returns 0, or a negative code when the shape / configuration is not supported (the caller then
 // uses gemm_skinny).
-// np_slabs != nullptr: the fused add-RMSNorm prologue (DecNorm): A and rn_ss are OUTPUTS of the
-// launch's first phase (A = resid * w fragment-packed, rn_ss = [M][K/512] sums of squares of the
-// updated residual) - returns -6 when the grid would not be resident (more workgroups than CUs) or
-// the shape is outside the prologue's tiling, so the caller keeps the separate add_norm launch.
 extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, void* Y, long ldy, int M, int N, int K,
                                int splits, int epi, int ntw, int waves, int depth, const float* rn_ss, int rn_nc,
-                               int rn_d, float rn_eps, const float* np_slabs, int np_S, void* np_resid,
-                               const void* np_w, void* np_seam, int* np_err, int experts, long a_es, long w_es,
+                               int rn_d, float rn_eps, int experts, long a_es, long w_es,
                                long y_es, const float* rw, int rw_ld, hipStream_t s) {
   if (M <= 0) return 0;
-  if (experts < 1 || (experts > 1 && np_slabs != nullptr) || (rw != nullptr && epi != DEC_SLAB)) return -1;
+  if (experts < 1 || (rw != nullptr && epi != DEC_SLAB)) return -1;
   if (M > 64 || N % 16 || K % 32 || splits < 1 || K % splits) return -1;
   const int ntiles = N / 16, nwg_tiles = ntw * waves;
   const int kchunk = K / splits;
@@ -520,30 +392,15 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
   const float inv_d = rn_d > 0 ? 1.f / (float)rn_d : 0.f;
   const int MT = (M + 15) / 16;
   const dim3 grid((ntiles + nwg_tiles - 1) / nwg_tiles, splits, experts), blk(64 * waves);
-  const bool np = np_slabs != nullptr;
-  if (np) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return -6;
-    }
-    const long nwg = (long)grid.x * grid.y;
-    if (nwg > cus || K % 512 || (long)M * (K / 512) > nwg * waves || np_S < 1 || np_S > 8 || rn_ss == nullptr ||
-        rn_nc != K / 512 || np_resid == nullptr || np_w == nullptr || np_seam == nullptr || np_err == nullptr)
-      return -6;
-  }
-  const DecNorm dn{np_slabs, np_S, (bf16_t*)np_resid, (const bf16_t*)np_w, (unsigned long long*)np_seam, np_err};
   const DecGroup dg{a_es, w_es, y_es, rw, rw_ld};
   int rc = -5;
   const bool rnw = rn_ss != nullptr && rn_nc > 4 * kRnMax;  // the wide deferred-norm form (gemm_dec_rc sums)
-  if (rnw && (rn_nc % 16 || rn_nc > 16 * kRnWide || np)) return -1;
-#define K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, RW)                                                                 \
-  hipLaunchKernelGGL((gemm_dec_kernel<MTV, NTWV, WV, EPV, DV, NPV, RW>), grid, blk, 0, s, (const bf16_t*)A,          \
-                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kchunk, rn_ss, rn_nc, inv_d, rn_eps, dn, dg); \
+  if (rnw && (rn_nc % 16 || rn_nc > 16 * kRnWide)) return -1;
+#define K8S_DEC_W(MTV, NTWV, WV, EPV, DV, RW)                                                                       \
+  hipLaunchKernelGGL((gemm_dec_kernel<MTV, NTWV, WV, EPV, DV, RW>), grid, blk, 0, s, (const bf16_t*)A,               \
+                     (const bf16_t*)Wp, partial, (bf16_t*)Y, ldy, M, N, K, kchunk, rn_ss, rn_nc, inv_d, rn_eps, dg);     \
   rc = 0
-#define K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, NPV) K8S_DEC_NPW(MTV, NTWV, WV, EPV, DV, NPV, false)
-#define K8S_DEC(MTV, NTWV, WV, EPV, DV) K8S_DEC_NP(MTV, NTWV, WV, EPV, DV, false)
+#define K8S_DEC(MTV, NTWV, WV, EPV, DV) K8S_DEC_W(MTV, NTWV, WV, EPV, DV, false)
 #define K8S_DEC_M(NTWV, WV, EPV, DV) \
   switch (MT) {                      \
     case 1: K8S_DEC(1, NTWV, WV, EPV, DV); break; \
@@ -551,35 +408,16 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
     case 3: K8S_DEC(3, NTWV, WV, EPV, DV); break; \
     default: K8S_DEC(4, NTWV, WV, EPV, DV); break; \
   }
-#define K8S_DEC_MNP(NTWV, WV, EPV, DV) \
-  switch (MT) {                        \
-    case 1: K8S_DEC_NP(1, NTWV, WV, EPV, DV, true); break; \
-    case 2: K8S_DEC_NP(2, NTWV, WV, EPV, DV, true); break; \
-    case 3: K8S_DEC_NP(3, NTWV, WV, EPV, DV, true); break; \
-    default: K8S_DEC_NP(4, NTWV, WV, EPV, DV, true); break; \
-  }
-  if (np) {  // the fused-norm consumers: qkv (slabs) and gate_up (SwiGLU) of Llama-3 decode
-    if (epi == DEC_SLAB && ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_MNP(1, 6, DEC_SLAB, 8) }
-    else if (epi == DEC_SLAB && ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_MNP(1, 8, DEC_SLAB, 8) }
-    else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_MNP(1, 7, DEC_SWIGLU8, 8) }
-    else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_MNP(1, 7, DEC_SWIGLU8, 16) }
-#undef K8S_DEC_MNP
-    if (rc) return -6;
-    return (int)hipGetLastError();
-  }
-  if (rnw) {  // consumers of gemm_dec_rc's per-16-column partials: gate_up (behind o) and qkv (behind down)
+  if (rnw) {  // consumers of gemm_dec_rc's per-16-column partials: gate_up behind the row-complete o
 #define K8S_DEC_MW(NTWV, WV, EPV, DV) \
   switch (MT) {                       \
-    case 1: K8S_DEC_NPW(1, NTWV, WV, EPV, DV, false, true); break; \
-    case 2: K8S_DEC_NPW(2, NTWV, WV, EPV, DV, false, true); break; \
-    case 3: K8S_DEC_NPW(3, NTWV, WV, EPV, DV, false, true); break; \
-    default: K8S_DEC_NPW(4, NTWV, WV, EPV, DV, false, true); break; \
+    case 1: K8S_DEC_W(1, NTWV, WV, EPV, DV, true); break; \
+    case 2: K8S_DEC_W(2, NTWV, WV, EPV, DV, true); break; \
+    case 3: K8S_DEC_W(3, NTWV, WV, EPV, DV, true); break; \
+    default: K8S_DEC_W(4, NTWV, WV, EPV, DV, true); break; \
   }
     if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 8) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 8) }
     else if (epi == DEC_SWIGLU8 && ntw == 1 && waves == 7 && depth == 16) { K8S_DEC_MW(1, 7, DEC_SWIGLU8, 16) }
-    // the next layer's qkv behind a row-complete down projection
-    else if (epi == DEC_SLAB && ntw == 1 && waves == 6 && depth == 8) { K8S_DEC_MW(1, 6, DEC_SLAB, 8) }
-    else if (epi == DEC_SLAB && ntw == 1 && waves == 8 && depth == 8) { K8S_DEC_MW(1, 8, DEC_SLAB, 8) }
 #undef K8S_DEC_MW
     if (rc) return rc;
     return (int)hipGetLastError();
@@ -603,8 +441,7 @@ extern "C" int k8sllm_gemm_dec(const void* A, const void* Wp, float* partial, vo
   }
 #undef K8S_DEC_M
 #undef K8S_DEC
-#undef K8S_DEC_NP
-#undef K8S_DEC_NPW
+#undef K8S_DEC_W
   if (rc) return rc;
   return (int)hipGetLastError();
 }
@@ -618,7 +455,6 @@ extern "C" int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, co
   if (M <= 0) return 0;
   if (M > 64 || N % 32 || K % 32 || (K / 32) % 8) return -1;
   const int nks = K / 32 / 8;
-  if (nks == 56 && M > 32) return -1;  // the down projection's form: buckets of <= 32 rows
   const int MT = (M + 15) / 16;
   const dim3 grid(N / 16), blk(512);
 #define K8S_RC(MTV, DV, NK)                                                                                        \
@@ -631,12 +467,8 @@ extern "C" int k8sllm_gemm_dec_rc(const void* A, const void* Wp, void* resid, co
       case 3: K8S_RC(3, 8, 16); break;
       default: K8S_RC(4, 8, 16); break;
     }
-  } else if (nks == 56) {  // K = 14336: the down projection of Llama-3-8B (small decode buckets)
-    switch (MT) {
-      case 1: K8S_RC(1, 14, 56); break;
-      default: K8S_RC(2, 14, 56); break;
-    }
-  } else {
+  } else {  // (K = 14336, the down projection row-complete: bit-identical but 0.2-4.5 % slower per
+            // decode step at 4-32 rows, profiles/r05/rc_down_*_ab.jsonl - removed)
     return -1;
   }
 #undef K8S_RC

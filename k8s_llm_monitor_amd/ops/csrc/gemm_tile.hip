@@ -41,7 +41,14 @@
 //     `(2t + i) % 5` written inline hipcc emitted ~25 mul-hi / per-read address instructions in
 //     front of every k-tile's first MFMA; removing them made the kernel 4-5 % faster on every
 //     shape (profiles/r03/gemm_ring_addressing.jsonl).
-// Measured and removed (profiles/r03): an 8-wave 128 x 64-per-wave kernel (0.375 reads per MFMA),
+// Measured against hipBLASLt's own gfx950 256x256x64 kernel (profiles/r06/README.md): the same
+// instruction mix per k-tile (128 MFMA, 32 ds_read_b128, 16 LDS-DMA pieces); ported its schedule
+// (two whole-k-tile buffers, three barriers per k-tile, reads one per two MFMAs, its operand
+// order) and four other row swizzles - all within +-1 % of this kernel, bit-identical, removed;
+// the 5-7 % gap to it is per-tile and independent of the tile-wave count (1, 4, 16).
+// Measured and removed (profiles/r03, r05): an 8-wave 128 x 64-per-wave kernel (0.375 reads per MFMA;
+// the round-5 ping-pong form of it, bit-identical, 5-6 % slower), non-temporal residual-epilogue
+// stores (-1.9 % on o in isolation, below what an end-to-end A/B resolves),
 // a persistent form (spilled), register-staged refill (8-10 % slower: ds_write_b128 costs more
 // than the DMA issue), the same tile on v_mfma_f32_32x32x16_bf16 (1-5 % slower), unswizzled rows
 // (bank conflicts, 10-15 % slower), L1-bypass / nt cache policies and staggered per-wave issue
@@ -67,7 +74,7 @@ template <int EPI, bool GROUPED, int SCH, bool RS = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                          bf16_t* __restrict__ Y, const int* __restrict__ offsets,
                                                          int E, int M, int N, int K, long w_es, int n_mt, int n_nt,
-                                                         TileEpi ep) {
+                                                         TileEpi ep, int wpk) {
   constexpr int HS = 32768;  // one half-slot: 256 rows x 128 B
   __shared__ __attribute__((aligned(16))) char smem[5 * HS];
   const int lane = threadIdx.x & 63;
@@ -118,7 +125,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     const int cl = (lane & 7) ^ ((rl >> 1) & 7);
     soff[0][p] = (uint32_t)(((long)min(rl, mrows - 1) * K + cl * 8) * 2);  // rows past the end: clamped, never stored
     soff[1][p] = (uint32_t)(((long)min(rl, nrows - 1) * K + cl * 8) * 2);
+    if (wpk) {  // W fragment-packed [N/16][K/32][64][8]: piece = one contiguous 1-KiB block (n-tile, k-step)
+      const int blk = p * 4 + wave, j = min(blk >> 1, (nrows >> 4) - 1);
+      soff[1][p] = (uint32_t)(((long)j * (K >> 5) + (blk & 1)) * 1024 + lane * 16);
+    }
   }
+  const int kstrB = wpk ? 2048 : 128;  // bytes of W per k-tile step, in the piece's soffset
   // buffer descriptors over this tile's X rows / W rows, built from wave-uniform values only so
   // hipcc keeps them in SGPRs (no waterfall loops, cdna_hip_programming.md T20)
   auto rsrc = [](const void* base, long bytes) {
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   auto piece = [&](int o, int p, int kt, int slot) {
     char* dst = smem + slot * HS + (p * 4 + wave) * 1024;
     if (o)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)dst, 16, soff[1][p], min(kt, nk - 1) * 128, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)dst, 16, soff[1][p], min(kt, nk - 1) * kstrB, 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)dst, 16, soff[0][p], min(kt, nk - 1) * 128, 0, 0);
   };
@@ -150,8 +162,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   int rd[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) rd[ks] = (lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+  // packed W: the LDS image is the blocks verbatim, block (n-tile, k-step) at (2 n-tile + k-step) KiB:
+  // every fragment read is lane-linear (conflict-free without a swizzle)
+  int rdB[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) rdB[ks] = wpk ? ks * 1024 + lane * 16 : rd[ks];
   auto frag = [&](int slot, int ks, int o, int blk) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + rd[ks]);
+    return *reinterpret_cast<const bf16x8*>(smem + slot * HS + ((o ? wn : wm) * 8 + blk) * 2048 + (o ? rdB[ks] : rd[ks]));
   };
 
   float rs_inv = 1.f;  // RS: 1 / rms of this thread's row (threadIdx.x of the tile)
@@ -172,13 +189,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
     // by one conditional subtract per tile, and each sub-step forms ONE A and ONE B fragment base
     // VGPR (every block read is that base + an immediate).
     const uint32_t fbA0 = (uint32_t)(rd[0] + wm * 16384), fbA1 = (uint32_t)(rd[1] + wm * 16384);
-    const uint32_t fbB0 = (uint32_t)(rd[0] + wn * 16384), fbB1 = (uint32_t)(rd[1] + wn * 16384);
+    const uint32_t fbB0 = (uint32_t)(rdB[0] + wn * 16384), fbB1 = (uint32_t)(rdB[1] + wn * 16384);
     auto rd16 = [&](uint32_t base, int blk) -> bf16x8 {
       return *reinterpret_cast<const bf16x8*>(smem + base + blk * 2048);
     };
     auto pc = [&](int o, int p, int kt, uint32_t slot_bytes) {
       char* dst = smem + slot_bytes + (p * 4 + wave) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], min(kt, nk - 1) * 128, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? wr : xr, (lds_void_t*)dst, 16, soff[o][p], min(kt, nk - 1) * (o ? kstrB : 128),
+                                               0, 0);
     };
     // PM (the ring tail, peeled): 0 = B_{t+2} and A_{t+3} refills; 1 = B_{t+2} only (A_{t+3} is
     // past the end); 2 = no refill; 3 = no refill and, in (t, 1), no reads of tile t+1 (there is
@@ -429,13 +447,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
       }
       const uint4 hq = pack8(h), wq = pack8(hw);
       const uint32_t off = ro + (uint32_t)(4 * b * N * 2);
-      if (ep.st_nt) {
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 2);
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 0);
-      }
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{hq.x, hq.y, hq.z, hq.w}, rres, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{wq.x, wq.y, wq.z, wq.w}, rhw, off, 0, 0);
       ss = row16_sum(ss);
       const int grow = wm * 128 + r;
       if (cc == 0 && grow < mrows) ep.ss_out[(long)(row0 + grow) * ss_np + ssc] = ss;
@@ -504,26 +517,13 @@ using namespace k8sllm;
 // Grouped: W [E][N][K] with expert stride w_es elements; M = total expert-sorted rows (the grid
 // bound: ceil(M / 256) + E m-tiles); expert e's rows are offsets[e] .. offsets[e + 1] - 1.
 // Shapes: N % 16 == 0 (SwiGLU: N % 256 == 0), K % 64 == 0.  algo: the refill schedule (0 or 1).
-extern "C" int k8sllm_gemm_pp(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
-                              long w_es, int epi, const int* rope_pos, const float* rope_cs, int rope_heads,
-                              const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw, const void* norm_w,
-                              float* ss_out, hipStream_t s);
-
-// algo 2: the 8-wave ping-pong schedule (gemm_pp.hip), same contract.
-static int g_resid_nt = 0;  // tools/bench_tile_epilogues.py: 1 = non-temporal residual-epilogue stores
-extern "C" void k8sllm_tile_resid_nt(int v) { g_resid_nt = v; }
-
+// wpk: W is fragment-packed ([E][N/16][K/32][64][8], ops.pack_skinny - the decode GEMMs' layout)
+// instead of row-major: every W DMA piece is one contiguous 1-KiB block, read lane-linear from LDS.
 extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E,
                                 long w_es, int epi, int algo, const int* rope_pos, const float* rope_cs,
                                 int rope_heads, const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw,
-                                const void* norm_w, float* ss_out, hipStream_t s) {
+                                const void* norm_w, float* ss_out, int wpk, hipStream_t s) {
   if (M <= 0) return 0;
-  if (algo == 2) {
-    if (K >= 128 && !(epi == TILE_EPI_RESID && N % 256))
-      return k8sllm_gemm_pp(X, W, Y, M, N, K, offsets, E, w_es, epi, rope_pos, rope_cs, rope_heads, rs_part, rs_np,
-                            rs_eps, resid, hw, norm_w, ss_out, s);
-    algo = 1;  // shapes the ping-pong kernel does not take: the 4-wave kernel
-  }
   const bool grouped = offsets != nullptr;
   const bool rs = rs_part != nullptr;
   if (grouped && (E < 1 || E > 256)) return -1;
@@ -542,7 +542,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
              (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
     return -1;
   const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,
-                   (const bf16_t*)norm_w, ss_out, g_resid_nt};
+                   (const bf16_t*)norm_w, ss_out};
   // 32-bit DMA offsets (X: relative to the tile's first row; W: within one expert / n-tile)
   if ((long)N * K * 2 >= (1L << 31) || 256L * K * 2 >= (1L << 31)) return -3;
   if (epi == TILE_EPI_RESID && 256L * N * 2 >= (1L << 31)) return -3;
@@ -552,7 +552,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
   const dim3 grid((unsigned)nwg);
 #define K8_TILE_LAUNCH(EPI_, G_, SCH_, RS_)                                                                          \
   hipLaunchKernelGGL((gemm_w4_kernel<EPI_, G_, SCH_, RS_>), grid, dim3(256), 0, s, (const bf16_t*)X,                \
-                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt, ep)
+                     (const bf16_t*)W, (bf16_t*)Y, offsets, E, M, N, K, w_es, n_mt, n_nt, ep, wpk)
 #define K8_TILE_SCH(SCH_)                                                                                            \
   if (grouped) {                                                                                                     \
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true, SCH_, false);                                  \

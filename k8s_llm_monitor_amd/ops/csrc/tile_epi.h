@@ -1,5 +1,5 @@
-// Fused epilogues shared by the prefill tile GEMMs (gemm_tile.hip: 4 waves, gemm_pp.hip: 8-wave
-// ping-pong): epilogue kinds, their operands, and a 16-lane row reduction.
+// Fused epilogues of the prefill tile GEMM (gemm_tile.hip): epilogue kinds, their operands, and a
+// 16-lane row reduction.
 #pragma once
 #include "common.h"
 
@@ -33,7 +33,6 @@ struct TileEpi {
   bf16_t* hw;            // RESID: [M][N] resid * norm_w
   const bf16_t* norm_w;  // RESID: [N] the next RMSNorm's weight
   float* ss_out;         // RESID: [M][N / 128]
-  int st_nt;             // RESID: non-temporal resid / hw stores (tools A/B: k8sllm_tile_resid_nt)
 };
 
 // sum over the 16 lanes of a DPP row (lanes 16r .. 16r + 15), the total in every lane

@@ -12,8 +12,8 @@ step captured in a hipGraph contains no RCCL call at all.
 
 On by default at TP 2..8 on the GPU (``K8SLLM_CUSTOM_AR=0`` keeps RCCL for everything), but only
 after a startup self-test on the actual devices is exact (``self_test``: integer-valued bf16
-all-reduces and all-gathers of several sizes against CPU-group references, exact in any summation
-order, as RCCL's are);
+all-reduces (one- and two-shot), all-gathers, all-to-alls and fused decode tails against CPU-group
+references, exact in any summation order, as RCCL's are);
 a rank that sees a mismatch or a raised error flag turns it off on every rank of the group.
 Validated on one MI355X with two processes sharing the GPU (tests/test_custom_ar.py,
 tests/test_tp_gpu.py); no multi-GPU xGMI run exists yet, which is what the self-test guards.
@@ -119,34 +119,88 @@ def enabled() -> bool:
 
 
 def self_test(car: CustomAllReduce, ps, sizes=None) -> bool:
-    """Collective over the TP group: the custom all-reduce / all-gather on the real devices against
-    exact references built over the CPU group, on integer-valued bf16 data (sums stay integers
-    < 256, exact in any summation order - what RCCL returns too).  True on every rank only if every
+    """Collective over the TP group: every custom collective the engine routes through IPC, run on
+    the real devices against exact references built over the CPU group, on integer-valued bf16
+    data (every sum stays an integer of magnitude < 256, exact in any summation order - what RCCL
+    returns too).  Covered: the all-reduce one-shot AND two-shot, the all-gather (vocab-parallel
+    logits), the all-to-all (EP decode dispatch / combine) and the fused decode tail (slab sum +
+    all-reduce + residual add + RMSNorm, one-shot and two-shot, row-major and fragment-packed: the
+    Llama-3-70B TP=8 decode hot path) - residual bit-exact, the RMSNorm output within bf16
+    rounding of the fp32 reference and one-shot == two-shot bit for bit.  A cross-device
+    visibility or ordering fault in any of them therefore turns the custom path off on every rank
+    (RCCL carries everything) instead of producing wrong tokens.  True on every rank only if every
     rank passed."""
+    from .. import ops
+
     dev = ps.device
+    world, rank, grp = car.world, ps.tp_rank, ps.cpu_group
     sizes = sizes or (8, 4096, 64 * 4096, car.max_elems)
     ok = True
+
+    def gather_cpu(t: torch.Tensor) -> list:
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t.contiguous(), group=grp)
+        return parts
+
     try:
         for n in sizes:
             n = max(8, min(int(n), car.max_elems)) // 8 * 8
             g = torch.Generator().manual_seed(7919 + n)
-            xc = (torch.randint(-8, 9, (n,), generator=g) + ps.tp_rank).to(torch.bfloat16)
+            xc = (torch.randint(-8, 9, (n,), generator=g) + rank).to(torch.bfloat16)
             x = xc.to(dev)
-            y = car.all_reduce(x)
-            m = min(n, car.max_elems // car.world // 8 * 8)
-            gat = car.all_gather(x[:m].contiguous())
-            # references over the CPU group: exact integer sums / the ranks' slices
             ref = xc.float()
-            dist.all_reduce(ref, group=ps.cpu_group)
-            gref = [torch.empty_like(xc[:m]) for _ in range(car.world)]
-            dist.all_gather(gref, xc[:m].contiguous(), group=ps.cpu_group)
+            dist.all_reduce(ref, group=grp)
+            ref = ref.to(torch.bfloat16)
+            ys = [car.all_reduce(x, algo=a) for a in (0, 1)]  # one-shot, two-shot
+            m = min(n, car.max_elems // world // 8 * 8)
+            gat = car.all_gather(x[:m].contiguous())
             torch.cuda.synchronize(dev)
-            ok = (ok and torch.equal(y.cpu(), ref.to(torch.bfloat16)) and torch.equal(gat.cpu(), torch.stack(gref))
-                  and not car.error())
+            ok = (ok and all(torch.equal(y.cpu(), ref) for y in ys)
+                  and torch.equal(gat.cpu(), torch.stack(gather_cpu(xc[:m]))) and not car.error())
+        # all-to-all: out[p] = rank p's x[this rank]
+        for blk in (8, 64 * 128):
+            if world * blk > car.max_elems:
+                continue
+            g = torch.Generator().manual_seed(31 * blk + rank)
+            xc = torch.randint(-100, 101, (world, blk), generator=g).to(torch.bfloat16)
+            got = car.all_to_all(xc.to(dev))
+            parts = gather_cpu(xc)
+            torch.cuda.synchronize(dev)
+            ok = ok and torch.equal(got.cpu(), torch.stack([parts[p][rank] for p in range(world)])) and not car.error()
+        # the fused decode tail
+        for M, d, ns, packed in ((8, 1024, 2, False), (17, 8 * 512, 2, True)):
+            if not car.fits_tail(M, d):
+                continue
+            g = torch.Generator().manual_seed(1000 * M + d + rank)
+            slabs = torch.randint(-3, 4, (ns, M, d), generator=g).float()
+            res = torch.randint(-8, 9, (M, d), generator=g).to(torch.bfloat16)
+            w = (1 + torch.randint(-4, 5, (d,), generator=g).float() / 16).to(torch.bfloat16)
+            part = slabs.sum(0).to(torch.bfloat16).reshape(-1)
+            y = torch.zeros_like(part, dtype=torch.float32)
+            for p in gather_cpu(part):  # rank order, fp32, one rounding
+                y += p.float()
+            r2 = (res.float() + y.reshape(M, d)).to(torch.bfloat16)
+            rf = r2.float()
+            ref_out = rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+            outs = []
+            for algo in ((0, 1) if d % (8 * world) == 0 else (0,)):
+                rg = res.to(dev)
+                out = (ops.packed_empty(M, d, torch.bfloat16, dev) if packed
+                       else torch.empty(M, d, dtype=torch.bfloat16, device=dev))
+                car.fused_tail(slabs.to(dev).contiguous(), ns, rg, w.to(dev), 1e-5, out, packed, algo=algo)
+                torch.cuda.synchronize(dev)
+                got = out.cpu()
+                if packed:
+                    got = ops.unpack_skinny(got.view(-1, d // 32, 64, 8))[:M]
+                err = (got.float() - ref_out).abs().max().item()
+                ok = (ok and torch.equal(rg.cpu(), r2) and err <= 2e-2 * ref_out.abs().max().item()
+                      and not car.error())
+                outs.append(got)
+            ok = ok and all(torch.equal(o, outs[0]) for o in outs)
     except Exception:  # noqa: BLE001 - any failure disables the custom path
         ok = False
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ps.cpu_group)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=grp)
     return bool(flag.item())
 
 

@@ -1,6 +1,7 @@
 """REST contract tests: every route, dev mode and FakeCluster."""
 import http.client
 import json
+import time
 import os
 import threading
 
@@ -236,6 +237,28 @@ def test_chat_completions_endpoint(mon):
     d = J(a.handle("POST", "/v1/chat/completions", body))
     assert d["object"] == "chat.completion" and d["choices"][0]["message"]["role"] == "assistant"
     assert "NotReady" in d["choices"][0]["message"]["content"] and d["usage"]["completion_tokens"] > 0
+    # streaming and stop sequences are refused, not silently ignored; top_p passes through
+    msgs = [{"role": "user", "content": "hi"}]
+    assert a.handle("POST", "/v1/chat/completions", json.dumps({"messages": msgs, "stream": True}).encode()).code == 400
+    assert a.handle("POST", "/v1/chat/completions", json.dumps({"messages": msgs, "stop": ["\n"]}).encode()).code == 400
+    assert J(a.handle("POST", "/v1/chat/completions", json.dumps({"messages": msgs, "top_p": 0.9}).encode()))["object"]
+
+
+def test_chat_prompt_fits_the_window():
+    """A chat longer than the model window keeps its latest turns (oldest dropped first)."""
+    from k8s_llm_monitor_amd.llm.service import AnalysisService
+
+    class Small:
+        def max_prompt_tokens(self, max_tokens=None):
+            return 300
+
+        def count_tokens(self, text):
+            return len(text.encode())
+
+    an = AnalysisService(Small(), max_tokens=16)
+    parts = [f"turn {i}: " + "x" * 100 for i in range(10)]
+    out = an.fit_chat(parts, 16)
+    assert out.endswith(parts[-1]) and "turn 0:" not in out and len(out.encode()) <= 300
 
 
 def test_context_fits_a_short_model_window():
@@ -321,9 +344,101 @@ def test_query_answer_budget_timeout_is_504(mon, inline):
             return len(text) // 4
 
         def generate(self, prompt, **kw):
-            raise FutTimeout("answer not ready within the answer budget")
+            if inline:  # the engine backend's own budget (LocalEngineBackend.generate)
+                raise AnswerBudgetExceeded("answer not ready within the answer budget")
+            time.sleep(3)  # the pool's write-timeout backstop (1 s here) fires first
+
+    from k8s_llm_monitor_amd.llm.service import AnswerBudgetExceeded
 
     a = mon.app
+    a.write_timeout_s = a.llm_timeout_s = 1.5
     a.analysis.backend = SlowBackend()
     r = a.handle("POST", "/api/v1/query", json.dumps({"question": "why is node-1 NotReady?"}).encode())
     assert r.code == 504, (r.code, r.body[:200])
+    assert FutTimeout is not None
+
+
+def test_routed_socket_timeout_is_an_error_record_not_504(mon):
+    """only the engine's own answer budget (AnswerBudgetExceeded) means 504.  A routed
+    backend's socket timeout - a builtin TimeoutError, the same class as the futures one on
+    Python >= 3.11 - becomes an error record (500 with the record), on every interpreter."""
+    class Upstream:
+        provider, model = "openai", "upstream"
+
+        def generate(self, prompt, **kw):
+            raise TimeoutError("timed out")
+
+    a = mon.app
+    a.analysis.routes["query"] = Upstream()
+    r = a.handle("POST", "/api/v1/query", json.dumps({"question": "why?", "context": {"cluster_state": "x"}}).encode())
+    assert r.code == 500, (r.code, r.body[:200])
+    d = J(r)
+    assert d["status"] == "error" and "TimeoutError" in d["error"]
+
+
+def test_fit_uses_the_routed_backends_window(mon):
+    """a routed analysis type is trimmed to ITS backend's window with ITS tokenizer; a
+    backend that publishes no window gets the context untrimmed."""
+    class Small:
+        provider, model = "stub", "small"
+        seen = []
+
+        def max_prompt_tokens(self, max_tokens=None):
+            return 200
+
+        def count_tokens(self, text):
+            return len(text.encode())
+
+        def generate(self, prompt, **kw):
+            self.seen.append(prompt)
+            return {"text": "ok", "model": self.model, "provider": self.provider}
+
+    class NoWindow(Small):
+        max_prompt_tokens = None
+
+    ctx = "\n".join(f"- node-{i:03d} CPU={i % 97}%" for i in range(400))
+    a = mon.app
+    small, big = Small(), NoWindow()
+    small.seen, big.seen = [], []
+    a.analysis.routes["query"] = small
+    J(a.handle("POST", "/api/v1/query", json.dumps({"question": "q", "context": {"cluster_state": ctx}}).encode()))
+    assert len(small.seen[-1].encode()) < 400
+    a.analysis.routes["query"] = big
+    J(a.handle("POST", "/api/v1/query", json.dumps({"question": "q", "context": {"cluster_state": ctx}}).encode()))
+    assert ctx in big.seen[-1]
+
+
+def test_query_runs_inline_only_with_a_ready_context(mon, monkeypatch):
+    """the handler-thread (inline) path skips the write-timeout backstop, so it is taken
+    only when building the prompt cannot block on the K8s API: a supplied context or a context
+    already built for the current snapshot; otherwise the bounded pool runs the query."""
+    from k8s_llm_monitor_amd.monitor import server as S
+
+    class Eng:
+        provider, model = "stub", "stub"
+        enforces_deadline = True
+
+        def count_tokens(self, text):
+            return 1
+
+        def generate(self, prompt, **kw):
+            return {"text": "ok", "model": self.model, "provider": self.provider}
+
+    used = []
+    real = S._bounded_pool
+
+    def spy():
+        used.append(1)
+        return real()
+
+    monkeypatch.setattr(S, "_bounded_pool", spy)
+    a = mon.app
+    a.analysis.backend = Eng()
+    a.analysis._ctx_cache = (None, "")  # a new snapshot: its context is not built yet
+    assert not a.analysis.context_ready()
+    assert J(a.handle("POST", "/api/v1/query", b'{"question":"q"}'))["status"] == "success"
+    assert used == [1]  # pool path
+    assert a.analysis.context_ready()  # built by that query
+    J(a.handle("POST", "/api/v1/query", b'{"question":"q"}'))
+    J(a.handle("POST", "/api/v1/query", b'{"question":"q","context":{"cluster_state":"c"}}'))
+    assert used == [1]  # both inline

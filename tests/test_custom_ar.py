@@ -162,6 +162,15 @@ def _rank_main(rank: int, world: int, port: int, q) -> None:
             if not all(torch.equal(o.cpu(), ref) for o in souts):
                 bad.append(("graph", it))
         torch.cuda.synchronize()
+        # the startup self-test (maybe_create runs it before the engine may use the IPC path): it
+        # must pass on healthy collectives - all-reduce both forms, all-gather, all-to-all, the
+        # fused tail packed and row-major
+        from types import SimpleNamespace
+
+        from k8s_llm_monitor_amd.parallel.custom_ar import self_test
+
+        if not self_test(car, SimpleNamespace(device=torch.device("cuda", 0), tp_rank=rank, cpu_group=None)):
+            bad.append(("self_test",))
         err = car.error()
         dist.barrier()
         car.close()

@@ -163,63 +163,6 @@ def test_embed_norm_partial_matches_resolve_embed_norm(M):
     torch.testing.assert_close(ss, ss0, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("M", [1, 17, 64])
-@pytest.mark.parametrize("epi", [0, 2])
-def test_dec_fused_norm_matches_two_launches(M, epi):
-    """ops.dec_gemm_fused_norm (the add-RMSNorm as the GEMM's first phase, grid seam) against
-    add_norm_partial + dec_gemm: the same arithmetic in the same order, so the residual, the
-    slabs / SwiGLU output must be BIT-identical - over 12 back-to-back launches on one seam state
-    with fresh slabs each time (a stale hand-off would reuse the previous launch's A), and against
-    an fp32 reference of the normed product."""
-    d, eps = 4096, 1e-5
-    N = 6144 if epi == 0 else 2 * 14336
-    S_in = 8
-    g = torch.Generator(device=DEV).manual_seed(M * 7 + epi)
-    w = (torch.randn(N, d, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
-    wp = ops.pack_skinny(ops.interleave_gate_up8(w) if epi == 2 else w)
-    norm_w = (1 + 0.1 * torch.randn(d, device=DEV, generator=g)).to(torch.bfloat16)
-    seam = ops.SeamState(DEV)
-    S_out = ops.dec_config(N, d, epi)[0]
-    for it in range(12):
-        resid0 = torch.randn(M, d, device=DEV, generator=g).to(torch.bfloat16)
-        slabs = torch.randn(S_in * M * d, device=DEV, generator=g) * 0.5
-        # fused: the slab workspace doubles as the GEMM's output workspace (as in the engine)
-        ws_f = torch.zeros(max(S_in, S_out) * M * max(N, d), device=DEV)
-        ws_f[: S_in * M * d] = slabs
-        r_f = resid0.clone()
-        out_f = ops.packed_empty(M, N // 2, torch.bfloat16, DEV) if epi == 2 else None
-        ns = ops.dec_gemm_fused_norm(wp, epi, M, r_f, ws_f, S_in, norm_w, eps, seam.counters[epi // 2], seam.err,
-                                     workspace=ws_f if epi == 0 else None, out=out_f)
-        # reference: two launches
-        ws_r = torch.zeros_like(ws_f)
-        ws_r[: S_in * M * d] = slabs
-        r_r = resid0.clone()
-        xw, ss = ops.add_norm_partial(r_r, ws_r, S_in, norm_w)
-        out_r = ops.packed_empty(M, N // 2, torch.bfloat16, DEV) if epi == 2 else None
-        ws_o = torch.zeros_like(ws_f)
-        ns_r = ops.dec_gemm(xw, wp, epi, M, workspace=ws_o if epi == 0 else None, out=out_r, rownorm=(ss, eps))
-        torch.cuda.synchronize()
-        assert not seam.failed()
-        assert ns == ns_r
-        assert torch.equal(r_f, r_r), f"residual differs at launch {it}"
-        if epi == 0:
-            assert torch.equal(ws_f[: ns * M * N], ws_o[: ns * M * N]), f"slabs differ at launch {it}"
-            y = ws_f[: ns * M * N].view(ns, M, N).sum(0)
-        else:
-            assert torch.equal(ops.unpack_skinny(out_f)[:M], ops.unpack_skinny(out_r)[:M]), f"swiglu differs {it}"
-    # fp32 reference of the last launch
-    h = (resid0.float() + slabs.view(S_in, M, d).sum(0)).to(torch.bfloat16).float()
-    xn = h * torch.rsqrt((h * h).mean(-1, keepdim=True) + eps) * norm_w.float()
-    ref = xn @ w.float().t()
-    # (the kernel adds the slabs to the residual in order; the reference sums the slabs first)
-    torch.testing.assert_close(r_f.float(), h, rtol=1e-2, atol=1e-2)
-    if epi == 0:
-        _check(y, ref, f"fused qkv M{M}")
-    else:
-        ref_act = F_.silu(ref[:, : N // 2].to(torch.bfloat16).float()) * ref[:, N // 2:].to(torch.bfloat16).float()
-        _check(ops.unpack_skinny(out_f)[:M], ref_act, f"fused gate_up M{M}")
-
-
 @pytest.mark.parametrize("M", [1, 17, 40, 64])
 def test_dec_rc_matches_slabs_and_norm(M):
     """ops.dec_gemm_rc (row-complete o projection: residual add + deferred-norm operands in its
@@ -261,44 +204,3 @@ def test_dec_rc_matches_slabs_and_norm(M):
     _check(ops.unpack_skinny(a_rc)[:M], ref, f"rc gate_up vs fp32 M{M}")
 
 
-@pytest.mark.parametrize("M", [1, 9, 32])
-def test_dec_rc_down_matches_slabs_and_feeds_qkv(M):
-    """The row-complete form at K = 14336 (the down projection of Llama-3-8B in decode buckets of
-    <= 32 rows): the residual and the normed A operand BIT-identical to the 8-slab path +
-    add_norm_partial (same K slices, same order), and the next layer's qkv GEMM consuming the
-    wide (256-partial) row scale within rounding of the narrow form and of fp32."""
-    d, F, eps = 4096, 14336, 1e-5
-    nq = 6144
-    g = torch.Generator(device=DEV).manual_seed(100 + M)
-    act = torch.randn(M, F, device=DEV, generator=g).to(torch.bfloat16)
-    w2 = (torch.randn(d, F, device=DEV, generator=g) * 0.01).to(torch.bfloat16)
-    w2p = ops.pack_skinny(w2)
-    resid0 = torch.randn(M, d, device=DEV, generator=g).to(torch.bfloat16)
-    nw = (1 + 0.1 * torch.randn(d, device=DEV, generator=g)).to(torch.bfloat16)
-    ap = ops.pack_activation(act)
-    for _ in range(3):
-        r_rc = resid0.clone()
-        out = ops.dec_gemm_rc(ap, w2p, M, r_rc, nw, eps)
-        assert out is not None, "K = 14336 row-complete form must be compiled"
-        xw_rc, (ss_rc, _) = out
-        ws = torch.empty(8 * M * d, device=DEV)
-        ns = ops.dec_gemm(ap, w2p, 0, M, workspace=ws, cfg=(8, 1, 8, 8))
-        r_sl = resid0.clone()
-        xw_sl, ss_sl = ops.add_norm_partial(r_sl, ws, ns, nw)
-        torch.cuda.synchronize()
-        assert torch.equal(r_rc, r_sl)
-        assert torch.equal(ops.unpack_skinny(xw_rc)[:M], ops.unpack_skinny(xw_sl)[:M])
-        torch.testing.assert_close(ss_rc.view(M, 8, 32).sum(-1), ss_sl, rtol=1e-4, atol=1e-3)
-    wq = (torch.randn(nq, d, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
-    wqp = ops.pack_skinny(wq)
-    cfg = ops.dec_config(nq, d, 0)
-    ws_rc = torch.empty(cfg[0] * M * nq, device=DEV)
-    ws_sl = torch.empty(cfg[0] * M * nq, device=DEV)
-    s1 = ops.dec_gemm(xw_rc, wqp, 0, M, workspace=ws_rc, rownorm=(ss_rc, eps))
-    s2 = ops.dec_gemm(xw_sl, wqp, 0, M, workspace=ws_sl, rownorm=(ss_sl, eps))
-    y_rc = ws_rc[: s1 * M * nq].view(s1, M, nq).sum(0)
-    y_sl = ws_sl[: s2 * M * nq].view(s2, M, nq).sum(0)
-    _check(y_rc, y_sl, f"rc vs slab qkv M{M}", tol=1e-2)
-    h = r_rc.float()
-    xn = h * torch.rsqrt((h * h).mean(-1, keepdim=True) + eps) * nw.float()
-    _check(y_rc, xn @ wq.float().t(), f"rc qkv vs fp32 M{M}")

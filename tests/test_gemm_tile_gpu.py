@@ -24,7 +24,7 @@ def _close(a, b, atol, rtol=0.0, what=""):
     assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.4g}"
 
 
-ALGOS = [0, 1, 2]  # 4-wave kernel: 0 one barrier per k-tile, 1 two; 2 the 8-wave ping-pong kernel (gemm_pp.hip)
+ALGOS = [0, 1]  # the 4-wave kernel: 0 one barrier per k-tile, 1 two
 DENSE_ALGOS = ALGOS
 
 
@@ -121,3 +121,35 @@ def test_gemm_tile_in_graph_matches_eager():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, y0)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 1536, 1024), (257, 1296, 640), (2048, 768, 4096)])
+def test_gemm_tile_packed_weights_bit_identical(M, N, K, algo):
+    """W in the decode GEMMs' fragment-packed layout (pack_skinny) gives the same bits as W
+    row-major: only the DMA source / LDS image of W change, not the MFMA operands or their order -
+    plain, SwiGLU, grouped, RoPE + row scale and the residual epilogue."""
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    assert torch.equal(ops.gemm_tile(x, ops.pack_skinny(w), algo=algo), ops.gemm_tile(x, w, algo=algo))
+    if N % 256 == 0:
+        wi = ops.interleave_gate_up(w).contiguous()
+        assert torch.equal(ops.gemm_tile(x, ops.pack_skinny(wi), swiglu=True, algo=algo),
+                           ops.gemm_tile(x, wi, swiglu=True, algo=algo))
+    counts = [M // 3, 0, M - M // 3]
+    off = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device=DEV)
+    we = torch.stack([w, w.flip(0), w * 0.5]).contiguous()
+    wep = torch.stack([ops.pack_skinny(e) for e in we]).contiguous()
+    assert torch.equal(ops.gemm_tile(x, wep, off, algo=algo), ops.gemm_tile(x, we, off, algo=algo))
+    if algo == 1 and K >= 192 and K % 128 == 0 and N % 128 == 0:
+        pos = torch.arange(M, device=DEV, dtype=torch.int32)
+        cs = ref.rope_cos_sin(4096, 128, 500000.0).to(DEV).float().contiguous()
+        ss = (torch.rand(M, K // 128, device=DEV) * 64 + 16).contiguous()
+        kw = dict(algo=1, rope=(pos, cs, N // 128), rowscale=(ss, 1e-5))
+        assert torch.equal(ops.gemm_tile(x, ops.pack_skinny(w), **kw), ops.gemm_tile(x, w, **kw))
+        resid = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        nw = (torch.rand(N, device=DEV) + 0.5).to(torch.bfloat16)
+        r1, r2 = resid.clone(), resid.clone()
+        h1, s1 = ops.gemm_tile_resid(x, ops.pack_skinny(w), r1, nw)
+        h2, s2 = ops.gemm_tile_resid(x, w, r2, nw)
+        assert torch.equal(r1, r2) and torch.equal(h1, h2) and torch.equal(s1, s2)

@@ -148,38 +148,10 @@ def test_tile_rowscale_64_partials_d8192():
 
 def _fp32_forward(model, ids, rows=None):
     """Plain fp32 forward of the same weights (no HIP kernels): logits of ``rows`` (default: the
-    last token) [len(rows), vocab]."""
-    c = model.cfg
-    T = ids.numel()
-    x = model.embed[ids.long()].float()
-    cs = model.cos_sin.float()
-    pos = torch.arange(T, device=ids.device)
-    for L in model.layers:
-        h = F_.rms_norm(x, (c.d_model,), L["attn_norm"].float(), c.norm_eps)
-        qkv = h @ L["wqkv"].float().t()
-        Hq, Hk, D = model.hq, model.hkv, model.D
-        q, k, v = qkv.split([Hq * D, Hk * D, Hk * D], 1)
-        q, k = q.view(T, Hq, D), k.view(T, Hk, D)
+    last token) [len(rows), vocab] (models/reference.py, also smoke()'s oracle)."""
+    from k8s_llm_monitor_amd.models.reference import fp32_logits
 
-        def rope(t):
-            cos, sin = cs[pos, : D // 2][:, None], cs[pos, D // 2:][:, None]
-            a, b = t[..., : D // 2], t[..., D // 2:]
-            return torch.cat([a * cos - b * sin, a * sin + b * cos], -1)
-
-        q, k = rope(q), rope(k)
-        k = k.repeat_interleave(Hq // Hk, 1)
-        vv = v.view(T, Hk, D).repeat_interleave(Hq // Hk, 1)
-        att = F_.scaled_dot_product_attention(q.transpose(0, 1)[None], k.transpose(0, 1)[None],
-                                              vv.transpose(0, 1)[None], is_causal=True)[0]
-        x = x + att.transpose(0, 1).reshape(T, Hq * D) @ L["wo"].float().t()
-        h = F_.rms_norm(x, (c.d_model,), L["mlp_norm"].float(), c.norm_eps)
-        w13 = ops.deinterleave_gate_up(L["w13"]) if model._w13_il else L["w13"]
-        gu = h @ w13.float().t()
-        F = gu.shape[1] // 2
-        x = x + (F_.silu(gu[:, :F]) * gu[:, F:]) @ L["w2"].float().t()
-    rows = [T - 1] if rows is None else rows
-    h = F_.rms_norm(x[rows], (c.d_model,), model.final_norm.float(), c.norm_eps)
-    return (h @ model.lm_head.float().t())[:, : c.vocab_size]
+    return fp32_logits(model, ids, rows)
 
 
 @pytest.mark.parametrize("prompt_len", [1500, 3000])

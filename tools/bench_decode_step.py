@@ -4,9 +4,9 @@ decode hipGraph at 64 rows and ~1.7k-token contexts, timed by the engine's own G
 (``LLMEngine.step_samples``: back-to-back decode steps), with a path switch flipped and the
 graphs re-captured between phases.
 
-    python tools/bench_decode_step.py --switch seam [--rounds 3 --tokens 96]
+    python tools/bench_decode_step.py --switch rc [--rounds 3 --tokens 96]
 
-Switches: ``seam`` / ``rc`` - the decode fusions, on in every bucket vs off; ``merge`` - the
+Switches: ``rc`` - the row-complete o projection, on in every bucket vs off; ``merge`` - the
 attention's split partials merged in-launch (ops.DECODE_MERGE) vs a paged_decode_reduce launch (CausalLM.set_decode_fusion).  (Round 5
 also A/B'd write-through (sc1) epilogue stores in gemm_decode.hip with this tool: 6.107 vs 6.068
 ms per step, slower - profiles/r05/decode_step_writethrough_ab.jsonl.)
@@ -23,11 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-SWITCHES = {"seam": lambda m, on: m.set_decode_fusion(seam=on, rc=None if on is None else False),
-            "seam_auto_rc": lambda m, on: m.set_decode_fusion(seam=bool(on)),
-            "rc": lambda m, on: m.set_decode_fusion(seam=False, rc=on),
+SWITCHES = {"rc": lambda m, on: m.set_decode_fusion(rc=on),
             "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False),
-            "rc_down": lambda m, on: setattr(m, "RC_DOWN", on is not False),
             "tw32": lambda m, on: _ops().native().decode_tw_force(32 if on else 0)}
 
 
@@ -38,7 +35,7 @@ def _ops():
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--switch", default="seam", choices=sorted(SWITCHES))
+    ap.add_argument("--switch", default="rc", choices=sorted(SWITCHES))
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--rows", default="64", help="decode batch; a comma list runs each in turn")
     ap.add_argument("--ctx", type=int, default=1700)

@@ -44,8 +44,6 @@ def main() -> None:
         cases.append((name, 2 * T * N * K, {
             "w4": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=0)),
             "w4s": (lambda i, xin=xin, w=w, y=y: ops.gemm_tile(xin, w, out=y, algo=1)),
-            "pp": (lambda i, xin=xin, w=w, y=y: (ops.native().gemm_pp_sched(1), ops.gemm_tile(xin, w, out=y, algo=2))),
-            "pp0": (lambda i, xin=xin, w=w, y=y: (ops.native().gemm_pp_sched(0), ops.gemm_tile(xin, w, out=y, algo=2))),
             "hipblaslt": (lambda i, xin=xin, w=w, y=y: torch.matmul(xin, w.t(), out=y)),
         }))
     # qkv + RoPE + paged-cache write, as the prefill layer runs it: tile GEMM with the RoPE epilogue
@@ -80,7 +78,6 @@ def main() -> None:
     cases.append(("qkv+rope_rs", 2 * T * 6144 * d, {
         "plain": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40))),
         "rowscale": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=1, rope=(pos, cs, 40), rowscale=(ssq, 1e-5))),
-        "pp_rowscale": (lambda i: ops.gemm_tile(x, wq, out=yq, algo=2, rope=(pos, cs, 40), rowscale=(ssq, 1e-5))),
     }))
     cases.append(("o_resid", 2 * T * d * d, {
         "plain": (lambda i: ops.gemm_tile(x, wo_, out=yo, algo=1)),
@@ -92,13 +89,10 @@ def main() -> None:
     cases.append(("gate_up+swiglu_rs", 2 * T * 2 * F * d, {
         "plain": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
         "rowscale": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1, rowscale=(ssq, 1e-5))),
-        "pp_rowscale": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2, rowscale=(ssq, 1e-5))),
     }))
     cases.append(("gate_up+swiglu", 2 * T * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=0)),
         "w4s": (lambda i: ops.gemm_tile(x, w13, swiglu=True, out=act, algo=1)),
-        "pp": (lambda i: (ops.native().gemm_pp_sched(1), ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2))),
-        "pp0": (lambda i: (ops.native().gemm_pp_sched(0), ops.gemm_tile(x, w13, swiglu=True, out=act, algo=2))),
         "hipblaslt": (lambda i: ops.silu_mul(torch.matmul(x, w13.t(), out=gu), out=act, interleaved=True)),
         "hipblaslt_gemm_only": (lambda i: torch.matmul(x, w13.t(), out=gu)),
     }))
@@ -131,14 +125,12 @@ def main() -> None:
     cases.append(("moe_w13+swiglu", 2 * rows * 2 * F * d, {
         "w4": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=0)),
         "w4s": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=1)),
-        "pp": (lambda i: ops.gemm_tile(xs, we13, offsets, swiglu=True, out=ha, algo=2)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(xs, we13, offsets, swiglu=True, out=ha)),
         "hipblaslt_loop": loop13,
     }))
     cases.append(("moe_w2", 2 * rows * d * F, {
         "w4": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=0)),
         "w4s": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=1)),
-        "pp": (lambda i: ops.gemm_tile(hs, we2, offsets, out=ys, algo=2)),
         "moe_gemm128": (lambda i: ops.moe_grouped_gemm(hs, we2, offsets, out=ys)),
         "hipblaslt_loop": loop2,
     }))

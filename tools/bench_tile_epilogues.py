@@ -46,15 +46,12 @@ def main() -> None:
                         2 * T * 6144 * d),
         "o_plain": (lambda _i: ops.gemm_tile(x, wo, out=hw, algo=ops.TILE_ALGO), 2 * T * d * d),
         "o_resid": (lambda _i: ops.gemm_tile_resid(x, wo, resid, nw, hw, ss), 2 * T * d * d),
-        "o_resid_nt": (lambda _i: ops.gemm_tile_resid(x, wo, resid, nw, hw, ss), 2 * T * d * d),
     }
     res: dict = {k: [] for k in cases}
     for _ in range(a.rounds):
         for k, (fn, flop) in cases.items():
-            ops.native().tile_resid_nt(1 if k.endswith("_nt") else 0)  # graphs capture the kernel argument
             us = timeit(fn, a.iters)
             res[k].append(us)
-    ops.native().tile_resid_nt(0)
     for k, (fn, flop) in cases.items():
         us = sorted(res[k])[len(res[k]) // 2]
         print(json.dumps({"case": k, "tokens": T, "us": round(us, 1), "pflops": round(flop / us / 1e9, 3),
