@@ -79,6 +79,10 @@ def parse(argv=None):
                     help="A/B runs of the decode-step fusion (CausalLM.set_decode_fusion): auto = the "
                          "default (row-complete o only for the smallest buckets), none = off, rc = "
                          "every bucket")
+    ap.add_argument("--layout", choices=["one", "two"], default="one",
+                    help="dense Llama weights: one = the single fragment-packed copy read by prefill and "
+                         "decode (CausalLM.ONE_LAYOUT), two = row-major prefill weights + decode copies "
+                         "(the round-5 form, for A/B runs)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     a = ap.parse_args(argv)
@@ -199,6 +203,8 @@ def run_rank(a) -> None:
         # prefill step) so the wave starts as one prefill batch (config 1, VERDICT r5 Missing #3)
         admit.setdefault("admit_gap_ms", 25.0)
         admit.setdefault("admit_window_ms", 250.0)
+    from k8s_llm_monitor_amd.models.llama import CausalLM
+    CausalLM.ONE_LAYOUT = a.layout == "one"
     eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=max(a.batch, 8) if a.mode == "latency" else a.batch,
                                  max_model_len=8192, max_prefill_tokens=a.max_prefill_tokens,
                                  chunked_prefill=bool(a.chunked_prefill), tp_size=a.tp,
@@ -370,7 +376,9 @@ def _finish(a, ps, comm, elapsed, n_ok, ptoks, gtoks, res, stats, devices, eng, 
                    "prompt_tokens_mean": round(total_p / max(1.0, total_ans), 1),
                    "max_new_tokens": a.max_new_tokens, "path": a.path, "mode": a.mode,
                    "client": a.client if a.path != "engine" else None,
-                   "server_timeouts": "production 15s/30s" if a.production else "bench 600s"},
+                   "server_timeouts": "production 15s/30s" if a.production else "bench 600s",
+                   "weight_layout": "one (fragment-packed)" if getattr(eng.model, "_packed", False) else "row-major + decode copies",
+                   "resident_weight_gb_per_rank": round(eng.model.resident_weight_bytes() / 1e9, 2)},
         "p50_latency_ms": round(p50, 2),
         "p99_latency_ms": _pct(lats, 0.99),
         "generated_tokens_per_s": round(total_gen / t_max, 1) if t_max > 0 else 0.0,

@@ -288,11 +288,11 @@ def hf_state_dict(model) -> Iterator[tuple[str, torch.Tensor]]:
     yield "model.norm.weight", model.final_norm
     for i, L in enumerate(model.layers):
         p = f"model.layers.{i}."
-        w = L["wqkv"]
+        w = model.canonical(L, "wqkv")  # row-major whatever the resident layout (ONE_LAYOUT packs it)
         yield p + "self_attn.q_proj.weight", w[:nq]
         yield p + "self_attn.k_proj.weight", w[nq:nq + nk]
         yield p + "self_attn.v_proj.weight", w[nq + nk:]
-        yield p + "self_attn.o_proj.weight", L["wo"]
+        yield p + "self_attn.o_proj.weight", model.canonical(L, "wo")
         yield p + "input_layernorm.weight", L["attn_norm"]
         yield p + "post_attention_layernorm.weight", L["mlp_norm"]
         F = c.ffn_dim
@@ -310,10 +310,10 @@ def hf_state_dict(model) -> Iterator[tuple[str, torch.Tensor]]:
                 yield f"{m}experts.{e}.w3.weight", w13[F:]
                 yield f"{m}experts.{e}.w2.weight", L["w2"][e]
         else:
-            w13 = canon(L["w13"])
+            w13 = model.canonical(L, "w13")
             yield p + "mlp.gate_proj.weight", w13[:F]
             yield p + "mlp.up_proj.weight", w13[F:]
-            yield p + "mlp.down_proj.weight", L["w2"]
+            yield p + "mlp.down_proj.weight", model.canonical(L, "w2")
 
 
 def save_checkpoint(model, path: PathLike, max_shard_bytes: int = 4 << 30) -> Path:

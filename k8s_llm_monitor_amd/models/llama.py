@@ -88,6 +88,11 @@ class CausalLM:
     # real-shape tests); DECODE_GEMM "auto" | "dec" | "rm" = the decode projections' kernel (_want_dec)
     SKINNY_DECODE = True
     DECODE_GEMM = "auto"
+    # ONE resident copy of every dense Llama projection on the GPU: the decode GEMMs' fragment-packed
+    # layout, which the prefill tile GEMM reads as well (gemm_tile wpk mode - bit-identical to the
+    # row-major form and within +-1.4 % of its speed: profiles/r06/gemm_packed_w_*.jsonl); the
+    # row-major tensors are dropped.  "force": also on the CPU (tests).
+    ONE_LAYOUT = True
 
     def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16, seed: int = 0,
                  pstate: Optional[ParallelState] = None, init_std: float = 0.02, init: str = "random"):
@@ -130,6 +135,8 @@ class CausalLM:
         self.moe_decode = os.environ.get("K8SLLM_MOE_DECODE", "allreduce")
         self.layers: list[dict] = []
         self._w13_il = False  # w13 gate/up-interleaved per 128 rows (set by _init_skinny)
+        self._packed = False  # ONE_LAYOUT: the dense projections are resident fragment-packed only
+        self._swg = True  # gemm_tile's SwiGLU pairing of w13: True = per 128 rows, 8 = per 16 (packed)
         self.skinny_layout = None
         self._build()
         self._init_skinny()
@@ -226,6 +233,20 @@ class CausalLM:
                     del w2
             self.layers.append(L)
 
+    def resident_weight_bytes(self) -> int:
+        """Bytes of every distinct weight tensor this rank holds (parameters, decode-layout copies
+        and the LM head's packed copy; a tensor referenced under two keys counts once)."""
+        seen, n = set(), 0
+        ts = [self.embed, self.lm_head, getattr(self, "lm_head_d", None), self.final_norm]
+        for L in self.layers:
+            for v in L.values():
+                ts.extend(v if isinstance(v, tuple) else (v,))
+        for t in ts:
+            if isinstance(t, torch.Tensor) and t.data_ptr() not in seen:
+                seen.add(t.data_ptr())
+                n += t.numel() * t.element_size()
+        return n
+
     def num_local_params(self) -> int:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
         for L in self.layers:
@@ -277,7 +298,7 @@ class CausalLM:
                                               meta.block_tables, meta.seq_lens, self.hq, self.hkv, self.D, self.scale,
                                               workspace=meta.decode_ws, out=out)
             partial = ws
-            qkv = torch.empty(T, L["wqkv"].shape[0], dtype=self.dtype, device=self.device)
+            qkv = torch.empty(T, ops.w_out(L["wqkv"]), dtype=self.dtype, device=self.device)
         elif "bqkv" in L:
             qkv = F.linear(x, L["wqkv"], L["bqkv"])
         elif c.arch == "llama" and self.D == 128 and self.cos_sin is not None:
@@ -327,7 +348,7 @@ class CausalLM:
                 return self._moe_a2a_decode(L, x)
             return tp_all_reduce(self._moe(L, x, meta), self.ps)
         if self._w13_il:
-            h = ops.prefill_linear(x, L["w13"], swiglu=True)
+            h = ops.prefill_linear(x, L["w13"], swiglu=self._swg)
         else:
             h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=False)
         return tp_all_reduce(ops.prefill_linear(h, L["w2"]), self.ps)
@@ -563,7 +584,7 @@ class CausalLM:
     def _mlp_local(self, L: dict, x: torch.Tensor) -> torch.Tensor:
         """Dense SwiGLU MLP of this rank's F shard, before the row-parallel all-reduce."""
         if self._w13_il:
-            h = ops.prefill_linear(x, L["w13"], swiglu=True)
+            h = ops.prefill_linear(x, L["w13"], swiglu=self._swg)
         else:
             h = ops.silu_mul(F.linear(x, L["w13"]), interleaved=False)
         return ops.prefill_linear(h, L["w2"])
@@ -620,8 +641,8 @@ class CausalLM:
         if self.D != 128 or self.cos_sin is None or any(k in self.layers[0] for k in ("bqkv", "bo")):
             return False
         L = self.layers[0]
-        return ops.fused_norm_ok(h.shape[0], c.d_model, L["wqkv"].shape[0], L["wo"].shape[1], L["w13"].shape[0],
-                                 L["w2"].shape[1])
+        return ops.fused_norm_ok(h.shape[0], c.d_model, ops.w_out(L["wqkv"]), ops.w_in(L["wo"]), ops.w_out(L["w13"]),
+                                 ops.w_in(L["w2"]))
 
     def _prefill_fused_norm(self, residual: torch.Tensor, meta: AttnMeta, kv_caches: Optional[list]) -> torch.Tensor:
         """The prefill layers with every RMSNorm but the first and the final one folded into the
@@ -638,7 +659,7 @@ class CausalLM:
             kv = kv_caches[i] if kv_caches is not None else None
             o = self._attn_core(L, x, meta, kv, rowscale=(ss, eps) if ss is not None else None)
             x, ss = ops.gemm_tile_resid(o, L["wo"], residual, L["mlp_norm"])
-            act = ops.prefill_linear(x, L["w13"], swiglu=True, rowscale=(ss, eps))
+            act = ops.prefill_linear(x, L["w13"], swiglu=self._swg, rowscale=(ss, eps))
             if i + 1 < n:
                 x, ss = ops.gemm_tile_resid(act, L["w2"], residual, self.layers[i + 1]["attn_norm"])
             else:
@@ -699,6 +720,11 @@ class CausalLM:
         self._skinny_ws = None
         self.lm_head_d = None
         self._rc_o = 0
+        if self._packed:  # re-initialised over ONE_LAYOUT weights: back to the canonical row-major form
+            for L in self.layers:
+                for key in ("wqkv", "wo", "w13", "w2"):
+                    L[key] = self.canonical(L, key).contiguous()
+            self._packed, self._swg, self._w13_il = False, True, False
         for L in self.layers:  # (re)built below from the current weights
             for key in ("wqkv_d", "wo_d", "w13_d", "w2_d", "w13_dg", "w2_dg"):
                 L.pop(key, None)
@@ -896,12 +922,13 @@ class CausalLM:
         weights' bytes: the LM head always (<= 2.1 GB, Llama-3-70B); the attention projections
         while W + their copies fit 70 % of the device; a dense MLP while 2W fits half of it
         (Llama-3-8B: 16 GB of 288); MoE experts while 2W fits 70 % (Mixtral-8x7B at TP=1: 93 + 93
-        GB).  Llama-3-70B at TP=1 (141 GB) gets head + attention copies (+24 GB) and keeps its MLP
-        on the row-major skinny kernel."""
+        GB).  Llama-3-70B at TP=1 (141 GB) would get head + attention copies (+24 GB) and keep its
+        MLP on the row-major skinny kernel - but dense Llama now runs ONE_LAYOUT: every projection
+        is packed and the packed tensor is the only copy (no extra memory at any size)."""
         mode = self.DECODE_GEMM
         if mode in ("rm", "0", "off") or self.cfg.arch != "llama":
             return set()
-        if mode in ("dec", "1", "on") or self.device.type != "cuda":
+        if mode in ("dec", "1", "on") or self.device.type != "cuda" or self._one_layout_wanted():
             return {"head", "attn", "mlp", "experts"}
         total = torch.cuda.get_device_properties(self.device).total_memory
         w = self.num_local_params() * 2
@@ -916,14 +943,43 @@ class CausalLM:
             parts.add("mlp")
         return parts
 
+    def _one_layout_wanted(self) -> bool:
+        """ONE_LAYOUT applies: dense Llama whose four projections all have a decode configuration
+        (the shapes are the same in every layer, so layer 0 decides)."""
+        c = self.cfg
+        if not (self.ONE_LAYOUT and c.arch == "llama" and not c.is_moe and self.layers and self.SKINNY_DECODE
+                and self.DECODE_GEMM not in ("rm", "0", "off")
+                and (self.device.type == "cuda" or self.ONE_LAYOUT == "force")):
+            return False
+        L = self.layers[0]
+        if L["wqkv"].dim() != 2 or L["w13"].dim() != 2:
+            return False
+        (nq, d), (f2, _) = L["wqkv"].shape, L["w13"].shape
+        return (ops.dec_available(nq, d, 0) and ops.dec_available(d, nq - 2 * self.hkv * self.D, 0)
+                and ops.dec_available(f2, d, 2) and ops.dec_available(d, f2 // 2, 0) and d % 256 == 0
+                and f2 % 256 == 0)
+
+    def canonical(self, L: dict, key: str) -> torch.Tensor:
+        """A dense projection as the row-major [out, in] weight of the reference / the checkpoint
+        format (w13 as [gate; up]), whatever its resident layout (row-major, gate/up interleaved
+        per 128 rows, or the one fragment-packed copy)."""
+        w = L[key]
+        if w.dim() == 4:  # ONE_LAYOUT: fragment-packed (w13: interleaved per 16 rows)
+            w = ops.unpack_skinny(w)
+            return ops.deinterleave_gate_up8(w) if key == "w13" else w
+        return ops.deinterleave_gate_up(w) if key == "w13" and self._w13_il else w
+
     def _init_dec(self) -> None:
         """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
         launch configuration for its shape (ops.dec_config): wqkv_d / wo_d / w2_d
         ([N/16, K/32, 64, 8]), w13_d (gate/up interleaved per 16 rows as [8 gate | 8 up]), and the
-        LM head.  Prefill keeps reading the row-major tensors."""
+        LM head.  ONE_LAYOUT (dense Llama): the packed copy REPLACES the row-major tensor layer by
+        layer (peak memory = the weights + one layer's copy) and prefill reads it too; otherwise
+        prefill keeps reading the row-major tensors."""
         self.lm_head_d = None
         parts = self._want_dec()
         c = self.cfg
+        one = self._one_layout_wanted()
         for L in self.layers:
             keys = (("wqkv", "wo") if "attn" in parts else ()) + (("w2",) if "mlp" in parts and not c.is_moe else ())
             for key in keys:
@@ -935,6 +991,10 @@ class CausalLM:
                 if ops.dec_available(w.shape[0], w.shape[1], 2):
                     L["w13_d"] = ops.pack_skinny(ops.interleave_gate_up8(w))
                 del w
+            if one:
+                for key in ("wqkv", "wo", "w13", "w2"):
+                    L[key] = L[key + "_d"]
+                    L.pop(key + "_p", None)  # the skinny kernel's reference to the row-major tensor
             elif "experts" in parts and c.is_moe:  # [E, ...] stacks for the grouped (grid.z = expert) launches
                 E, F2, d = L["w13"].shape
                 if (ops.dec_config(F2, d, 2, experts=E) is not None
@@ -945,6 +1005,8 @@ class CausalLM:
         N, K = self.lm_head.shape
         if "head" in parts and N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
             self.lm_head_d = ops.pack_skinny(self.lm_head)
+        self._packed = one
+        self._swg = 8 if one else True  # the prefill SwiGLU's gate/up interleave (gemm_tile swiglu)
 
     def _tp_tail(self, ws, ns: int, residual: torch.Tensor, norm_w, packed: bool) -> Optional[torch.Tensor]:
         """TP>1 on the GPU with the IPC all-reduce: the row-parallel tail (slab sum, all-reduce,

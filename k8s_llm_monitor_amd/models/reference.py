@@ -1,6 +1,7 @@
 """Plain fp32 forward of a Llama-architecture CausalLM's own weights (no HIP kernels, no KV cache,
 no fused epilogues): the numeric oracle for the GPU engine in ``__graft_entry__.smoke`` and the
-real-shape GPU tests.  Weights are read from the model (interleaved gate/up rows undone), moved to
+real-shape GPU tests.  Weights are read from the model in their canonical row-major form (CausalLM.canonical: packed
+or interleaved resident layouts undone), moved to
 ``device`` and upcast, so a GPU model can be checked against an fp32 pass on the CPU."""
 from __future__ import annotations
 
@@ -8,8 +9,6 @@ from typing import Optional
 
 import torch
 import torch.nn.functional as F
-
-from .. import ops
 
 
 @torch.no_grad()
@@ -38,17 +37,16 @@ def fp32_logits(model, ids: torch.Tensor, rows: Optional[list] = None, device: O
 
     for L in model.layers:
         h = F.rms_norm(x, (c.d_model,), w(L["attn_norm"]), c.norm_eps)
-        q, k, v = (h @ w(L["wqkv"]).t()).split([Hq * D, Hk * D, Hk * D], 1)
+        q, k, v = (h @ w(model.canonical(L, "wqkv")).t()).split([Hq * D, Hk * D, Hk * D], 1)
         q, k = rope(q.view(T, Hq, D)), rope(k.view(T, Hk, D))
         att = F.scaled_dot_product_attention(q.transpose(0, 1)[None], k.transpose(0, 1)[None],
                                              v.view(T, Hk, D).transpose(0, 1)[None], is_causal=True,
                                              enable_gqa=Hq != Hk)[0]
-        x = x + att.transpose(0, 1).reshape(T, Hq * D) @ w(L["wo"]).t()
+        x = x + att.transpose(0, 1).reshape(T, Hq * D) @ w(model.canonical(L, "wo")).t()
         h = F.rms_norm(x, (c.d_model,), w(L["mlp_norm"]), c.norm_eps)
-        w13 = ops.deinterleave_gate_up(L["w13"]) if getattr(model, "_w13_il", False) else L["w13"]
-        gu = h @ w(w13).t()
+        gu = h @ w(model.canonical(L, "w13")).t()
         f = gu.shape[1] // 2
-        x = x + (F.silu(gu[:, :f]) * gu[:, f:]) @ w(L["w2"]).t()
+        x = x + (F.silu(gu[:, :f]) * gu[:, f:]) @ w(model.canonical(L, "w2")).t()
     rows = [T - 1] if rows is None else rows
     h = F.rms_norm(x[rows], (c.d_model,), w(model.final_norm), c.norm_eps)
     return (h @ w(model.lm_head).t())[:, : c.vocab_size]

@@ -959,7 +959,9 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
     rsqrt(sum(ss_part[row]) / K + eps) before the epilogue (``x`` holds the norm's weighted input,
     gemm_tile_resid's ``hw``).
     ``w`` may also be fragment-packed (pack_skinny: [N/16, K/32, 64, 8], grouped [E, ...]): the
-    decode GEMMs' layout, consumed as is (every W DMA piece one contiguous 1-KiB block)."""
+    decode GEMMs' layout, consumed as is (every W DMA piece one contiguous 1-KiB block).
+    ``swiglu=8``: the gate/up rows are interleaved per 16 (interleave_gate_up8, the decode GEMMs'
+    SwiGLU copy) instead of per 128 - prefill and decode then share one weight."""
     M = x.shape[0]
     packed = w.dim() == (5 if offsets is not None else 4)
     N = w.shape[-4] * 16 if packed else w.shape[-2]
@@ -983,6 +985,9 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
             if inv is not None:
                 y = y * inv
             y = y.to(x.dtype)
+            if swiglu == 8:
+                g = y.view(y.shape[0], -1, 16)
+                return (torch.nn.functional.silu(g[..., :8].float()) * g[..., 8:].float()).reshape(y.shape[0], -1).to(x.dtype)
             return silu_mul(y, interleaved=True) if swiglu else y
         if offsets is None:
             out.copy_(one(x, w))
@@ -1007,10 +1012,10 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, offsets: Optional[torch.Tensor] 
         pos, cs, heads = rope
         native().gemm_tile(out, x.contiguous(), w, None, False, algo, pos, cs, heads, rs_part, rs_eps)
     elif rowscale is not None:
-        native().gemm_tile(out, x.contiguous(), w, None, swiglu, algo, None, None, 0, rs_part, rs_eps)
+        native().gemm_tile(out, x.contiguous(), w, None, int(swiglu), algo, None, None, 0, rs_part, rs_eps)
     else:
         native().gemm_tile(out, x.contiguous(), w, offsets.contiguous() if offsets is not None else None,
-                           swiglu, algo)
+                           int(swiglu), algo)
     return out
 
 
@@ -1073,6 +1078,17 @@ def fused_norm_ok(M: int, d: int, n_qkv: int, n_o_in: int, n_13: int, f: int) ->
             and tile_shape_ok(M, n_13, d, swiglu=True) and tile_shape_ok(M, d, f) and 256 * d * 2 < (1 << 31))
 
 
+def w_out(w: torch.Tensor) -> int:
+    """Output features of a dense projection weight: row-major [N, K] or fragment-packed
+    [N/16, K/32, 64, 8] (pack_skinny)."""
+    return w.shape[0] * 16 if w.dim() == 4 else w.shape[0]
+
+
+def w_in(w: torch.Tensor) -> int:
+    """Input features (K) of a row-major or fragment-packed dense projection weight."""
+    return w.shape[1] * 32 if w.dim() == 4 else w.shape[1]
+
+
 def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
                    out: Optional[torch.Tensor] = None, rope: Optional[tuple] = None,
                    rowscale: Optional[tuple] = None) -> torch.Tensor:
@@ -1081,8 +1097,15 @@ def prefill_linear(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
     into the tile kernel's epilogue, or F.linear + silu_mul on the library path.
     ``rope = (positions, cos_sin, heads)`` (the qkv projection, head_dim 128): the tile kernel
     rotates heads 0 .. heads - 1 in its epilogue; returns ``(y, rotated)`` - rotated False when the
-    library took the GEMM (the caller then applies RoPE itself)."""
+    library took the GEMM (the caller then applies RoPE itself).
+    A fragment-packed ``w`` (pack_skinny, the ONE_LAYOUT resident form; ``swiglu=8`` with the
+    interleave_gate_up8 pairing) always takes the tile kernel, whatever the row count - hipBLASLt
+    cannot read it; on the CPU gemm_tile unpacks it for the fp32 reference."""
     M, K = x.shape
+    if w.dim() == 4:
+        if rope is not None:
+            return gemm_tile(x, w, out=out, algo=TILE_ALGO, rope=rope, rowscale=rowscale), True
+        return gemm_tile(x, w, swiglu=swiglu, out=out, algo=TILE_ALGO, rowscale=rowscale)
     N = w.shape[0]
     mode = PREFILL_GEMM
     tile_ok = _gpu(x) and tile_shape_ok(M, N, K, swiglu)

@@ -43,7 +43,6 @@ int k8sllm_moe_align(const int* topk_ids, long n, int E, int* expert_offsets, in
 int k8sllm_moe_combine(void* out, const void* expert_out, const int* inv_idx, const float* topk_w, long T, int K,
                        int d, hipStream_t s);
 int k8sllm_gather_rows(void* out, const void* x, const int* idx, long n, int d, int div, hipStream_t s);
-void k8sllm_flash_stagger(int v);
 int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, int N, int K, const int* offsets, int E, long w_es,
                      int epi, int algo, const int* rope_pos, const float* rope_cs, int rope_heads,
                      const float* rs_part, int rs_np, float rs_eps, void* resid, void* hw, const void* norm_w,
@@ -400,7 +399,9 @@ void moe_grouped_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, torch::
 // no host sync).  swiglu: w gate/up-interleaved per 128 rows, y [M, N / 2] = silu(gate) * up.
 // rope_pos / rope_cs (dense, N % 128 == 0): the qkv projection with the rotary embedding of heads
 // 0 .. rope_heads - 1 (q and k, head_dim 128) applied in the epilogue (TILE_EPI_ROPE)
-void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, bool swiglu,
+// swiglu: 0 none, 1 = gate/up interleaved per 128 rows (interleave_gate_up), 8 = per 16 rows
+// (interleave_gate_up8, the decode GEMMs' packed copy)
+void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> offsets, int64_t swiglu,
                int64_t algo, c10::optional<torch::Tensor> rope_pos, c10::optional<torch::Tensor> rope_cs,
                int64_t rope_heads, c10::optional<torch::Tensor> rs_part, double rs_eps,
                c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> hw,
@@ -465,7 +466,8 @@ void gemm_tile(torch::Tensor y, torch::Tensor x, torch::Tensor w, c10::optional<
     TORCH_CHECK(ss_out->is_cuda() && ss_out->scalar_type() == torch::kFloat32 && ss_out->is_contiguous() &&
                     ss_out->numel() >= (long)M * (N / 128), "gemm_tile: ss_out [M, N / 128] fp32");
   }
-  const int epi = rsd ? 3 : rp ? 2 : (swiglu ? 1 : 0);
+  TORCH_CHECK(swiglu == 0 || swiglu == 1 || swiglu == 8, "gemm_tile: swiglu 0, 1 or 8");
+  const int epi = rsd ? 3 : rp ? 2 : (swiglu == 8 ? 4 : swiglu ? 1 : 0);
   check(k8sllm_gemm_tile(x.data_ptr(), w.data_ptr(), rsd ? resid->data_ptr() : y.data_ptr(), M, N, K, op, E,
                          (long)N * K, epi, (int)algo, rp, rc, (int)rope_heads, rsp, rs_np, (float)rs_eps,
                          rsd ? resid->data_ptr() : nullptr, rsd ? hw->data_ptr() : nullptr,
@@ -963,7 +965,6 @@ PYBIND11_MODULE(_k8sllm_ops, m) {
   m.def("gather_rows", &gather_rows);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_grouped", &gemm_skinny_grouped);
-  m.def("flash_stagger", [](int64_t v) { k8sllm_flash_stagger((int)v); });
   m.def("gemm_dec", &gemm_dec);
   m.def("gemm_dec_grouped", &gemm_dec_grouped);
   m.def("gemm_dec_rc", &gemm_dec_rc);

@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(bf16_t* __restric
 //    accumulator converted in place), online softmax lane-local (query = lane).
 //  * heads are remapped nowhere: blockIdx.x = kv head, so all workgroups of one kv head share an
 //    XCD (dispatch round-robin over 8 XCDs) and its L2 serves the head's K/V to every q-block.
-template <int G, bool STAG>
+template <int G>
 __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
     bf16_t* __restrict__ out, long out_stride, const bf16_t* __restrict__ qkv, long qkv_stride,
     const int* __restrict__ cu_seqlens, const int* __restrict__ qb_seq, const int* __restrict__ qb_start, int Hq,
@@ -458,159 +458,36 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
     l = l * alpha + xor32_sum((rq[0] + rq[1]) + (rq[2] + rq[3]));
   };
 
-  if constexpr (STAG) {
-    // Staggered (ping-pong) form: the two waves of a SIMD (w and w + 4, one of each group) run the
-    // same per-tile work half a tile apart, so one's softmax VALU runs under the other's MFMAs
-    // instead of both SIMD waves entering the softmax together after the tile barrier.  Per tile
-    // the work is an MFMA phase (PV of the previous tile + QK of this one, 32 MFMAs) and a VALU
-    // phase (mask, max, lazy rescale, exponentials: sm).  Iteration t, both groups read K(t) and
-    // V(t - 1):
-    //   group 0 (waves 0-3): [PV(t-1), QK(t)]  then  [SM(t)]
-    //   group 1 (waves 4-7): [SM(t-1)]         then  [PV(t-1), QK(t)]
-    // O is rescaled in SM(t) only after PV(t-1) was added (the lazy-rescale hazard), in both
-    // orders.  A tile's slot is read until the iteration after its own (V), so the ring keeps
-    // t - 1 .. t + 2: the refill at barrier t goes into tile t - 2's slot (two tiles in flight).
-    const int grp = wave >> 2;
-    bf16x8 pb[4];
-    auto sm = [&](int t, f32x16 (&sa)[2]) {
-      mask(t, sa);
-      float mq[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) mq[c] = fmaxf(sa[c >> 1][8 * (c & 1)], sa[c >> 1][8 * (c & 1) + 1]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int r = 2; r < 8; ++r) mq[c] = fmaxf(mq[c], sa[c >> 1][8 * (c & 1) + r]);
-      const float mx = xor32_max(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
-      const float mt = mx * scale_log2;
-      const float mnew = mt > m + 8.f ? mt : m;
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-      if (__builtin_amdgcn_ballot_w64(mnew != m) != 0) {
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-      }
-      m = mnew;
-      float rq[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i][8 * s + j], scale_log2, -mnew));
-            rq[2 * i + s] += p;
-            pb[2 * i + s][j] = (__bf16)p;
-          }
-      l = l * alpha + xor32_sum((rq[0] + rq[1]) + (rq[2] + rq[3]));
-    };
-    auto pv = [&](int t) {
-      const char* vt = fp2_smem + (t % NBUF) * TILE + 16384;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 vfr[DT];
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const int d = 32 * dt + r32;
-            vfr[dt] = *reinterpret_cast<const bf16x8*>(vt + (2 * i + s) * 4096 + (d * 2 + (hh ^ ((d >> 3) & 1))) * 16);
-          }
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt)
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[dt], pb[2 * i + s], o[dt], 0, 0, 0);
-        }
-    };
-    const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
-    // K fragments in two halves of 8 (32 VGPRs each) - the staggered loop carries P or S across
-    // iterations, so the whole-tile K read of the unstaggered form does not fit beside it
-    auto qk2 = [&](int t, f32x16 (&sa)[2]) {
-      const char* kt = fp2_smem + (t % NBUF) * TILE;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sa[i][r] = 0.f;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 kfr[KS / 2][2];
-#pragma unroll
-        for (int k = 0; k < KS / 2; ++k)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int ks = h * (KS / 2) + k;
-            kfr[k][i] = *reinterpret_cast<const bf16x8*>(kt + (2 * i + (r32 >> 4)) * 4096 +
-                                                         ((2 * ks + hh) * 16 + (r32 & 15)) * 16);
-          }
-#pragma unroll
-        for (int k = 0; k < KS / 2; ++k)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            sa[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[k][i], qf[h * (KS / 2) + k], sa[i], 0, 0, 0);
-      }
-    };
-    auto head = [&](int t) {  // tile t landed for every wave; refill tile t - 2's slot with t + 2
-      if (t < ntiles) {
-        if (t + 1 < ntiles)
-          wait_vmcnt_fp<4>();  // this wave's pieces of tile t landed; t + 1 may still fly
-        else
-          wait_vmcnt_fp<0>();
-        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t landed; iteration t - 1 done
-        if (t + 2 < ntiles) issue(t + 2, (t + 2) % NBUF);
-      }
-    };
-    issue(0, 0);
-    if (ntiles > 1) issue(1, 1);
-    if (grp == 0) {
-      for (int t = 0; t <= ntiles; ++t) {
-        head(t);
-        if (t >= 1 && t - 1 < nt_w) pv(t - 1);
-        if (t < nt_w) {
-          f32x16 sa[2];
-          qk2(t, sa);
-          sm(t, sa);
-        }
-      }
-    } else {
-      f32x16 sa[2];
-      for (int t = 0; t <= ntiles; ++t) {
-        head(t);
-        if (t >= 1 && t - 1 < nt_w) {
-          sm(t - 1, sa);
-          pv(t - 1);
-        }
-        if (t < nt_w) qk2(t, sa);
-      }
-    }
-  } else {
-    // Main loop: ONE barrier per tile; tiles t + 1 and t + 2 are in flight while tile t is
-    // computed (4-slot ring).  At tile t's barrier every wave has finished tile t - 1, whose slot
-    // (t + 3) % 4 is refilled right after it.  (A software-pipelined variant that put tile t + 1's
-    // QK beside tile t's softmax measured no faster and spilled once the two phases shared a
-    // basic block.)  The wave computes only its first nt_w tiles (later ones are in the future of
-    // all its rows) but joins every barrier and issues its DMA pieces for every tile.
-    const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
-    // (No static priority for the second-dispatched half: with each 16-key group's exponentials
-    // interleaved with the PV MFMAs it measured 1-2 % slower at 10 x 1609 and equal at 4k-16k,
-    // profiles/r04/flash_no_setprio_ab.jsonl.)
-    issue(0, 0);
-    if (ntiles > 1) issue(1, 1);
-    if (ntiles > 2) issue(2, 2);
-    for (int t = 0; t < ntiles; ++t) {
-      if (t + 2 < ntiles)
-        wait_vmcnt_fp<8>();  // this wave's pieces of tile t landed; t + 1, t + 2 may still fly
-      else if (t + 1 < ntiles)
-        wait_vmcnt_fp<4>();
-      else
-        wait_vmcnt_fp<0>();
-      __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t landed; tile t - 1 reads done
-      if (t + 3 < ntiles) issue(t + 3, (t + 3) % NBUF);
-      if (t >= nt_w) continue;
-      f32x16 sa[2];
-      qk(t, sa);
-      mask(t, sa);
-      softmax_pv(t, sa);
-    }
+  // Main loop: ONE barrier per tile; tiles t + 1 and t + 2 are in flight while tile t is
+  // computed (4-slot ring).  At tile t's barrier every wave has finished tile t - 1, whose slot
+  // (t + 3) % 4 is refilled right after it.  (A software-pipelined variant that put tile t + 1's
+  // QK beside tile t's softmax measured no faster and spilled once the two phases shared a
+  // basic block.  Round 6: a staggered form - the two waves of a SIMD half a tile apart, one's
+  // softmax under the other's MFMAs: PV(t-1) + QK(t) then softmax(t) vs softmax(t-1) then
+  // PV(t-1) + QK(t), K in two 8-fragment halves, 196 VGPRs - was bit-identical and 3-8 % SLOWER at
+  // 10 x 1609, 64 x 1609 and 2 x 8192, Hq 32 and 64: profiles/r06/flash_stagger_ab.jsonl.)  The wave computes only its first nt_w tiles (later ones are in the future of
+  // all its rows) but joins every barrier and issues its DMA pieces for every tile.
+  const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
+  // (No static priority for the second-dispatched half: with each 16-key group's exponentials
+  // interleaved with the PV MFMAs it measured 1-2 % slower at 10 x 1609 and equal at 4k-16k,
+  // profiles/r04/flash_no_setprio_ab.jsonl.)
+  issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
+  if (ntiles > 2) issue(2, 2);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 2 < ntiles)
+      wait_vmcnt_fp<8>();  // this wave's pieces of tile t landed; t + 1, t + 2 may still fly
+    else if (t + 1 < ntiles)
+      wait_vmcnt_fp<4>();
+    else
+      wait_vmcnt_fp<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t landed; tile t - 1 reads done
+    if (t + 3 < ntiles) issue(t + 3, (t + 3) % NBUF);
+    if (t >= nt_w) continue;
+    f32x16 sa[2];
+    qk(t, sa);
+    mask(t, sa);
+    softmax_pv(t, sa);
   }
 
   if (myq < L) {
@@ -632,9 +509,6 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
 
 using namespace k8sllm;
 
-static int g_flash_stag = 0;  // tools A/B: 1 = the staggered (ping-pong) v2 main loop
-extern "C" void k8sllm_flash_stagger(int v) { g_flash_stag = v; }
-
 extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv, long qkv_stride,
                                     const int* cu_seqlens, const int* qb_seq, const int* qb_start, int n_qblocks,
                                     int Hq, int Hkv, int D, float scale, const int* ctx_start, const void* k_cache,
@@ -648,14 +522,9 @@ extern "C" int k8sllm_flash_prefill(void* out, long out_stride, const void* qkv,
     // v2: q-blocks of 128 rows split into 128 / QR workgroups (QR = 256 / G rows each), adjacent in y
     const int z = 128 / (256 / G);
 #define K8S_FP2(GG)                                                                                                 \
-  if (g_flash_stag)                                                                                                 \
-    hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG, true>), dim3(Hkv, n_qblocks * z), dim3(512), 0, s,       \
-                       (bf16_t*)out, out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq,  \
-                       Hkv, sl2, ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride); \
-  else                                                                                                              \
-    hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG, false>), dim3(Hkv, n_qblocks * z), dim3(512), 0, s,      \
-                       (bf16_t*)out, out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq,  \
-                       Hkv, sl2, ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride)
+  hipLaunchKernelGGL((flash_prefill_paged_v2_kernel<GG>), dim3(Hkv, n_qblocks * z), dim3(512), 0, s, (bf16_t*)out,  \
+                     out_stride, (const bf16_t*)qkv, qkv_stride, cu_seqlens, qb_seq, qb_start, Hq, Hkv, sl2,       \
+                     ctx_start, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride)
     switch (G) {
       case 2: K8S_FP2(2); break;
       case 4: K8S_FP2(4); break;

@@ -379,7 +379,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   // the accumulator layout directly, which is what bounds a store tail (T21). ----
   lgkm_wait0();
   __builtin_amdgcn_s_barrier();  // every wave is done with the ring (its last DMAs retired above)
-  constexpr int OUTW = EPI == TILE_EPI_SWIGLU ? 64 : 128;  // output columns of this wave's quarter
+  constexpr bool SWG = EPI == TILE_EPI_SWIGLU || EPI == TILE_EPI_SWIGLU8;
+  constexpr int OUTW = SWG ? 64 : 128;  // output columns of this wave's quarter
   constexpr int RS_ = OUTW * 2 + 16;                       // LDS row stride (16-B pad: 2-way writes)
   char* stage = smem + wave * (128 * RS_);
   const int ml = lane & 15, nq = 4 * (lane >> 4);
@@ -411,6 +412,31 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
           o[r] = gt * up / (1.f + __expf(-gt));
         }
         *reinterpret_cast<uint2*>(srow + j * 32) = uint2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      }
+    } else if constexpr (EPI == TILE_EPI_SWIGLU8) {
+      // [8 gate | 8 up] per 16-column n-tile j: gate column 4 q + r (q = 0, 1: lanes 0-31) pairs
+      // with up column 8 + 4 q + r in lane + 32.  One v_permlane32_swap per register puts (gate,
+      // up) in both lane halves; lanes 0-31 finish r = 0, 1 and lanes 32-63 r = 2, 3 of feature
+      // 8 j + 4 q + r (4 bytes each).
+      const int hi = lane >> 5, qq = (lane >> 4) & 1;
+      char* srow8 = stage + (i * 16 + ml) * RS_ + (8 * qq + 4 * hi);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g[4], u[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t v = __float_as_uint(acc[i][j][r] * sc[i]);
+          const auto pr = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+          g[r] = __uint_as_float(pr[0]);
+          u[r] = __uint_as_float(pr[1]);
+        }
+        float o[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float gt = bf2f(f2bf(hi ? g[2 + k] : g[k])), up = bf2f(f2bf(hi ? u[2 + k] : u[k]));
+          o[k] = gt * up / (1.f + __expf(-gt));
+        }
+        *reinterpret_cast<uint32_t*>(srow8 + j * 16) = pack2(o[0], o[1]);
       }
     } else {
 #pragma unroll
@@ -490,9 +516,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16_t* __restric
   }
   constexpr int CPR = OUTW / 8;  // 16-B chunks per row
   constexpr int RPI = 64 / CPR;  // rows per wave instruction
-  const int ldy = EPI == TILE_EPI_SWIGLU ? (N >> 1) : N;
-  const int col0 = EPI == TILE_EPI_SWIGLU ? ((n0 + wn * 128) >> 1) : n0 + wn * 128;
-  const int ncols = EPI == TILE_EPI_SWIGLU ? (nrows >> 1) - wn * 64 : nrows - wn * 128;
+  const int ldy = SWG ? (N >> 1) : N;
+  const int col0 = SWG ? ((n0 + wn * 128) >> 1) : n0 + wn * 128;
+  const int ncols = SWG ? (nrows >> 1) - wn * 64 : nrows - wn * 128;
   const int rr2 = lane / CPR, cc2 = lane % CPR;
   // branch-free masked stores: a buffer descriptor over this m-tile's rows drops every store past
   // row mrows (out of range), and a lane whose columns are past N gets an out-of-range offset
@@ -532,14 +558,15 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
     if (epi == TILE_EPI_RESID || rs_part != nullptr) return -1;
     algo = 0;
   }
-  if (N % 16 != 0 || K % 64 != 0 || K < 64 || (epi == TILE_EPI_SWIGLU && N % 256 != 0)) return -1;
+  const bool swg = epi == TILE_EPI_SWIGLU || epi == TILE_EPI_SWIGLU8;
+  if (N % 16 != 0 || K % 64 != 0 || K < 64 || (swg && N % 256 != 0) || epi < 0 || epi > 4) return -1;
   if (epi == TILE_EPI_ROPE && (grouped || N % 128 != 0 || rope_pos == nullptr || rope_cs == nullptr)) return -1;
   if (epi == TILE_EPI_RESID && (grouped || rs || N % 128 != 0 || resid == nullptr || hw == nullptr ||
                                 norm_w == nullptr || ss_out == nullptr || algo != 1))
     return -1;
   // row scale: the fused consumers only (qkv + RoPE, gate_up + SwiGLU), schedule 1
   if (rs && (grouped || algo != 1 || rs_np < 4 || rs_np > 64 || rs_np % 4 != 0 ||
-             (epi != TILE_EPI_ROPE && epi != TILE_EPI_SWIGLU)))
+             (epi != TILE_EPI_ROPE && !swg)))
     return -1;
   const TileEpi ep{rope_pos, rope_cs, rope_heads, rs_part, rs_np, rs_eps, (bf16_t*)resid, (bf16_t*)hw,
                    (const bf16_t*)norm_w, ss_out};
@@ -556,9 +583,11 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
 #define K8_TILE_SCH(SCH_)                                                                                            \
   if (grouped) {                                                                                                     \
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, true, SCH_, false);                                  \
+    else if (epi == TILE_EPI_SWIGLU8) K8_TILE_LAUNCH(TILE_EPI_SWIGLU8, true, SCH_, false);                           \
     else K8_TILE_LAUNCH(TILE_EPI_BF16, true, SCH_, false);                                                           \
   } else {                                                                                                           \
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, SCH_, false);                                 \
+    else if (epi == TILE_EPI_SWIGLU8) K8_TILE_LAUNCH(TILE_EPI_SWIGLU8, false, SCH_, false);                          \
     else if (epi == TILE_EPI_ROPE) K8_TILE_LAUNCH(TILE_EPI_ROPE, false, SCH_, false);                                \
     else K8_TILE_LAUNCH(TILE_EPI_BF16, false, SCH_, false);                                                          \
   }
@@ -566,6 +595,7 @@ extern "C" int k8sllm_gemm_tile(const void* X, const void* W, void* Y, int M, in
     K8_TILE_LAUNCH(TILE_EPI_RESID, false, 1, false);
   } else if (rs) {
     if (epi == TILE_EPI_SWIGLU) K8_TILE_LAUNCH(TILE_EPI_SWIGLU, false, 1, true);
+    else if (epi == TILE_EPI_SWIGLU8) K8_TILE_LAUNCH(TILE_EPI_SWIGLU8, false, 1, true);
     else K8_TILE_LAUNCH(TILE_EPI_ROPE, false, 1, true);
   } else if (algo == 1) {
     K8_TILE_SCH(1)

@@ -5,9 +5,13 @@
 
 namespace k8sllm {
 
-enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2, TILE_EPI_RESID = 3 };
+enum { TILE_EPI_BF16 = 0, TILE_EPI_SWIGLU = 1, TILE_EPI_ROPE = 2, TILE_EPI_RESID = 3, TILE_EPI_SWIGLU8 = 4 };
 
 // Fused epilogues of the dense prefill projections.
+//
+// TILE_EPI_SWIGLU / TILE_EPI_SWIGLU8: silu(gate) * up of a gate/up-interleaved weight, [64 gate |
+// 64 up] per 128 rows (interleave_gate_up) or [8 gate | 8 up] per 16 rows (interleave_gate_up8:
+// the decode GEMMs' packed copy, so prefill and decode share ONE weight).
 //
 // TILE_EPI_ROPE (the qkv projection): the output columns are heads of 128; a wave's 128-column
 // quarter is exactly one head, and for q / k heads (head < rope_heads) the rotary embedding (neox

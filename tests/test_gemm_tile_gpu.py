@@ -153,3 +153,32 @@ def test_gemm_tile_packed_weights_bit_identical(M, N, K, algo):
         h1, s1 = ops.gemm_tile_resid(x, ops.pack_skinny(w), r1, nw)
         h2, s2 = ops.gemm_tile_resid(x, w, r2, nw)
         assert torch.equal(r1, r2) and torch.equal(h1, h2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("M", [7, 700, 1500])
+@pytest.mark.parametrize("rowscale", [False, True])
+def test_gemm_tile_swiglu8_matches_fp32_and_decode_layout(M, rowscale):
+    """SwiGLU over the decode GEMMs' gate/up copy (interleave_gate_up8, fragment-packed): the
+    features silu(gate) * up against fp32, row-major vs packed bit for bit, dense and grouped -
+    the one weight copy prefill and decode share."""
+    K, F = 512, 768
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
+    w8 = ops.interleave_gate_up8(w13).contiguous()
+    kw = {}
+    xs = x.cpu().float()
+    if rowscale:
+        ss = (torch.rand(M, K // 128, device=DEV) * 64 + 16).contiguous()
+        kw = dict(algo=1, rowscale=(ss, 1e-5))
+        xs = xs * torch.rsqrt(ss.cpu().sum(1, keepdim=True) / K + 1e-5)
+    y = ops.gemm_tile(x, ops.pack_skinny(w8), swiglu=8, **kw)
+    assert torch.equal(y, ops.gemm_tile(x, w8, swiglu=8, **kw))
+    gu = F_.linear(xs, w13.cpu().float()).to(torch.bfloat16).float()
+    r = F_.silu(gu[:, :F]) * gu[:, F:]
+    _close(y.cpu(), r, atol=3e-2, rtol=2e-2, what="swiglu8")
+    if not rowscale:
+        counts = [M // 2, M - M // 2]
+        off = torch.tensor([0, counts[0], M], dtype=torch.int32, device=DEV)
+        we = torch.stack([ops.pack_skinny(w8), ops.pack_skinny(w8.flip(1).contiguous())]).contiguous()
+        yg = ops.gemm_tile(x, we, off, swiglu=8)
+        assert torch.equal(yg[: counts[0]], y[: counts[0]])

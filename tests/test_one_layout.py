@@ -1,0 +1,111 @@
+"""ONE_LAYOUT: a dense Llama keeps ONE resident copy of every projection - the
+decode GEMMs' fragment-packed layout, read by the prefill tile GEMM as well.  CPU forms: the
+packed model computes what the row-major model computes (prefill and decode), its canonical
+weights round-trip bit-exactly, and checkpoint export sees row-major tensors.  (GPU numerics of
+the packed tile GEMM: test_gemm_tile_gpu.py; end to end: test_tile_real_shapes_gpu.py.)"""
+import pytest
+import torch
+
+from k8s_llm_monitor_amd import ops
+from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
+
+
+def _pair(monkeypatch):
+    cfg = get_config("llama-tiny-d128")
+    monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
+    ref = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=11)
+    monkeypatch.setattr(CausalLM, "ONE_LAYOUT", "force")
+    one = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=11)
+    return ref, one
+
+
+def test_one_layout_single_packed_copy(monkeypatch):
+    ref, one = _pair(monkeypatch)
+    assert one._packed and not ref._packed and one._swg == 8
+    for L, L0 in zip(one.layers, ref.layers):
+        for key in ("wqkv", "wo", "w13", "w2"):
+            assert L[key].dim() == 4 and L[key] is L[key + "_d"]  # the decode copy IS the weight
+            assert key + "_p" not in L
+            assert torch.equal(one.canonical(L, key), ref.canonical(L0, key))
+    assert one.num_local_params() == ref.num_local_params()
+
+
+def test_one_layout_prefill_and_decode_match_rowmajor(monkeypatch):
+    ref, one = _pair(monkeypatch)
+    bs, nb = 16, 8
+    g = torch.Generator().manual_seed(0)
+    kv0 = [(torch.randn(nb, ref.hkv, ref.D // 8, bs, 8, generator=g), torch.randn(nb, ref.hkv, ref.D, bs, generator=g))
+           for _ in ref.layers]
+    kv1 = [(k.clone(), v.clone()) for k, v in kv0]
+    # prefill: two prompts of 5 and 9 tokens into blocks 0 and 1..2
+    T = torch.tensor([5, 9])
+    ids = torch.randint(0, 1000, (14,), generator=g, dtype=torch.int32)
+    pos = torch.cat([torch.arange(5), torch.arange(9)]).to(torch.int32)
+    slots = torch.cat([torch.arange(5), 16 + torch.arange(9)]).to(torch.int32)
+    cu = torch.tensor([0, 5, 14], dtype=torch.int32)
+    meta = AttnMeta(is_prefill=True, positions=pos, slot_mapping=slots, cu_seqlens=cu,
+                    logits_idx=torch.tensor([4, 13]))
+    a = ref.forward(ids, meta, kv0)
+    b = one.forward(ids, meta, kv1)
+    assert (a - b).abs().max().item() < 1e-4
+    for (k0, v0), (k1, v1) in zip(kv0, kv1):
+        assert (k0 - k1).abs().max().item() < 1e-5 and (v0 - v1).abs().max().item() < 1e-5
+    # one decode step of both sequences
+    lens = T + 1
+    dm = AttnMeta(is_prefill=False, positions=(lens - 1).to(torch.int32), slot_mapping=torch.tensor([5, 25], dtype=torch.int32),
+                  block_tables=torch.tensor([[0, 3], [1, 2]], dtype=torch.int32), seq_lens=lens.to(torch.int32))
+    nid = torch.tensor([7, 99], dtype=torch.int32)
+    a = ref.forward(nid, dm, kv0)
+    b = one.forward(nid, dm, kv1)
+    assert (a - b).abs().max().item() < 1e-4
+
+
+def test_one_layout_checkpoint_export_is_rowmajor(monkeypatch):
+    from k8s_llm_monitor_amd.models.checkpoint import hf_state_dict
+
+    ref, one = _pair(monkeypatch)
+    sd0 = dict(hf_state_dict(ref))
+    sd1 = dict(hf_state_dict(one))
+    assert sd0.keys() == sd1.keys()
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+
+
+def test_one_layout_reinit_restores_rowmajor(monkeypatch):
+    """_init_skinny over packed weights (e.g. after a DECODE_GEMM change) starts from the canonical
+    tensors again instead of packing the packed copy."""
+    ref, one = _pair(monkeypatch)
+    monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
+    one._init_skinny()
+    assert not one._packed
+    for L, L0 in zip(one.layers, ref.layers):
+        for key in ("wqkv", "wo", "w13", "w2"):
+            assert L[key].dim() == 2 and torch.equal(L[key], L0[key])
+
+
+@pytest.mark.gpu
+def test_one_layout_gpu_matches_two_layouts():
+    """On the GPU the one packed copy gives the row-major model's logits: prefill (1300 tokens: the
+    tile GEMMs with the fused norms, packed W and the per-16 SwiGLU pairing) and a decode step
+    (the decode GEMMs read the same packed tensors either way)."""
+    cfg = get_config("llama-tiny-d128")
+    CausalLM.ONE_LAYOUT = False
+    try:
+        two = CausalLM(cfg, device="cuda", dtype=torch.bfloat16, seed=5)
+    finally:
+        CausalLM.ONE_LAYOUT = True
+    one = CausalLM(cfg, device="cuda", dtype=torch.bfloat16, seed=5)
+    assert one._packed and not two._packed
+    n = 1300
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(3, cfg.vocab_size, (n,), generator=g, dtype=torch.int32).cuda()
+    rows = [0, 511, 1024, n - 1]
+    meta = AttnMeta(is_prefill=True, positions=torch.arange(n, dtype=torch.int32, device="cuda"),
+                    slot_mapping=torch.full((n,), -1, dtype=torch.int32, device="cuda"),
+                    cu_seqlens=torch.tensor([0, n], dtype=torch.int32, device="cuda"),
+                    logits_idx=torch.tensor(rows, device="cuda"))
+    a = two.forward(ids, meta, None).float()
+    b = one.forward(ids, meta, None).float()
+    scale = float(a.abs().max())
+    err = float((a - b).abs().max())
+    assert err <= 1e-3 * scale, f"one layout vs two: max err {err} (scale {scale})"

@@ -25,9 +25,16 @@ def _fp32_reference(gpu_model):
     if ref.lm_head is not ref.embed:
         ref.lm_head.copy_(gpu_model.lm_head.float().cpu())
     ref.final_norm.copy_(gpu_model.final_norm.float().cpu())
+    from k8s_llm_monitor_amd import ops
+
     for Lr, Lg in zip(ref.layers, gpu_model.layers):
         for k, v in Lr.items():
-            if not k.endswith("_p") and not k.endswith("_pg"):
+            if k.endswith(("_p", "_pg", "_d", "_dg")):
+                continue
+            if gpu_model._packed and k in ("wqkv", "wo", "w13", "w2"):  # ONE_LAYOUT: the packed copy only
+                w = gpu_model.canonical(Lg, k).float().cpu()
+                v.copy_(ops.interleave_gate_up(w) if k == "w13" and ref._w13_il else w)
+            else:
                 v.copy_(Lg[k].float().cpu())
     return ref
 
@@ -55,7 +62,10 @@ def test_gpu_real_shape_engine_matches_fp32_reference(model, layers):
     eng = LLMEngine(EngineConfig(model=model, model_overrides={"n_layers": layers}, max_num_seqs=8,
                                  max_model_len=2048, kv_cache_gb=1.0, seed=21), device="cuda")
     eng.warmup()
-    assert eng.runner.graphs and "wqkv_p" in eng.model.layers[0], "skinny decode path not active"
+    L0 = eng.model.layers[0]
+    assert eng.runner.graphs and ("wqkv_p" in L0 or "wqkv_d" in L0), "skinny decode path not active"
+    if model == "llama-3-8b":  # dense Llama: one resident copy, packed (CausalLM.ONE_LAYOUT)
+        assert eng.model._packed and L0["w13"] is L0["w13_d"] and "w13_p" not in L0
     prompts = ["集群状态概览: node-001 CPU=93.1% [资源压力] MEM=88% 为什么我的pod频繁重启？ " * 3,
                "Why is pod default/api-gateway not ready? kube-system coredns CrashLoopBackOff " * 2,
                "node-007 NotReady, payments-api OOMKilled x12"]

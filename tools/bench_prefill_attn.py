@@ -26,7 +26,6 @@ def main() -> None:
     ap.add_argument("--orders", default="seq", help="q-block orders to time (ops.prefill_qblocks order)")
     ap.add_argument("--hq", type=int, default=32, help="query heads (64: Llama-3-70B at TP=1)")
     ap.add_argument("--hkv", type=int, default=8)
-    ap.add_argument("--stag", default="1", help="paged kernel main loops to time: 1 staggered, 0 unstaggered")
     a = ap.parse_args()
     Hq, Hkv, D = a.hq, a.hkv, 128
     T = a.seqs * a.len
@@ -68,20 +67,9 @@ def main() -> None:
         qs, st = ops.prefill_qblocks(cu.tolist(), order=order)
         qbo[order] = (torch.tensor(qs, dtype=torch.int32, device="cuda"),
                       torch.tensor(st, dtype=torch.int32, device="cuda"))
-    outs = {}
-    for sg in a.stag.split(","):  # the staggered and unstaggered loops give the same bits
-        ops.native().flash_stagger(int(sg))
-        o2 = torch.empty_like(out)
-        ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qbo[next(iter(qbo))], out=o2, paged=(cst, kc, vc, bt))
-        outs[sg] = o2
-    ref_o = next(iter(outs.values()))
-    for sg, o2 in outs.items():
-        if not torch.equal(o2, ref_o):
-            raise SystemExit(f"stagger {sg} differs")
     for _ in range(3):
-        for order, sg in [(o_, s_) for o_ in qbo for s_ in a.stag.split(",")]:
-            ops.native().flash_stagger(int(sg))
-            tag = f"paged_v2_{order}_stag{sg}"
+        for order in qbo:
+            tag = f"paged_v2_{order}"
             qb = qbo[order]
             for _ in range(3):
                 ops.flash_prefill(qkv, cu, Hq, Hkv, D, D ** -0.5, qblocks=qb, out=out, paged=(cst, kc, vc, bt))
@@ -96,7 +84,6 @@ def main() -> None:
         us = min(ts)
         print(json.dumps({"seqs": a.seqs, "len": a.len, "hq": Hq, "hkv": Hkv, "kernel": tag, "us": round(us, 1),
                           "PFps": round(flops / us / 1e9, 3)}))
-    ops.native().flash_stagger(0)
 
 
 if __name__ == "__main__":
