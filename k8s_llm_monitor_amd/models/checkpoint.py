@@ -284,7 +284,7 @@ def hf_state_dict(model) -> Iterator[tuple[str, torch.Tensor]]:
     nq, nk = c.n_heads * D, c.n_kv_heads * D
     yield "model.embed_tokens.weight", model.embed[:V]
     if not c.tie_embeddings:
-        yield "lm_head.weight", model.lm_head[:V]
+        yield "lm_head.weight", model.canonical_head()[:V]
     yield "model.norm.weight", model.final_norm
     for i, L in enumerate(model.layers):
         p = f"model.layers.{i}."

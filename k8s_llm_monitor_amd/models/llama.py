@@ -682,6 +682,12 @@ class CausalLM:
         elif hd is not None and x.is_cuda and x.shape[0] <= ops.SKINNY_MAX_M:
             logits = torch.empty(x.shape[0], hd.shape[0] * 16, dtype=self.dtype, device=self.device)
             ops.dec_gemm(ops.pack_activation(x), hd, 1, x.shape[0], out=logits)
+        elif self.lm_head.dim() == 4:  # ONE_LAYOUT: the packed head is the only copy - 64-row chunks
+            M, mc = x.shape[0], ops.SKINNY_MAX_M
+            logits = torch.empty(M, hd.shape[0] * 16, dtype=self.dtype, device=self.device)
+            for i in range(0, M, mc):
+                m = min(mc, M - i)
+                ops.dec_gemm(ops.pack_activation(x[i:i + m]), hd, 1, m, out=logits[i:i + m])
         else:
             logits = F.linear(x, self.lm_head)
         logits = tp_all_gather_last(logits, self.ps)
@@ -720,6 +726,8 @@ class CausalLM:
         self._skinny_ws = None
         self.lm_head_d = None
         self._rc_o = 0
+        if self.lm_head.dim() == 4:
+            self.lm_head = self.canonical_head().contiguous()
         if self._packed:  # re-initialised over ONE_LAYOUT weights: back to the canonical row-major form
             for L in self.layers:
                 for key in ("wqkv", "wo", "w13", "w2"):
@@ -959,6 +967,11 @@ class CausalLM:
                 and ops.dec_available(f2, d, 2) and ops.dec_available(d, f2 // 2, 0) and d % 256 == 0
                 and f2 % 256 == 0)
 
+    def canonical_head(self) -> torch.Tensor:
+        """The LM head as row-major [vocab shard, d] (ONE_LAYOUT keeps only its packed copy)."""
+        h = self.lm_head
+        return ops.unpack_skinny(h) if h.dim() == 4 else h
+
     def canonical(self, L: dict, key: str) -> torch.Tensor:
         """A dense projection as the row-major [out, in] weight of the reference / the checkpoint
         format (w13 as [gate; up]), whatever its resident layout (row-major, gate/up interleaved
@@ -968,6 +981,40 @@ class CausalLM:
             w = ops.unpack_skinny(w)
             return ops.deinterleave_gate_up8(w) if key == "w13" else w
         return ops.deinterleave_gate_up(w) if key == "w13" and self._w13_il else w
+
+    @torch.no_grad()
+    def copy_weights_from(self, src: "CausalLM") -> None:
+        """Copy ``src``'s weights into this model (same config and TP shard; any device / dtype /
+        resident layout on either side - the dense projections go through their canonical form),
+        then rebuild this model's derived decode copies.  Used to give an fp32 CPU reference the
+        GPU model's exact weights."""
+        dense = ("wqkv", "wo", "w13", "w2")
+        self.embed.copy_(src.embed)
+        if self.lm_head is not self.embed:
+            h = src.canonical_head().to(self.lm_head.device)
+            self.lm_head.copy_(ops.pack_skinny(h) if self.lm_head.dim() == 4 else h)
+        for a, b in zip(self.final_norm if isinstance(self.final_norm, tuple) else (self.final_norm,),
+                        src.final_norm if isinstance(src.final_norm, tuple) else (src.final_norm,)):
+            a.copy_(b)
+        derived = False
+        for Ld, Ls in zip(self.layers, src.layers):
+            for k, v in Ld.items():
+                if k.endswith(("_p", "_pg", "_d", "_dg")):
+                    derived = True
+                    continue
+                if k in dense and not self.cfg.is_moe and (self._packed or src._packed):
+                    w = src.canonical(Ls, k).to(v.device)
+                    if v.dim() == 4:
+                        v.copy_(ops.pack_skinny(ops.interleave_gate_up8(w) if k == "w13" else w))
+                    else:
+                        v.copy_(ops.interleave_gate_up(w) if k == "w13" and self._w13_il else w)
+                elif isinstance(v, tuple):
+                    for a, b in zip(v, Ls[k]):
+                        a.copy_(b)
+                else:
+                    v.copy_(Ls[k])
+        if derived and not self._packed:  # separate decode copies (two-layout / MoE) are stale now
+            self._init_skinny()
 
     def _init_dec(self) -> None:
         """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
@@ -1002,9 +1049,11 @@ class CausalLM:
                     L["w13_dg"] = torch.stack([ops.pack_skinny(ops.interleave_gate_up8(
                         ops.deinterleave_gate_up(w) if self._w13_il else w)) for w in L["w13"]])
                     L["w2_dg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
-        N, K = self.lm_head.shape
+        N, K = ops.w_out(self.lm_head), ops.w_in(self.lm_head)
         if "head" in parts and N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
-            self.lm_head_d = ops.pack_skinny(self.lm_head)
+            self.lm_head_d = self.lm_head if self.lm_head.dim() == 4 else ops.pack_skinny(self.lm_head)
+            if one and self.lm_head is not self.embed:
+                self.lm_head = self.lm_head_d  # ONE_LAYOUT: the packed head is the only copy too
         self._packed = one
         self._swg = 8 if one else True  # the prefill SwiGLU's gate/up interleave (gemm_tile swiglu)
 

@@ -49,4 +49,4 @@ def fp32_logits(model, ids: torch.Tensor, rows: Optional[list] = None, device: O
         x = x + (F.silu(gu[:, :f]) * gu[:, f:]) @ w(model.canonical(L, "w2")).t()
     rows = [T - 1] if rows is None else rows
     h = F.rms_norm(x[rows], (c.d_model,), w(model.final_norm), c.norm_eps)
-    return (h @ w(model.lm_head).t())[:, : c.vocab_size]
+    return (h @ w(model.canonical_head()).t())[:, : c.vocab_size]

@@ -35,6 +35,42 @@
 // epoch this holds for any sequence of message sizes and call kinds.
 // Signal blocks live in uncached device memory (hipDeviceMallocUncached); data buffers are plain
 // hipMalloc memory ordered by the release/acquire pairs.
+//
+// Memory-ordering argument (car_exchange; the HSA / AMDGPU memory model as it applies to gfx950,
+// where each XCD has its own L2 that is NOT coherent with the other XCDs' L2s or with a peer GPU for
+// coarse-grained hipMalloc memory):
+//  (a) producer side.  Every thread's staging stores are complete at its L2 before the barrier
+//      (`s_waitcnt vmcnt(0)` per thread, then __syncthreads: the barrier orders them before lane 0's
+//      next instruction).  Lane 0's system-scope RELEASE fence then writes back the dirty lines of
+//      this XCD's L2 - the whole cache, so the other threads' completed stores are included - and
+//      waits for the write-back before any later store issues.  The flag stores that follow are
+//      therefore ordered after the data at system scope (release fence + relaxed store = a
+//      release store), wherever the data lives (our staging buffer: a peer reads it over xGMI
+//      from our HBM).
+//  (b) flag transport.  Flags live in the READER's signal block, uncached memory: the remote
+//      store goes straight to the reader's HBM and the reader's relaxed system-scope polls bypass
+//      every cache, so a poll cannot be satisfied from a stale line and observes the store once it
+//      lands.  Flags only grow (epochs), compared wrap-safe as `(int)(flag - e) >= 0`.
+//  (c) consumer side.  Lanes r < W each observe flag[r][b] >= e, then __syncthreads, then lane 0
+//      issues a system-scope ACQUIRE fence, which invalidates this CU's L1 and the non-coherent
+//      lines of this XCD's L2; a second __syncthreads orders every thread's subsequent loads of
+//      the peers' staged data after that invalidation, so they are served from memory written
+//      under (a) - the acquire synchronizes-with each peer's release through the flag it read.
+//      All threads of a workgroup share one CU, so the one L1 invalidation covers them.
+//  (d) two-shot.  Round 2 repeats (a)-(c) over flag2 for the part each rank reduced IN PLACE in
+//      its own staging buffer; that reduction reads peers' data (after the round-1 acquire) and
+//      writes only the own buffer (before the round-2 release).
+//  (e) reuse / epochs.  Half e & 1 of the double buffer is rewritten only in call e + 2; the
+//      argument above ("Buffer-reuse safety") shows every peer has finished reading it by then.
+//      `epoch` / `done` are agent-scope counters touched only by this rank's own kernels, ordered
+//      between launches by stream order (a kernel boundary is a full agent-scope release/acquire),
+//      and within a call only the last-arriving workgroup (fetch_add on `done`) publishes it.
+//  (f) liveness.  Every spin is bounded (spin_limit); a missing peer sets `err` (checked on the host
+//      after the step) and the kernel still completes, so a failed peer cannot hang the GPU.
+// Exercised before the engine may use the IPC path: custom_ar.self_test runs every mode against
+// exact integer references (tests/test_custom_ar.py at W = 2 / 4 / 8 on one GPU, where the same
+// fences order the ranks' accesses across XCDs of that GPU).  Over xGMI between GPUs the protocol
+// has NOT been measured: no multi-GPU node was available to this work.
 #include <hip/hip_runtime.h>
 #include <string.h>
 

@@ -28,6 +28,9 @@ def test_one_layout_single_packed_copy(monkeypatch):
             assert key + "_p" not in L
             assert torch.equal(one.canonical(L, key), ref.canonical(L0, key))
     assert one.num_local_params() == ref.num_local_params()
+    assert one.lm_head is one.lm_head_d and torch.equal(one.canonical_head(), ref.lm_head)
+    x = torch.randn(70, ref.cfg.d_model)  # > 64 rows: the packed head in 64-row chunks
+    assert (one._logits(x) - ref._logits(x)).abs().max().item() < 1e-4
 
 
 def test_one_layout_prefill_and_decode_match_rowmajor(monkeypatch):
@@ -109,3 +112,21 @@ def test_one_layout_gpu_matches_two_layouts():
     scale = float(a.abs().max())
     err = float((a - b).abs().max())
     assert err <= 1e-3 * scale, f"one layout vs two: max err {err} (scale {scale})"
+
+
+def test_copy_weights_between_layouts(monkeypatch):
+    """copy_weights_from moves weights between a packed (ONE_LAYOUT) and a row-major model in either
+    direction (the GPU tests build their fp32 CPU references this way)."""
+    ref, one = _pair(monkeypatch)
+    cfg = get_config("llama-tiny-d128")
+    monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
+    a = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=99, init="empty")
+    a.copy_weights_from(one)
+    monkeypatch.setattr(CausalLM, "ONE_LAYOUT", "force")
+    b = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=99, init="empty")
+    b.copy_weights_from(ref)
+    for L0, La, Lb in zip(ref.layers, a.layers, b.layers):
+        for key in ("wqkv", "wo", "w13", "w2"):
+            assert torch.equal(a.canonical(La, key), ref.canonical(L0, key))
+            assert torch.equal(b.canonical(Lb, key), ref.canonical(L0, key))
+        assert torch.equal(La["wo_d"], L0["wo_d"])  # a's decode copies were rebuilt from the new weights

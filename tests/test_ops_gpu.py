@@ -412,14 +412,7 @@ def test_llama_decode_skinny_matches_generic(monkeypatch):
     b = m.forward(ids, meta, kv).float()
     # fp32 CPU reference of the same decode step (same weights, the pre-step caches)
     rm = CausalLM(cfg, device="cpu", dtype=torch.float32, init="empty")
-    rm.embed.copy_(m.embed.float().cpu())
-    if rm.lm_head is not rm.embed:
-        rm.lm_head.copy_(m.lm_head.float().cpu())
-    rm.final_norm.copy_(m.final_norm.float().cpu())
-    for Lr, Lg in zip(rm.layers, m.layers):
-        for k, v in Lr.items():
-            if not k.endswith("_p") and not k.endswith("_pg"):
-                v.copy_(Lg[k].float().cpu())
+    rm.copy_weights_from(m)
     cpu = lambda t: t.cpu() if t is not None else None  # noqa: E731
     meta_c = AttnMeta(is_prefill=False, positions=cpu(meta.positions), slot_mapping=cpu(meta.slot_mapping),
                       block_tables=cpu(bt), seq_lens=cpu(lens))

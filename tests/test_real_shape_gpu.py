@@ -21,21 +21,7 @@ def _fp32_reference(gpu_model):
         ref = CausalLM(gpu_model.cfg, device="cpu", dtype=torch.float32, pstate=ParallelState(), init="empty")
     finally:
         CausalLM.SKINNY_DECODE = True
-    ref.embed.copy_(gpu_model.embed.float().cpu())
-    if ref.lm_head is not ref.embed:
-        ref.lm_head.copy_(gpu_model.lm_head.float().cpu())
-    ref.final_norm.copy_(gpu_model.final_norm.float().cpu())
-    from k8s_llm_monitor_amd import ops
-
-    for Lr, Lg in zip(ref.layers, gpu_model.layers):
-        for k, v in Lr.items():
-            if k.endswith(("_p", "_pg", "_d", "_dg")):
-                continue
-            if gpu_model._packed and k in ("wqkv", "wo", "w13", "w2"):  # ONE_LAYOUT: the packed copy only
-                w = gpu_model.canonical(Lg, k).float().cpu()
-                v.copy_(ops.interleave_gate_up(w) if k == "w13" and ref._w13_il else w)
-            else:
-                v.copy_(Lg[k].float().cpu())
+    ref.copy_weights_from(gpu_model)
     return ref
 
 
