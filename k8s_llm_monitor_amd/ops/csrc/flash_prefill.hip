@@ -465,7 +465,11 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   // basic block.  Round 6: a staggered form - the two waves of a SIMD half a tile apart, one's
   // softmax under the other's MFMAs: PV(t-1) + QK(t) then softmax(t) vs softmax(t-1) then
   // PV(t-1) + QK(t), K in two 8-fragment halves, 196 VGPRs - was bit-identical and 3-8 % SLOWER at
-  // 10 x 1609, 64 x 1609 and 2 x 8192, Hq 32 and 64: profiles/r06/flash_stagger_ab.jsonl.)  The wave computes only its first nt_w tiles (later ones are in the future of
+  // 10 x 1609, 64 x 1609 and 2 x 8192, Hq 32 and 64: profiles/r06/flash_stagger_ab.jsonl.  A
+  // persistent form - one workgroup per CU walking these work items, the next item's first three
+  // tiles DMA'd under the current item's last three - was bit-identical and 0-14 % SLOWER: the
+  // static item assignment loses more to imbalance than the hardware dispatcher's per-workgroup
+  // overhead costs; profiles/r06/flash_persistent_v3_ab.jsonl.)  The wave computes only its first nt_w tiles (later ones are in the future of
   // all its rows) but joins every barrier and issues its DMA pieces for every tile.
   const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
   // (No static priority for the second-dispatched half: with each 16-key group's exponentials

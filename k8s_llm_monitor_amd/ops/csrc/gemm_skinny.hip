@@ -1,6 +1,8 @@
 // Decode-time "skinny" GEMM on gfx950 MFMA: Y[M, N] = A[M, K] . W[N, K]^T for M <= 64 rows (the
-// decode batch), bf16 in, fp32 accumulate.  Every decode projection of a dense Llama layer runs
-// here (qkv, o, gate_up, down); prefill keeps hipBLASLt on the row-major copy of the weights.
+// decode batch), bf16 in, fp32 accumulate.  Serves the decode projections gemm_decode.hip has no
+// launch configuration for (MoE experts as grouped launches, odd shapes) and models built without
+// CausalLM.ONE_LAYOUT; dense Llama decode runs on gemm_decode.hip over the one packed weight copy,
+// which the prefill tile GEMM (gemm_tile.hip) reads as well.
 //
 // Weight layout - "fragment-packed" [N/16][K/32][64 lanes][8] bf16 (pack_weight_for_skinny in
 // ops/__init__.py): the 16x32 B fragment of v_mfma_f32_16x16x32_bf16 for n-tile j, k-step s is one
@@ -248,8 +250,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void gemm_skinny_kernel(const bf16_t
 }
 
 // Row-major weights, LDS-DMA staged: the SAME decomposition, epilogues and fragment-packed A as
-// gemm_skinny_kernel, but W is the plain row-major [N][K] tensor that prefill's hipBLASLt GEMMs
-// also read - one resident copy of every projection (no fragment-packed duplicate).
+// gemm_skinny_kernel, but W is the plain row-major [N][K] tensor (MoE experts, and dense models
+// built without CausalLM.ONE_LAYOUT, whose prefill GEMMs read the same tensor).
 //
 // Why LDS: an MFMA B fragment (16 rows x 32 k) read straight from a row-major W touches 16 rows x
 // 64 B per wave-instruction; whole-line orders stream 1.5-4x faster (tools/membw.hip).  Here each
