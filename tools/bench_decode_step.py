@@ -9,7 +9,9 @@ graphs re-captured between phases.
 Switches: ``rc`` - the row-complete o projection, on in every bucket vs off; ``merge`` - the
 attention's split partials merged in-launch (ops.DECODE_MERGE) vs a paged_decode_reduce launch (CausalLM.set_decode_fusion).  (Round 5
 also A/B'd write-through (sc1) epilogue stores in gemm_decode.hip with this tool: 6.107 vs 6.068
-ms per step, slower - profiles/r05/decode_step_writethrough_ab.jsonl.)
+ms per step, slower - profiles/r05/decode_step_writethrough_ab.jsonl.  Round 6: ``split4*`` - o /
+down on 4 split-K slabs instead of 8 (half the bytes add_norm_partial reads) - 6.02 vs 5.93 ms at 64
+rows, 3.78 vs 3.75 at 16: slower, DEC_TABLE unchanged; profiles/r06/decode_step_split4_ab.jsonl.)
 """
 from __future__ import annotations
 
@@ -25,7 +27,20 @@ import torch  # noqa: E402
 
 SWITCHES = {"rc": lambda m, on: m.set_decode_fusion(rc=on),
             "merge": lambda m, on: setattr(_ops(), "DECODE_MERGE", on is not False),
-            "tw32": lambda m, on: _ops().native().decode_tw_force(32 if on else 0)}
+            "tw32": lambda m, on: _ops().native().decode_tw_force(32 if on else 0),
+            # fewer split-K slabs for o / down (4 splits x 64 column groups of 4-wave workgroups
+            # instead of 8 x 32 of 8-wave ones): half the slab bytes add_norm_partial reads
+            "split4": lambda m, on: _dec_table(on, {(4096, 4096, 0): (4, 1, 4, 16), (4096, 14336, 0): (4, 1, 4, 16)}),
+            "split4o": lambda m, on: _dec_table(on, {(4096, 4096, 0): (4, 1, 4, 16)}),
+            "split4d": lambda m, on: _dec_table(on, {(4096, 14336, 0): (4, 1, 4, 16)})}
+_DEC_DEFAULT: dict = {}
+
+
+def _dec_table(on, alt: dict) -> None:
+    t = _ops().DEC_TABLE
+    for k, v in alt.items():
+        _DEC_DEFAULT.setdefault(k, t.get(k))
+        t[k] = v if on else _DEC_DEFAULT[k]
 
 
 def _ops():
