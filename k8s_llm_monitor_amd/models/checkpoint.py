@@ -194,6 +194,13 @@ def load_checkpoint(model, path: PathLike, strict: bool = True) -> list[str]:
             L["w2"] = put(get(p + "mlp.c_proj.weight").t()[:, f_lo:f_hi])
             L["b2"] = put(get(p + "mlp.c_proj.bias"))
     else:
+        # the resident layout's derived tensors (decode copies; under ONE_LAYOUT the packed weights
+        # themselves) go before their replacements arrive: peak memory stays ~one copy of the model
+        # (Llama-3-70B at TP = 1 would not fit two)
+        model.lm_head_d = None
+        for L in model.layers:
+            for k in [k for k in L if k.endswith(("_p", "_d", "_pg", "_dg"))]:
+                del L[k]
         model.embed = vocab_rows("model.embed_tokens.weight")
         if c.tie_embeddings or "lm_head.weight" not in src:
             model.lm_head = model.embed
