@@ -469,7 +469,11 @@ __global__ __launch_bounds__(512, 2) void flash_prefill_paged_v2_kernel(
   // persistent form - one workgroup per CU walking these work items, the next item's first three
   // tiles DMA'd under the current item's last three - was bit-identical and 0-14 % SLOWER: the
   // static item assignment loses more to imbalance than the hardware dispatcher's per-workgroup
-  // overhead costs; profiles/r06/flash_persistent_v3_ab.jsonl.)  The wave computes only its first nt_w tiles (later ones are in the future of
+  // overhead costs; profiles/r06/flash_persistent_v3_ab.jsonl.  A 4-wave form with two 32-row
+  // units per wave (one wave per SIMD; each LDS fragment feeds twice the MFMAs), plain or with
+  // the units' MFMA / softmax interleaved by sched_group_barrier, was bit-identical and 15-22 %
+  // SLOWER: the softmax VALU needs the second wave per SIMD to hide behind;
+  // profiles/r06/flash_v4_two_unit_ab.jsonl.)  The wave computes only its first nt_w tiles (later ones are in the future of
   // all its rows) but joins every barrier and issues its DMA pieces for every tile.
   const int nt_w = min(ntiles, (wave_q0 + 31) / 64 + 1);
   // (No static priority for the second-dispatched half: with each 16-key group's exponentials
