@@ -703,13 +703,14 @@ class CausalLM:
                 and meta.logits_idx is None and self.SKINNY_DECODE)
 
     def _init_skinny(self) -> None:
-        """Decode-path weights.  The row-major tensors prefill reads serve decode through
-        gemm_skinny_rm_kernel (ops/csrc/gemm_skinny.hip: whole 128-B lines by LDS-DMA; a shape it
-        does not take keeps fragment-packed copies).  On top of that, ``_init_dec`` adds
-        decode-only fragment-packed copies for the shared-A decode GEMM (gemm_decode.hip) where
-        the weights fit a quarter of the device: Llama-3-8B holds 16 GB row-major + 16.5 GB packed
-        (the decode step is ~8 % faster on them: profiles/r04/README.md); 70B at TP=1 keeps the one
-        141 GB copy.
+        """Decode-path weights.  Dense Llama (``ONE_LAYOUT``, round 6): ``_init_dec`` packs every
+        projection and the LM head into the shared-A decode GEMM's fragment-packed layout
+        (gemm_decode.hip) and that packed tensor REPLACES the row-major one - prefill's tile GEMM
+        reads it too (Llama-3-8B: 16.1 GB resident, Llama-3-70B at TP=1: 141 GB with every
+        projection on gemm_decode).  Otherwise (MoE experts, ``ONE_LAYOUT`` off) the row-major
+        tensors prefill reads serve decode through gemm_skinny_rm_kernel (ops/csrc/gemm_skinny.hip:
+        whole 128-B lines by LDS-DMA; a shape it does not take keeps fragment-packed copies), and
+        ``_init_dec`` adds decode-only packed copies where they fit (``_want_dec``).
 
         w13 is stored gate/up-interleaved per 128 rows ([64 gate | 64 up], the SwiGLU epilogue's
         pairing): called on canonical [gate; up] tensors (after _build or load_checkpoint), it
