@@ -303,19 +303,15 @@ def hf_state_dict(model) -> Iterator[tuple[str, torch.Tensor]]:
         yield p + "input_layernorm.weight", L["attn_norm"]
         yield p + "post_attention_layernorm.weight", L["mlp_norm"]
         F = c.ffn_dim
-        from .. import ops
-
-        def canon(w):  # the resident w13 is gate/up-interleaved per 128 rows (CausalLM._init_skinny)
-            return ops.deinterleave_gate_up(w) if model._w13_il else w
 
         if c.is_moe:
             m = p + "block_sparse_moe."
             yield m + "gate.weight", L["router"]
+            w13s, w2s = model.canonical(L, "w13"), model.canonical(L, "w2")  # any resident layout
             for e in range(c.n_experts):
-                w13 = canon(L["w13"][e])
-                yield f"{m}experts.{e}.w1.weight", w13[:F]
-                yield f"{m}experts.{e}.w3.weight", w13[F:]
-                yield f"{m}experts.{e}.w2.weight", L["w2"][e]
+                yield f"{m}experts.{e}.w1.weight", w13s[e][:F]
+                yield f"{m}experts.{e}.w3.weight", w13s[e][F:]
+                yield f"{m}experts.{e}.w2.weight", w2s[e]
         else:
             w13 = model.canonical(L, "w13")
             yield p + "mlp.gate_proj.weight", w13[:F]

@@ -370,8 +370,8 @@ class CausalLM:
             wd.scatter_(1, ids.long(), w)
             out = torch.zeros(T, c.d_model, dtype=torch.float32, device=x.device)
             for j, e in enumerate(range(self.e_lo, self.e_hi)):
-                h = ops.silu_mul(F.linear(x, L["w13"][j]), interleaved=self._w13_il)
-                out += F.linear(h, L["w2"][j]).float() * wd[:, e:e + 1]
+                h = ops.silu_mul(F.linear(x, self._expert(L, "w13", j)), interleaved=self._w13_il)
+                out += F.linear(h, self._expert(L, "w2", j)).float() * wd[:, e:e + 1]
             return out.to(x.dtype)
         offsets, sorted_idx, inv_idx = ops.moe_align(ids, c.n_experts)
         xs = ops.gather_rows(x, sorted_idx, K)
@@ -381,7 +381,7 @@ class CausalLM:
             offl = offsets[self.e_lo:self.e_hi + 1]
             part = self.tp > 1  # other ranks' experts' rows stay zero
             if self._w13_il:
-                h = ops.moe_grouped_gemm(xs, L["w13"], offl, swiglu=True, zero_fill=part)
+                h = ops.moe_grouped_gemm(xs, L["w13"], offl, swiglu=self._swg, zero_fill=part)
             else:
                 h = ops.silu_mul(ops.moe_grouped_gemm(xs, L["w13"], offl, zero_fill=part))
             ys = ops.moe_grouped_gemm(h, L["w2"], offl, zero_fill=part)
@@ -391,8 +391,8 @@ class CausalLM:
         for j, e in enumerate(range(self.e_lo, self.e_hi)):
             a, b = off[e], off[e + 1]
             if b > a:
-                h = ops.silu_mul(F.linear(xs[a:b], L["w13"][j]), interleaved=self._w13_il)
-                ys[a:b] = F.linear(h, L["w2"][j])
+                h = ops.silu_mul(F.linear(xs[a:b], self._expert(L, "w13", j)), interleaved=self._w13_il)
+                ys[a:b] = F.linear(h, self._expert(L, "w2", j))
         return ops.moe_combine(ys, inv_idx, w, T)
 
     def _moe_a2a(self, L: dict, x: torch.Tensor) -> torch.Tensor:
@@ -434,7 +434,7 @@ class CausalLM:
         loc_off[1:] = torch.cumsum(counts, 0).to(torch.int32)
         xs_l = recv[order]
         if self._w13_il:
-            h = ops.moe_grouped_gemm(xs_l, L["w13"], loc_off, swiglu=True, zero_fill=False)
+            h = ops.moe_grouped_gemm(xs_l, L["w13"], loc_off, swiglu=self._swg, zero_fill=False)
         else:
             h = ops.silu_mul(ops.moe_grouped_gemm(xs_l, L["w13"], loc_off, zero_fill=False))
         y = torch.empty_like(recv)
@@ -500,7 +500,17 @@ class CausalLM:
         re = recv_e[:, :npair].reshape(-1).float()
         onehot = (re.unsqueeze(1) == torch.arange(epr, device=x.device, dtype=torch.float32).unsqueeze(0)).float()
         ws = self._skinny_ws
-        if ws is not None and "w13_pg" in L:
+        if ws is not None and "w13_pg" not in L and "w13_dg" in L:
+            # ONE_LAYOUT: the shared-A grouped decode GEMM over the packed experts, 64 rows a launch
+            y = torch.empty(R, d, dtype=x.dtype, device=x.device)
+            E = L["w13_dg"].shape[0]
+            for c0 in range(0, R, ops.SKINNY_MAX_M):
+                mc = min(ops.SKINNY_MAX_M, R - c0)
+                act = torch.empty((E, -(-mc // 16), L["w13_dg"].shape[1] // 4, 64, 8), dtype=x.dtype, device=x.device)
+                ops.dec_gemm_grouped(ops.pack_activation(rows[c0:c0 + mc]), L["w13_dg"], 2, mc, out=act)
+                ns = ops.dec_gemm_grouped(act, L["w2_dg"], 0, mc, workspace=ws, row_w=onehot[c0:c0 + mc].contiguous())
+                ops.reduce_slabs(ws, ns, mc, d, dtype=x.dtype, out=y[c0:c0 + mc])
+        elif ws is not None and "w13_pg" in L:
             y = torch.empty(R, d, dtype=x.dtype, device=x.device)
             # up to 128 rows per grouped launch over the row-major expert weights: at decode batch
             # 64 and TP=2 the P x cap x top-k = 128 received rows stream each local expert ONCE
@@ -514,8 +524,8 @@ class CausalLM:
         else:
             yf = torch.zeros(R, d, dtype=torch.float32, device=x.device)
             for j in range(epr):
-                h = ops.silu_mul(F.linear(rows, L["w13"][j]), interleaved=self._w13_il)
-                yf += F.linear(h, L["w2"][j]).float() * onehot[:, j:j + 1]
+                h = ops.silu_mul(F.linear(rows, self._expert(L, "w13", j)), interleaved=self._w13_il)
+                yf += F.linear(h, self._expert(L, "w2", j)).float() * onehot[:, j:j + 1]
             y = yf.to(x.dtype)
         back = self._a2a_equal(y.view(P, npair, d))
         res = back[dest, torch.arange(npair, device=x.device)]  # [cap*K, d]
@@ -956,17 +966,34 @@ class CausalLM:
         """ONE_LAYOUT applies: dense Llama whose four projections all have a decode configuration
         (the shapes are the same in every layer, so layer 0 decides)."""
         c = self.cfg
-        if not (self.ONE_LAYOUT and c.arch == "llama" and not c.is_moe and self.layers and self.SKINNY_DECODE
+        if not (self.ONE_LAYOUT and c.arch == "llama" and self.layers and self.SKINNY_DECODE
                 and self.DECODE_GEMM not in ("rm", "0", "off")
                 and (self.device.type == "cuda" or self.ONE_LAYOUT == "force")):
             return False
         L = self.layers[0]
-        if L["wqkv"].dim() != 2 or L["w13"].dim() != 2:
+        if L["wqkv"].dim() != 2 or L["w13"].dim() != (3 if c.is_moe else 2):
             return False
-        (nq, d), (f2, _) = L["wqkv"].shape, L["w13"].shape
-        return (ops.dec_available(nq, d, 0) and ops.dec_available(d, nq - 2 * self.hkv * self.D, 0)
-                and ops.dec_available(f2, d, 2) and ops.dec_available(d, f2 // 2, 0) and d % 256 == 0
-                and f2 % 256 == 0)
+        (nq, d), (f2, _) = L["wqkv"].shape, L["w13"].shape[-2:]
+        attn = ops.dec_available(nq, d, 0) and ops.dec_available(d, nq - 2 * self.hkv * self.D, 0)
+        if c.is_moe:  # every local expert on the grouped (grid.z = expert) decode GEMM and the grouped tile GEMM
+            E = L["w13"].shape[0]
+            mlp = (ops.dec_config(f2, d, 2, experts=E) is not None
+                   and ops.dec_config(d, f2 // 2, 0, experts=E) is not None)
+        else:
+            mlp = ops.dec_available(f2, d, 2) and ops.dec_available(d, f2 // 2, 0)
+        return attn and mlp and d % 256 == 0 and f2 % 256 == 0
+
+    def _expert(self, L: dict, key: str, j: int) -> torch.Tensor:
+        """Local expert j's weight row-major as the per-expert fallback paths read it (w13 in the
+        ``_w13_il`` pairing), whatever the resident layout (ONE_LAYOUT: packed [E, N/16, K/32, 64, 8])."""
+        w = L[key][j]
+        if w.dim() == 2:
+            return w
+        w = ops.unpack_skinny(w)
+        if key == "w13":
+            w = ops.deinterleave_gate_up8(w)
+            return ops.interleave_gate_up(w) if self._w13_il else w
+        return w
 
     def canonical_head(self) -> torch.Tensor:
         """The LM head as row-major [vocab shard, d] (ONE_LAYOUT keeps only its packed copy)."""
@@ -978,7 +1005,12 @@ class CausalLM:
         format (w13 as [gate; up]), whatever its resident layout (row-major, gate/up interleaved
         per 128 rows, or the one fragment-packed copy)."""
         w = L[key]
-        if w.dim() == 4:  # ONE_LAYOUT: fragment-packed (w13: interleaved per 16 rows)
+        if w.dim() == 5 or (w.dim() == 3 and self.cfg.is_moe):  # MoE experts [E, ...]
+            return torch.stack([self._canon2(e, key, e.dim() == 4) for e in w])
+        return self._canon2(w, key, w.dim() == 4)
+
+    def _canon2(self, w: torch.Tensor, key: str, packed: bool) -> torch.Tensor:
+        if packed:  # ONE_LAYOUT: fragment-packed (w13: interleaved per 16 rows)
             w = ops.unpack_skinny(w)
             return ops.deinterleave_gate_up8(w) if key == "w13" else w
         return ops.deinterleave_gate_up(w) if key == "w13" and self._w13_il else w
@@ -1003,12 +1035,15 @@ class CausalLM:
                 if k.endswith(("_p", "_pg", "_d", "_dg")):
                     derived = True
                     continue
-                if k in dense and not self.cfg.is_moe and (self._packed or src._packed):
+                if k in dense and (self._packed or src._packed):
                     w = src.canonical(Ls, k).to(v.device)
-                    if v.dim() == 4:
-                        v.copy_(ops.pack_skinny(ops.interleave_gate_up8(w) if k == "w13" else w))
-                    else:
-                        v.copy_(ops.interleave_gate_up(w) if k == "w13" and self._w13_il else w)
+                    ws = list(w) if w.dim() == 3 else [w]  # MoE: per expert
+                    vs = list(v) if v.dim() in (3, 5) else [v]
+                    for vd, wd in zip(vs, ws):
+                        if vd.dim() == 4:
+                            vd.copy_(ops.pack_skinny(ops.interleave_gate_up8(wd) if k == "w13" else wd))
+                        else:
+                            vd.copy_(ops.interleave_gate_up(wd) if k == "w13" and self._w13_il else wd)
                 elif isinstance(v, tuple):
                     for a, b in zip(v, Ls[k]):
                         a.copy_(b)
@@ -1039,7 +1074,7 @@ class CausalLM:
                 if ops.dec_available(w.shape[0], w.shape[1], 2):
                     L["w13_d"] = ops.pack_skinny(ops.interleave_gate_up8(w))
                 del w
-            if one:
+            if one and not c.is_moe:
                 for key in ("wqkv", "wo", "w13", "w2"):
                     L[key] = L[key + "_d"]
                     L.pop(key + "_p", None)  # the skinny kernel's reference to the row-major tensor
@@ -1050,6 +1085,13 @@ class CausalLM:
                     L["w13_dg"] = torch.stack([ops.pack_skinny(ops.interleave_gate_up8(
                         ops.deinterleave_gate_up(w) if self._w13_il else w)) for w in L["w13"]])
                     L["w2_dg"] = torch.stack([ops.pack_skinny(w) for w in L["w2"]])
+                if one:  # ONE_LAYOUT: the packed attention projections and experts are the only copies
+                    for key in ("wqkv", "wo"):
+                        L[key] = L[key + "_d"]
+                        L.pop(key + "_p", None)
+                    L["w13"], L["w2"] = L["w13_dg"], L["w2_dg"]
+                    L.pop("w13_pg", None)
+                    L.pop("w2_pg", None)
         N, K = ops.w_out(self.lm_head), ops.w_in(self.lm_head)
         if "head" in parts and N % 16 == 0 and K % 32 == 0 and ops.dec_available(N, K, 1):
             self.lm_head_d = self.lm_head if self.lm_head.dim() == 4 else ops.pack_skinny(self.lm_head)

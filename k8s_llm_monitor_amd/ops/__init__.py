@@ -920,7 +920,13 @@ def moe_grouped_gemm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, sw
     a slice for this rank's experts).  ``swiglu``: ``w`` is gate/up-interleaved and the result is
     silu(gate) * up [rows, N / 2].  Rows of other experts are left as in ``out`` (zeros when
     allocated here).  GPU: no host synchronisation (gemm_tile.hip 256 x 256 tiles where N % 256 == 0,
-    else moe_gemm.hip)."""
+    else moe_gemm.hip).  A fragment-packed ``w`` [E, N/16, K/32, 64, 8] (ONE_LAYOUT; ``swiglu=8``:
+    the per-16 gate/up pairing) always takes the tile kernel."""
+    if w.dim() == 5:
+        if out is None:
+            alloc = torch.zeros if zero_fill else torch.empty
+            out = alloc(x.shape[0], w.shape[1] * 8 if swiglu else w.shape[1] * 16, dtype=x.dtype, device=x.device)
+        return gemm_tile(x, w, offsets, swiglu=swiglu, out=out, algo=TILE_ALGO)
     E, N, K = w.shape
     if out is None:  # zero_fill=False when ``offsets`` covers every row (all experts are local)
         alloc = torch.zeros if zero_fill else torch.empty

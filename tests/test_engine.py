@@ -170,7 +170,9 @@ def test_gpu_moe_decode_grouped_skinny_matches_recompute():
     eng = LLMEngine(EngineConfig(model="mixtral-tiny-d128", max_num_seqs=8, max_model_len=1024, num_blocks=256),
                     device="cuda")
     eng.warmup()
-    assert eng.runner.graphs and "w13_pg" in eng.model.layers[0]
+    L0 = eng.model.layers[0]
+    assert eng.runner.graphs and ("w13_pg" in L0 or "w13_dg" in L0)
+    assert eng.model._packed and L0["w13"] is L0["w13_dg"]  # ONE_LAYOUT: the packed experts are the weights
     _check_greedy_consistency(eng, ["why is pod default/api not ready?", "kube-system coredns " * 20, "x" * 100],
                               8, "cuda")
 

@@ -103,10 +103,10 @@ def test_moe_decode_beyond_skinny_rows_grouped_in_graph(T):
     tw = tw / tw.sum(-1, keepdim=True)
     F = cfg.ffn_dim
     r = torch.zeros_like(xf)
+    w13s, w2s = gm.canonical(L, "w13"), gm.canonical(L, "w2")  # [gate; up] whatever the resident layout
     for e in range(cfg.n_experts):
-        w13 = ops.deinterleave_gate_up(L["w13"][e]).float() if gm._w13_il else L["w13"][e].float()
-        gu = xf @ w13.t()
-        h = (F_.silu(gu[:, :F]) * gu[:, F:]) @ L["w2"][e].float().t()
+        gu = xf @ w13s[e].float().t()
+        h = (F_.silu(gu[:, :F]) * gu[:, F:]) @ w2s[e].float().t()
         r += h * (tw * (ti == e)).sum(-1, keepdim=True)
     _close(y, r, atol=5e-2, rtol=5e-2, what=f"decode moe T{T}")
     xs = x.clone()

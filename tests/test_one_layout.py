@@ -10,8 +10,8 @@ from k8s_llm_monitor_amd import ops
 from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
 
 
-def _pair(monkeypatch):
-    cfg = get_config("llama-tiny-d128")
+def _pair(monkeypatch, model="llama-tiny-d128"):
+    cfg = get_config(model)
     monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
     ref = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=11)
     monkeypatch.setattr(CausalLM, "ONE_LAYOUT", "force")
@@ -19,13 +19,16 @@ def _pair(monkeypatch):
     return ref, one
 
 
-def test_one_layout_single_packed_copy(monkeypatch):
-    ref, one = _pair(monkeypatch)
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_one_layout_single_packed_copy(monkeypatch, model):
+    ref, one = _pair(monkeypatch, model)
     assert one._packed and not ref._packed and one._swg == 8
     for L, L0 in zip(one.layers, ref.layers):
         for key in ("wqkv", "wo", "w13", "w2"):
-            assert L[key].dim() == 4 and L[key] is L[key + "_d"]  # the decode copy IS the weight
-            assert key + "_p" not in L
+            moe = one.cfg.is_moe and key in ("w13", "w2")
+            dk = key + ("_dg" if moe else "_d")
+            assert L[key].dim() == (5 if moe else 4) and L[key] is L[dk]  # the decode copy IS the weight
+            assert key + "_p" not in L and key + "_pg" not in L
             assert torch.equal(one.canonical(L, key), ref.canonical(L0, key))
     assert one.num_local_params() == ref.num_local_params()
     assert one.lm_head is one.lm_head_d and torch.equal(one.canonical_head(), ref.lm_head)
@@ -33,8 +36,9 @@ def test_one_layout_single_packed_copy(monkeypatch):
     assert (one._logits(x) - ref._logits(x)).abs().max().item() < 1e-4
 
 
-def test_one_layout_prefill_and_decode_match_rowmajor(monkeypatch):
-    ref, one = _pair(monkeypatch)
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_one_layout_prefill_and_decode_match_rowmajor(monkeypatch, model):
+    ref, one = _pair(monkeypatch, model)
     bs, nb = 16, 8
     g = torch.Generator().manual_seed(0)
     kv0 = [(torch.randn(nb, ref.hkv, ref.D // 8, bs, 8, generator=g), torch.randn(nb, ref.hkv, ref.D, bs, generator=g))
@@ -63,10 +67,11 @@ def test_one_layout_prefill_and_decode_match_rowmajor(monkeypatch):
     assert (a - b).abs().max().item() < 1e-4
 
 
-def test_one_layout_checkpoint_export_is_rowmajor(monkeypatch):
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_one_layout_checkpoint_export_is_rowmajor(monkeypatch, model):
     from k8s_llm_monitor_amd.models.checkpoint import hf_state_dict
 
-    ref, one = _pair(monkeypatch)
+    ref, one = _pair(monkeypatch, model)
     sd0 = dict(hf_state_dict(ref))
     sd1 = dict(hf_state_dict(one))
     assert sd0.keys() == sd1.keys()
@@ -74,16 +79,17 @@ def test_one_layout_checkpoint_export_is_rowmajor(monkeypatch):
         assert torch.equal(sd0[k], sd1[k]), k
 
 
-def test_one_layout_reinit_restores_rowmajor(monkeypatch):
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_one_layout_reinit_restores_rowmajor(monkeypatch, model):
     """_init_skinny over packed weights (e.g. after a DECODE_GEMM change) starts from the canonical
     tensors again instead of packing the packed copy."""
-    ref, one = _pair(monkeypatch)
+    ref, one = _pair(monkeypatch, model)
     monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
     one._init_skinny()
     assert not one._packed
     for L, L0 in zip(one.layers, ref.layers):
         for key in ("wqkv", "wo", "w13", "w2"):
-            assert L[key].dim() == 2 and torch.equal(L[key], L0[key])
+            assert L[key].dim() == L0[key].dim() and torch.equal(L[key], L0[key])
 
 
 @pytest.mark.gpu
