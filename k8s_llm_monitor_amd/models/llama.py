@@ -943,7 +943,8 @@ class CausalLM:
         (Llama-3-8B: 16 GB of 288); MoE experts while 2W fits 70 % (Mixtral-8x7B at TP=1: 93 + 93
         GB).  Llama-3-70B at TP=1 (141 GB) would get head + attention copies (+24 GB) and keep its
         MLP on the row-major skinny kernel - but dense Llama now runs ONE_LAYOUT: every projection
-        is packed and the packed tensor is the only copy (no extra memory at any size)."""
+        is packed and the packed tensor is the only copy (no extra memory at any size); Mixtral's
+        experts too."""
         mode = self.DECODE_GEMM
         if mode in ("rm", "0", "off") or self.cfg.arch != "llama":
             return set()
@@ -963,8 +964,8 @@ class CausalLM:
         return parts
 
     def _one_layout_wanted(self) -> bool:
-        """ONE_LAYOUT applies: dense Llama whose four projections all have a decode configuration
-        (the shapes are the same in every layer, so layer 0 decides)."""
+        """ONE_LAYOUT applies: a Llama-family model (dense or MoE) whose projections all have a
+        decode configuration (the shapes are the same in every layer, so layer 0 decides)."""
         c = self.cfg
         if not (self.ONE_LAYOUT and c.arch == "llama" and self.layers and self.SKINNY_DECODE
                 and self.DECODE_GEMM not in ("rm", "0", "off")
@@ -1056,9 +1057,10 @@ class CausalLM:
         """Packed copies for the shared-A decode GEMM, per projection where gemm_decode has a
         launch configuration for its shape (ops.dec_config): wqkv_d / wo_d / w2_d
         ([N/16, K/32, 64, 8]), w13_d (gate/up interleaved per 16 rows as [8 gate | 8 up]), and the
-        LM head.  ONE_LAYOUT (dense Llama): the packed copy REPLACES the row-major tensor layer by
-        layer (peak memory = the weights + one layer's copy) and prefill reads it too; otherwise
-        prefill keeps reading the row-major tensors."""
+        LM head; MoE expert stacks w13_dg / w2_dg ([E, ...], grid.z = expert).  ONE_LAYOUT (Llama
+        and Mixtral): the packed copy REPLACES the row-major tensor layer by layer (peak memory =
+        the weights + one layer's copy) and prefill reads it too; otherwise prefill keeps reading
+        the row-major tensors."""
         self.lm_head_d = None
         parts = self._want_dec()
         c = self.cfg
