@@ -30,7 +30,7 @@ def _drive(eng, SamplingParams):
     return [s.output_ids for s in seqs], eng.counters["mixed_steps"]
 
 
-def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce"):
+def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce", one_layout=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), K8SLLM_STEP_BUS=bus, K8SLLM_MOE_DECODE=moe_decode)
     torch.set_num_threads(2)
@@ -38,11 +38,14 @@ def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce"):
     from k8s_llm_monitor_amd.models import AttnMeta, CausalLM, get_config
     from k8s_llm_monitor_amd.parallel.state import ParallelState, destroy, init_parallel
 
+    if one_layout:  # the GPU's single packed weight copy, on the CPU forms of the kernels
+        CausalLM.ONE_LAYOUT = "force"
     try:
         ps = init_parallel(tp_size=world, device="cpu")
         cfg = get_config(model)
         tp_model = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=11, pstate=ps)
         ref_model = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=11, pstate=ParallelState())
+        assert tp_model._packed == bool(one_layout)
         n = 12
         ids = torch.arange(3, 3 + n, dtype=torch.int32)
         meta = AttnMeta(is_prefill=True, positions=torch.arange(n, dtype=torch.int32),
@@ -74,21 +77,26 @@ def _worker(rank, world, port, model, q, bus="shm", moe_decode="allreduce"):
         q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("model,world,bus,moe_decode", [
-    ("llama-tiny", 2, "shm", "allreduce"), ("mixtral-tiny", 2, "shm", "allreduce"),
-    ("gpt2-tiny", 2, "shm", "allreduce"), ("llama-tiny", 2, "gloo", "allreduce"),
+@pytest.mark.parametrize("model,world,bus,moe_decode,one_layout", [
+    ("llama-tiny", 2, "shm", "allreduce", False), ("mixtral-tiny", 2, "shm", "allreduce", False),
+    ("gpt2-tiny", 2, "shm", "allreduce", False), ("llama-tiny", 2, "gloo", "allreduce", False),
     # TP 4 > 2 KV heads: each KV head replicated on 2 ranks
-    ("llama-tiny", 4, "shm", "allreduce"), ("mixtral-tiny", 4, "shm", "allreduce"),
+    ("llama-tiny", 4, "shm", "allreduce", False), ("mixtral-tiny", 4, "shm", "allreduce", False),
     # expert-parallel all-to-all MoE decode (static-capacity dispatch / combine)
-    ("mixtral-tiny", 2, "shm", "a2a"), ("mixtral-tiny", 4, "shm", "a2a"),
+    ("mixtral-tiny", 2, "shm", "a2a", False), ("mixtral-tiny", 4, "shm", "a2a", False),
     # TP 8, the Llama-3-70B deployment degree: one query head per rank, each KV head on 4 ranks;
     # EP 8: one expert per rank
-    ("llama-tiny-d128", 8, "shm", "allreduce"), ("mixtral-tiny-e8", 8, "shm", "a2a")])
-def test_tp_matches_tp1(model, world, bus, moe_decode):
+    ("llama-tiny-d128", 8, "shm", "allreduce", False), ("mixtral-tiny-e8", 8, "shm", "a2a", False),
+    # ONE_LAYOUT (the GPU default): every rank's shard resident once, packed - the row-parallel
+    # tails, the packed grouped prefill and the EP all-to-all decode on the packed experts
+    ("llama-tiny-d128", 2, "shm", "allreduce", True), ("mixtral-tiny-d128", 2, "shm", "allreduce", True),
+    ("mixtral-tiny-d128", 2, "shm", "a2a", True)])
+def test_tp_matches_tp1(model, world, bus, moe_decode, one_layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, bus, moe_decode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, bus, moe_decode, one_layout))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
