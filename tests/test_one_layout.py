@@ -138,20 +138,21 @@ def test_copy_weights_between_layouts(monkeypatch):
         assert torch.equal(La["wo_d"], L0["wo_d"])  # a's decode copies were rebuilt from the new weights
 
 
-def test_checkpoint_roundtrip_into_one_layout(monkeypatch, tmp_path):
+@pytest.mark.parametrize("model", ["llama-tiny-d128", "mixtral-tiny-d128"])
+def test_checkpoint_roundtrip_into_one_layout(monkeypatch, tmp_path, model):
     """A checkpoint saved from the row-major model loads into a ONE_LAYOUT model: the derived
     tensors are dropped before the new ones arrive, the weights are packed again, and the model
     computes what the source does."""
     from k8s_llm_monitor_amd.models.checkpoint import load_checkpoint, save_checkpoint
 
-    ref, one = _pair(monkeypatch)
-    cfg = get_config("llama-tiny-d128")
+    ref, one = _pair(monkeypatch, model)
+    cfg = get_config(model)
     monkeypatch.setattr(CausalLM, "ONE_LAYOUT", False)
     src = CausalLM(cfg, device="cpu", dtype=torch.float32, seed=77)
     save_checkpoint(src, tmp_path)
     monkeypatch.setattr(CausalLM, "ONE_LAYOUT", "force")
     load_checkpoint(one, tmp_path)
-    assert one._packed and one.layers[0]["w13"].dim() == 4 and one.lm_head is one.lm_head_d
+    assert one._packed and one.layers[0]["w13"].dim() == (5 if cfg.is_moe else 4) and one.lm_head is one.lm_head_d
     for L, L0 in zip(one.layers, src.layers):
         for key in ("wqkv", "wo", "w13", "w2"):
             assert torch.equal(one.canonical(L, key), src.canonical(L0, key))
