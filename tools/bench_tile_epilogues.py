@@ -39,6 +39,8 @@ def main() -> None:
     nw = torch.ones(d, device=dev, dtype=torch.bfloat16)
     hw = torch.empty_like(resid)
     ss = torch.empty(T, d // 128, device=dev, dtype=torch.float32)
+    w13p = ops.pack_skinny(ops.interleave_gate_up8(torch.randn(28672, d, device=dev, dtype=torch.bfloat16) * 0.02))
+    out_gu = torch.empty(T, 14336, device=dev, dtype=torch.bfloat16)
     cases = {
         "qkv_plain": (lambda _i: ops.gemm_tile(x, wq, out=out_q, algo=ops.TILE_ALGO), 2 * T * 6144 * d),
         "qkv_rope": (lambda _i: ops.gemm_tile(x, wq, out=out_q, rope=(pos, cs, 40), algo=ops.TILE_ALGO), 2 * T * 6144 * d),
@@ -46,6 +48,9 @@ def main() -> None:
                         2 * T * 6144 * d),
         "o_plain": (lambda _i: ops.gemm_tile(x, wo, out=hw, algo=ops.TILE_ALGO), 2 * T * d * d),
         "o_resid": (lambda _i: ops.gemm_tile_resid(x, wo, resid, nw, hw, ss), 2 * T * d * d),
+        # the engine's gate_up: packed W (one layout), SwiGLU over the per-16 pairing, row-scaled
+        "gu_swiglu8_rs": (lambda _i: ops.gemm_tile(x, w13p, swiglu=8, out=out_gu, rowscale=(ssp, 1e-5),
+                                                   algo=ops.TILE_ALGO), 2 * T * 28672 * d),
     }
     res: dict = {k: [] for k in cases}
     for _ in range(a.rounds):
