@@ -158,3 +158,24 @@ def test_checkpoint_roundtrip_into_one_layout(monkeypatch, tmp_path, model):
             assert torch.equal(one.canonical(L, key), src.canonical(L0, key))
     x = torch.randn(5, cfg.d_model)
     assert (one._logits(x) - src._logits(x)).abs().max().item() < 1e-4
+
+
+def test_moe_grouped_gemm_packed_cpu_path():
+    """ops.moe_grouped_gemm over fragment-packed expert weights (ONE_LAYOUT) equals the row-major
+    form: plain, and SwiGLU over the per-16 gate / up pairing (swiglu=8) vs the per-128 one."""
+    torch.manual_seed(3)
+    E, F, d = 3, 128, 64
+    x = torch.randn(20, d)
+    w13 = torch.randn(E, 2 * F, d) * 0.1  # [gate; up] per expert
+    off = torch.tensor([2, 9, 9, 20], dtype=torch.int32)  # rows 0-1 belong to another rank
+    w_il = torch.stack([ops.interleave_gate_up(w) for w in w13])
+    w_pk = torch.stack([ops.pack_skinny(ops.interleave_gate_up8(w)) for w in w13])
+    a = ops.moe_grouped_gemm(x, w_il, off, swiglu=True)
+    b = ops.moe_grouped_gemm(x, w_pk, off, swiglu=8)
+    assert torch.equal(b[:2], torch.zeros(2, F))
+    torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+    w2 = torch.randn(E, d, F) * 0.1
+    h = torch.randn(20, F)
+    torch.testing.assert_close(ops.moe_grouped_gemm(h, w2, off),
+                               ops.moe_grouped_gemm(h, torch.stack([ops.pack_skinny(w) for w in w2]), off),
+                               atol=1e-5, rtol=1e-5)
