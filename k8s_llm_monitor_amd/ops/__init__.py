@@ -1059,6 +1059,8 @@ def gemm_tile_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, norm_
 # the all-tile routing measured +1.4 % (three interleaved pairs, profiles/r04/bench_pg2_*.json:
 # 25.06 vs 24.71 q/s), with qkv's RoPE fused into the tile epilogue.  "auto" = tile for the fused
 # epilogues only (gate_up + SwiGLU, qkv + RoPE), hipBLASLt for o / down; "blas" = hipBLASLt for all.
+# These routes apply to row-major weights; the ONE_LAYOUT models' fragment-packed weights (every
+# Llama / Mixtral on the GPU) go to the tile kernel at any row count - hipBLASLt cannot read them.
 # These are module constants (tools and tests set them for A/B runs), not environment switches.
 PREFILL_GEMM = "tile"
 QKV_ROPE_TILE = True  # qkv + fused RoPE on the tile kernel
