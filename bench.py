@@ -25,6 +25,10 @@ With ``--path http`` (default) every query is a real ``POST /api/v1/query`` to t
 server, sent by a child load-generator process (``--client process``); ``--path engine`` submits
 to the engine queue directly; ``--path podcomm`` posts /api/v1/analyze/pod-communication.
 
+Weights: one resident copy in the decode kernels' packed layout, read by prefill too (default
+``--layout one``; ``--layout two`` = the round-5 row-major weights + decode copies, for A/B runs);
+the JSON config reports the layout and the resident weight GB per rank.
+
 Timing: W untimed warmup steps, then a barrier + device sync, K timed steps, a device sync +
 barrier; the elapsed time is the MAX over ranks.  ``value`` = total queries answered by all
 replicas / that time.  Weights are random-init (no checkpoints offline), prompts are synthetic.
