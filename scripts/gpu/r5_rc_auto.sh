@@ -13,6 +13,3 @@ timeout -k 10 300 python bench.py --mode latency --steps 5 --warmup 1 --out gpur
 python3 -c "import json;a=json.load(open('gpurun_out/rca_lat.json'));print('lat', a['p50_latency_ms'], a['tpot_ms'])"
 timeout -k 10 400 python bench.py --out gpurun_out/rca_bench.json > gpurun_out/rca_bench.log 2>&1 || { tail -20 gpurun_out/rca_bench.log; exit 1; }
 tail -c 400 gpurun_out/rca_bench.json
-timeout -k 10 300 python -u tools/bench_decode_step.py --switch seam_auto_rc --rows 1,2,4,8 --rounds 2 --tokens 64 \
-  > gpurun_out/rca_seam.jsonl 2> gpurun_out/rca_seam.err || { tail -20 gpurun_out/rca_seam.err; exit 1; }
-grep on_median gpurun_out/rca_seam.jsonl
